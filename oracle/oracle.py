@@ -1,0 +1,276 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes wrapper over the C oracle plus a tiny
+pure-Python restatement used as a second opinion on small inputs.
+
+The oracle is the checker for the product path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import
+this module; the product package ``gocask_amd`` never does.
+
+Reference anchors: core/db.go:110-178 (replay), core/keydir.go:22-53 (keydir),
+core/header.go:9-62 (record header), internal/crc/crc.go:5-10 (CRC-32/IEEE).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import subprocess
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+REC_DTYPE = np.dtype(
+    [
+        ("rec_off", "<u8"),
+        ("file", "<u4"),
+        ("key_len", "<u4"),
+        ("value_pos", "<u4"),
+        ("value_size", "<u4"),
+        ("crc", "<u4"),
+        ("ts", "<u4"),
+        ("flags", "<u4"),
+        ("crc_calc", "<u4"),
+    ]
+)
+F_TOMBSTONE = 1
+F_CRC_OK = 2
+OK, EUNEXPECTED_EOF = 0, 1
+
+
+class OrcFile(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("reset_after", ctypes.c_uint8)]
+
+
+class OrcStatus(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32),
+        ("err_file", ctypes.c_uint32),
+        ("err_off", ctypes.c_uint64),
+        ("n_recs", ctypes.c_uint64),
+        ("final_last_offset", ctypes.c_uint32),
+        ("files_walked", ctypes.c_uint32),
+    ]
+
+
+class CorpusCfg(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("max_file_size", ctypes.c_uint64),
+        ("n_ops", ctypes.c_uint64),
+        ("n_files", ctypes.c_uint32),
+        ("key_min", ctypes.c_uint32),
+        ("key_max", ctypes.c_uint32),
+        ("key_universe", ctypes.c_uint64),
+        ("val_fixed", ctypes.c_uint32),
+        ("tomb_permille", ctypes.c_uint32),
+        ("flip_permille", ctypes.c_uint32),
+        ("ts_base", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_crc32.restype = ctypes.c_uint32
+        L.orc_crc32.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_crc32_fast.restype = ctypes.c_uint32
+        L.orc_crc32_fast.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_replay.restype = ctypes.c_int
+        L.orc_replay.argtypes = [ctypes.POINTER(OrcFile), ctypes.c_uint32, ctypes.c_int,
+                                 ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(OrcStatus)]
+        L.orc_keydir.restype = ctypes.c_uint64
+        L.orc_keydir.argtypes = [ctypes.POINTER(OrcFile), ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.orc_baseline.restype = ctypes.c_uint64
+        L.orc_baseline.argtypes = [ctypes.POINTER(OrcFile), ctypes.c_uint32, ctypes.c_int,
+                                   ctypes.POINTER(OrcStatus)]
+        L.orc_gen_sizes.restype = ctypes.c_int
+        L.orc_gen_sizes.argtypes = [ctypes.POINTER(CorpusCfg), ctypes.POINTER(ctypes.c_uint64),
+                                    ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_gen_fill.restype = ctypes.c_int
+        L.orc_gen_fill.argtypes = [ctypes.POINTER(CorpusCfg), ctypes.c_void_p, ctypes.c_uint32]
+        L.orc_zipf_table.restype = None
+        L.orc_zipf_table.argtypes = [ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _as_u8(b) -> np.ndarray:
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8)
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+def _files_struct(files, reset_after):
+    arrs = [_as_u8(f) for f in files]
+    fa = (OrcFile * max(1, len(arrs)))()
+    for i, a in enumerate(arrs):
+        fa[i].data = a.ctypes.data if a.size else 0
+        fa[i].len = a.size
+        fa[i].reset_after = 1 if reset_after[i] else 0
+    return fa, arrs
+
+
+def crc32(b) -> int:
+    a = _as_u8(b)
+    return lib().orc_crc32(a.ctypes.data if a.size else 0, a.size)
+
+
+def replay(files, reset_after=None, verify_crc=True):
+    """Replay files (walk order).  Returns (records ndarray[REC_DTYPE], status dict)."""
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    st = OrcStatus()
+    L = lib()
+    L.orc_replay(fa, len(arrs), 1 if verify_crc else 0, None, 0, ctypes.byref(st))
+    n = st.n_recs
+    out = np.zeros(max(1, n), dtype=REC_DTYPE)
+    L.orc_replay(fa, len(arrs), 1 if verify_crc else 0, out.ctypes.data, n, ctypes.byref(st))
+    status = dict(status=st.status, err_file=st.err_file, err_off=st.err_off, n_recs=st.n_recs,
+                  final_last_offset=st.final_last_offset, files_walked=st.files_walked)
+    return out[:n], status
+
+
+def keydir(files, recs, reset_after=None):
+    """Live keydir as {key bytes: record row} after last-writer-wins."""
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    recs = np.ascontiguousarray(recs, dtype=REC_DTYPE)
+    live = np.zeros(max(1, len(recs)), dtype=np.uint64)
+    k = lib().orc_keydir(fa, recs.ctypes.data, len(recs), live.ctypes.data)
+    out = {}
+    for idx in live[:k]:
+        r = recs[int(idx)]
+        key = bytes(arrs[int(r["file"])][int(r["rec_off"]) + 16: int(r["rec_off"]) + 16 + int(r["key_len"])])
+        out[key] = r
+    return out
+
+
+def baseline(files, reset_after=None, verify_crc=True):
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    st = OrcStatus()
+    live = lib().orc_baseline(fa, len(arrs), 1 if verify_crc else 0, ctypes.byref(st))
+    return live, dict(status=st.status, n_recs=st.n_recs, crc_rejects=st.err_off,
+                      final_last_offset=st.final_last_offset)
+
+
+def zipf_table() -> np.ndarray:
+    t = np.zeros(65472, dtype=np.uint32)
+    lib().orc_zipf_table(t.ctypes.data)
+    return t
+
+
+def corpus_cfg(**kw) -> CorpusCfg:
+    c = CorpusCfg()
+    defaults = dict(seed=1, max_file_size=64 << 20, n_ops=0, n_files=1, key_min=16, key_max=16,
+                    key_universe=0, val_fixed=1024, tomb_permille=0, flip_permille=0,
+                    ts_base=1700000000)
+    defaults.update(kw)
+    for k, v in defaults.items():
+        setattr(c, k, v)
+    return c
+
+
+def gen_corpus(**kw):
+    """Generate the synthetic corpus on the CPU.  Returns (files in creation
+    order as numpy uint8 arrays, names)."""
+    c = corpus_cfg(**kw)
+    L = lib()
+    n_ops = ctypes.c_uint64()
+    nf = ctypes.c_uint32()
+    cap = 1 << 16
+    sizes = np.zeros(cap, dtype=np.uint64)
+    rc = L.orc_gen_sizes(ctypes.byref(c), ctypes.byref(n_ops), sizes.ctypes.data, cap, ctypes.byref(nf))
+    if rc != 0:
+        raise ValueError(f"orc_gen_sizes failed: {rc}")
+    files = [np.zeros(int(sizes[i]), dtype=np.uint8) for i in range(nf.value)]
+    ptrs = (ctypes.c_void_p * nf.value)(*[f.ctypes.data for f in files])
+    rc = L.orc_gen_fill(ctypes.byref(c), ptrs, nf.value)
+    if rc != 0:
+        raise ValueError(f"orc_gen_fill failed: {rc}")
+    names = [f"data_{n}_{c.ts_base + n}" for n in range(nf.value)]
+    return files, names
+
+
+# ---------------------------------------------------------------------------
+# Pure-Python second opinion (small inputs only).  Same restatement as the C
+# code, written independently; uses zlib.crc32 (CRC-32/ISO-HDLC == Go IEEE).
+# ---------------------------------------------------------------------------
+def replay_py(files, reset_after=None):
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    last = 0
+    recs = []
+    status = dict(status=OK, err_file=0, err_off=0)
+    for f, d in enumerate(files):
+        d = bytes(d)
+        p = 0
+        n = len(d)
+        err = False
+        while True:
+            if n - p == 0:
+                break
+            if n - p < 16:
+                status = dict(status=EUNEXPECTED_EOF, err_file=f, err_off=p)
+                err = True
+                break
+            rec = p
+            hcrc, ts, ks, vs = struct.unpack_from("<IIII", d, p)
+            p += 16
+            tomb = ks == 0
+            klen = vs if tomb else ks
+            if klen > 0 and n - p == 0:
+                break
+            if n - p < klen:
+                status = dict(status=EUNEXPECTED_EOF, err_file=f, err_off=rec)
+                err = True
+                break
+            key = d[p:p + klen]
+            p += klen
+            if not tomb:
+                if n - p < vs:
+                    break
+                p += vs
+            val = d[p - vs:p]
+            calc = zlib.crc32(val)
+            recs.append(dict(rec_off=rec, file=f, key=key, key_len=klen,
+                             value_pos=(last + 16 + ks) & 0xFFFFFFFF, value_size=vs, crc=hcrc,
+                             ts=ts, tomb=tomb, crc_calc=calc, crc_ok=calc == hcrc))
+            last = (last + 16 + klen) & 0xFFFFFFFF if tomb else (last + 16 + ks + vs) & 0xFFFFFFFF
+        if err:
+            break
+        if reset_after[f]:
+            last = 0
+    kd = {}
+    for r in recs:
+        if r["tomb"]:
+            kd.pop(r["key"], None)
+        else:
+            kd[r["key"]] = r
+    return recs, kd, status, last
+
+
+def entry(now: int, key: bytes, val: bytes) -> bytes:
+    """core/testutil/utils.go:10-19 — canonical record encoder."""
+    return struct.pack("<IIII", zlib.crc32(val), now & 0xFFFFFFFF, len(key), len(val)) + key + val
+
+
+def tombstone(now: int, key: bytes) -> bytes:
+    """core/db.go:245-247 — Delete writes header{CRC(key), t, 0, len(key)} || key."""
+    return struct.pack("<IIII", zlib.crc32(key), now & 0xFFFFFFFF, 0, len(key)) + key
