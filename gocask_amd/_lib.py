@@ -1,0 +1,184 @@
+"""ctypes binding of libgocask_hip.so (include/gocask_hip.h).
+
+This is the Python equivalent of the cgo stub a Go maintainer would add
+(INTEGRATION.md).  It loads the in-tree library and fails loudly when it is
+missing: there is no CPU fallback for the replay path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgocask_hip.so")
+
+GCK_OK = 0
+GCK_EUNEXPECTED_EOF = 1
+GCK_EDEVICE = 2
+GCK_EINVAL = 3
+GCK_ENOMEM = 4
+GCK_EIO = 5
+GCK_EKEY_NOT_FOUND = 6
+GCK_ECRC_FAILED = 7
+GCK_EINVALID_KEY = 8
+GCK_ENOT_DIR = 9
+
+F_TOMBSTONE = 1
+F_CRC_OK = 2
+
+REC_DTYPE = np.dtype(
+    [
+        ("rec_off", "<u8"),
+        ("file", "<u4"),
+        ("key_len", "<u4"),
+        ("value_pos", "<u4"),
+        ("value_size", "<u4"),
+        ("crc", "<u4"),
+        ("ts", "<u4"),
+        ("flags", "<u4"),
+        ("crc_calc", "<u4"),
+    ]
+)
+assert REC_DTYPE.itemsize == 40
+
+# Every symbol include/gocask_hip.h declares (tests check the .so exports them).
+EXPORTED = [
+    "gck_replay", "gck_result_free", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
+    "gck_ctx_fetch", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
+    "gck_ctx_read_file", "gck_encode_corpus", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_db_open",
+    "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
+    "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count",
+    "gck_version", "gck_last_error",
+]
+
+
+class GckFile(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("reset_after", ctypes.c_uint8)]
+
+
+class GckOpts(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("chunk_bytes", ctypes.c_uint32),
+        ("max_key", ctypes.c_uint32),
+        ("chunk_cap", ctypes.c_uint32),
+        ("flags", ctypes.c_uint32),
+    ]
+
+
+class GckResult(ctypes.Structure):
+    _fields_ = [
+        ("recs", ctypes.c_void_p),
+        ("n", ctypes.c_uint64),
+        ("n_crc_fail", ctypes.c_uint64),
+        ("final_last_offset", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("err_file", ctypes.c_uint32),
+        ("files_walked", ctypes.c_uint32),
+        ("err_off", ctypes.c_uint64),
+    ]
+
+
+class GckStats(ctypes.Structure):
+    _fields_ = [
+        ("bytes", ctypes.c_uint64),
+        ("n_recs", ctypes.c_uint64),
+        ("n_crc_fail", ctypes.c_uint64),
+        ("n_chunks", ctypes.c_uint64),
+        ("n_fixups", ctypes.c_uint64),
+        ("n_overflow", ctypes.c_uint64),
+        ("ms_total", ctypes.c_double),
+        ("ms_kernel", ctypes.c_double * 12),
+    ]
+
+
+class GckCorpusCfg(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("max_file_size", ctypes.c_uint64),
+        ("n_ops", ctypes.c_uint64),
+        ("n_files", ctypes.c_uint32),
+        ("key_min", ctypes.c_uint32),
+        ("key_max", ctypes.c_uint32),
+        ("key_universe", ctypes.c_uint64),
+        ("val_fixed", ctypes.c_uint32),
+        ("tomb_permille", ctypes.c_uint32),
+        ("flip_permille", ctypes.c_uint32),
+        ("ts_base", ctypes.c_uint32),
+    ]
+
+
+class GckConfig(ctypes.Structure):
+    _fields_ = [("max_data_file_size", ctypes.c_int64), ("data_dir", ctypes.c_char_p)]
+
+
+_lib = None
+
+
+def load():
+    """Load the in-tree HIP library.  Raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    sig = {
+        "gck_replay": (ctypes.c_int, [P(GckFile), ctypes.c_uint32, P(GckOpts), P(GckResult)]),
+        "gck_result_free": (None, [P(GckResult)]),
+        "gck_ctx_create": (ctypes.c_int, [P(GckOpts), P(vp)]),
+        "gck_ctx_destroy": (None, [vp]),
+        "gck_ctx_load": (ctypes.c_int, [vp, P(GckFile), ctypes.c_uint32]),
+        "gck_ctx_run": (ctypes.c_int, [vp]),
+        "gck_ctx_fetch": (ctypes.c_int, [vp, P(GckResult)]),
+        "gck_ctx_stats": (ctypes.c_int, [vp, P(GckStats)]),
+        "gck_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
+        "gck_ctx_device_recs": (ctypes.c_int, [vp, P(vp), P(ctypes.c_uint64)]),
+        "gck_ctx_stream": (vp, [vp]),
+        "gck_ctx_read_file": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint64, vp, ctypes.c_uint64]),
+        "gck_encode_corpus": (ctypes.c_int, [vp, P(GckCorpusCfg), P(ctypes.c_uint32), P(ctypes.c_uint64), vp,
+                                             ctypes.c_uint32]),
+        "gck_encode_walk_order": (ctypes.c_int, [vp, vp, ctypes.c_uint32]),
+        "gck_encode_zipf_table": (None, [vp]),
+        "gck_db_open": (ctypes.c_int, [ctypes.c_char_p, P(GckConfig), P(GckOpts), P(vp), ctypes.c_char_p,
+                                       ctypes.c_size_t]),
+        "gck_db_open_mem": (ctypes.c_int, [vp, ctypes.c_uint64, P(GckOpts), P(vp), ctypes.c_char_p,
+                                           ctypes.c_size_t]),
+        "gck_db_get": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_uint32, P(vp), P(ctypes.c_uint64)]),
+        "gck_db_keys": (ctypes.c_uint64, [vp]),
+        "gck_db_key": (ctypes.c_int, [vp, ctypes.c_uint64, P(vp), P(ctypes.c_uint32)]),
+        "gck_db_entry": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_uint32, P(ctypes.c_uint32),
+                                        P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32),
+                                        P(ctypes.c_char_p)]),
+        "gck_db_last_offset": (ctypes.c_uint32, [vp]),
+        "gck_db_active_file": (ctypes.c_char_p, [vp]),
+        "gck_db_nfiles": (ctypes.c_uint32, [vp]),
+        "gck_db_file_name": (ctypes.c_char_p, [vp, ctypes.c_uint32]),
+        "gck_db_close": (None, [vp]),
+        "gck_device_count": (ctypes.c_int, []),
+        "gck_version": (ctypes.c_char_p, []),
+        "gck_last_error": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class GckError(RuntimeError):
+    def __init__(self, code, msg=""):
+        self.code = code
+        super().__init__(f"gocask_hip error {code}: {msg}")
+
+
+def check(rc, allowed=(GCK_OK,)):
+    if rc not in allowed:
+        L = load()
+        raise GckError(rc, (L.gck_last_error() or b"").decode())
+    return rc

@@ -1,0 +1,336 @@
+"""Python mirror of the reference surface around cold-start replay.
+
+Names, argument meaning and error behaviour follow the Go reference so tests
+read like its own: ``NewDB`` (core/db.go:90-108) and ``Open`` (db.go:29-59)
+return ``(db, err)``; ``DB.Get`` returns ``(value, err)`` with ``ErrKeyNotFound``
+/ ``ErrCRCFailed`` / ``ErrInvalidKey`` (core/db.go:13-31); ``DB.Keys``
+(core/db.go:318-324).  Everything below the ctypes calls is native: the C++
+host mirror in gocask_amd/csrc/db.cpp and the HIP pipeline in replay.hip.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import (F_CRC_OK, F_TOMBSTONE, GCK_ECRC_FAILED, GCK_EINVALID_KEY, GCK_EKEY_NOT_FOUND, GCK_OK,
+                   GCK_EUNEXPECTED_EOF, REC_DTYPE, GckCorpusCfg, GckFile, GckOpts, GckResult, GckStats, check)
+
+InMemoryDB = "in:mem:db"  # core/db.go:32-34
+
+KB = 1024
+MB = KB * 1024
+GB = MB * 1024
+TB = GB * 1024
+
+
+class GoCaskError(Exception):
+    pass
+
+
+ErrKeyNotFound = GoCaskError("gocask: key not found")
+ErrPartialWrite = GoCaskError("gocask: key/value pair not fully written")
+ErrCRCFailed = GoCaskError("gocask: crc check failed for db entry (value is corrupted)")
+ErrInvalidKey = GoCaskError("gocask: key should not be empty or nil")
+ErrInvalidValue = GoCaskError("gocask: value should not be nil")
+ErrUnexpectedEOF = GoCaskError("unexpected EOF")
+
+
+class StartupError(GoCaskError):
+    """fmt.Errorf("gocask: startup error: %w", err) (core/db.go:138)."""
+
+    def __init__(self, wrapped=ErrUnexpectedEOF):
+        super().__init__(f"gocask: startup error: {wrapped}")
+        self.wrapped = wrapped
+
+    def is_(self, err):
+        return err is self.wrapped or err is self
+
+
+@dataclass
+class Config:  # core.Config (core/db.go:84-87)
+    MaxDataFileSize: int = 2 * GB
+    DataDir: str = "./"
+
+
+DefaultConfig = Config()  # core/db.go:78-81
+
+
+class Disk:
+    """Marker for fs.NewDisk() (internal/fs/disk.go:42-48)."""
+
+
+class InMemory:
+    """fs.NewInMemory(): one file "data" that is also the active file
+    (internal/fs/memory.go:38-80).  ``data`` holds the bytes written so far."""
+
+    def __init__(self, data: bytes = b""):
+        self.data = bytes(data)
+
+
+def NewDisk():
+    return Disk()
+
+
+def NewInMemory(data: bytes = b""):
+    return InMemory(data)
+
+
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+    o = GckOpts()
+    o.device = device
+    o.chunk_bytes = chunk_bytes
+    o.max_key = max_key
+    o.chunk_cap = chunk_cap
+    return o
+
+
+class DB:
+    """core.DB restricted to the replayed state: keydir, Get, Keys, Close."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self._L = _lib.load()
+
+    def Get(self, key: bytes):
+        if key is None:
+            key = b""
+        val = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        rc = self._L.gck_db_get(self._h, key, len(key), ctypes.byref(val), ctypes.byref(n))
+        if rc == GCK_OK:
+            return ctypes.string_at(val, n.value) if n.value else b"", None
+        err = {GCK_EKEY_NOT_FOUND: ErrKeyNotFound, GCK_ECRC_FAILED: ErrCRCFailed,
+               GCK_EINVALID_KEY: ErrInvalidKey}.get(rc)
+        if err is None:
+            err = GoCaskError(f"gocask: read failed ({rc})")
+        return None, err
+
+    def Keys(self):
+        n = self._L.gck_db_keys(self._h)
+        out = []
+        k = ctypes.c_void_p()
+        kl = ctypes.c_uint32()
+        for i in range(n):
+            check(self._L.gck_db_key(self._h, i, ctypes.byref(k), ctypes.byref(kl)))
+            out.append(ctypes.string_at(k, kl.value).decode("utf-8", "surrogateescape"))
+        return out
+
+    def Entry(self, key: bytes):
+        """The kdEntry for key (core/keydir.go:3-9) or None."""
+        crc, ts, pos, size = (ctypes.c_uint32() for _ in range(4))
+        f = ctypes.c_char_p()
+        rc = self._L.gck_db_entry(self._h, key, len(key), ctypes.byref(crc), ctypes.byref(ts), ctypes.byref(pos),
+                                  ctypes.byref(size), ctypes.byref(f))
+        if rc != GCK_OK:
+            return None
+        return dict(CRC=crc.value, Timestamp=ts.value, ValuePos=pos.value, ValueSize=size.value,
+                    File=f.value.decode())
+
+    @property
+    def last_offset(self):
+        return self._L.gck_db_last_offset(self._h)
+
+    @property
+    def active_file(self):
+        return self._L.gck_db_active_file(self._h).decode()
+
+    def files(self):
+        return [self._L.gck_db_file_name(self._h, i).decode() for i in range(self._L.gck_db_nfiles(self._h))]
+
+    def Close(self):
+        if self._h:
+            self._L.gck_db_close(self._h)
+            self._h = None
+        return None
+
+    def __del__(self):
+        try:
+            self.Close()
+        except Exception:
+            pass
+
+
+def NewDB(dbpath: str, fs, time=None, cfg: Config = DefaultConfig, device: int = 0):
+    """core.NewDB: returns (db, err).  On a startup error the DB is still
+    returned with the partially replayed keydir, as the reference does."""
+    L = _lib.load()
+    h = ctypes.c_void_p()
+    err = ctypes.create_string_buffer(256)
+    if isinstance(fs, InMemory):
+        buf = np.frombuffer(fs.data, dtype=np.uint8) if fs.data else np.zeros(1, np.uint8)
+        rc = L.gck_db_open_mem(buf.ctypes.data, len(fs.data), ctypes.byref(_opts(device)), ctypes.byref(h), err, 256)
+    else:
+        c = _lib.GckConfig()
+        c.max_data_file_size = cfg.MaxDataFileSize
+        c.data_dir = cfg.DataDir.encode()
+        rc = L.gck_db_open(dbpath.encode(), ctypes.byref(c), ctypes.byref(_opts(device)), ctypes.byref(h), err, 256)
+    if rc == GCK_OK:
+        return DB(h), None
+    if rc == GCK_EUNEXPECTED_EOF:
+        return DB(h), StartupError()
+    check(rc)
+
+
+def WithMaxDataFileSize(n: int):  # db.go:63-73
+    def opt(c: Config) -> Config:
+        return Config(n, c.DataDir)
+    return opt
+
+
+def WithDataDir(path: str):  # db.go:75-82
+    def opt(c: Config) -> Config:
+        return Config(c.MaxDataFileSize, path)
+    return opt
+
+
+def Open(dbPath: str, *opts, device: int = 0):
+    """gocask.Open: Disk FS unless dbPath == InMemoryDB; defaults 10 GiB files
+    under ~/gcdata (db.go:29-59).  Returns (db, err); db is None on error."""
+    cfg = Config(10 * GB, os.path.join(os.path.expanduser("~"), "gcdata"))
+    for o in opts:
+        cfg = o(cfg)
+    fs = NewInMemory() if dbPath == InMemoryDB else NewDisk()
+    db, err = NewDB(dbPath, fs, None, cfg, device=device)
+    if err is not None:
+        return None, err
+    return db, None
+
+
+# ---------------------------------------------------------------- replay API
+def _files_struct(files, reset_after):
+    arrs = [np.ascontiguousarray(np.frombuffer(f, np.uint8) if isinstance(f, (bytes, bytearray)) else f,
+                                 dtype=np.uint8) for f in files]
+    fa = (GckFile * max(1, len(arrs)))()
+    for i, a in enumerate(arrs):
+        fa[i].data = a.ctypes.data if a.size else None
+        fa[i].len = a.size
+        fa[i].reset_after = 1 if reset_after[i] else 0
+    return fa, arrs
+
+
+def _result(res: GckResult):
+    n = res.n
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    if n:
+        ctypes.memmove(recs.ctypes.data, res.recs, n * REC_DTYPE.itemsize)
+    return recs, dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=n,
+                      n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset,
+                      files_walked=res.files_walked)
+
+
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+    """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    res = GckResult()
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)), ctypes.byref(res))
+    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+    try:
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
+def keydir(files, recs):
+    """Apply the tuples in walk order (core/keydir.go:22-49): {key: record row}."""
+    kd = {}
+    for r in recs:
+        f = files[int(r["file"])]
+        o = int(r["rec_off"]) + 16
+        key = bytes(f[o:o + int(r["key_len"])])
+        if int(r["flags"]) & F_TOMBSTONE:
+            kd.pop(key, None)
+        else:
+            kd[key] = r
+    return kd
+
+
+class ReplayContext:
+    """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
+
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+        self._L = _lib.load()
+        self._h = ctypes.c_void_p()
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
+                                     ctypes.byref(self._h)))
+
+    def load(self, files, reset_after=None):
+        if reset_after is None:
+            reset_after = [True] * len(files)
+        fa, arrs = _files_struct(files, reset_after)
+        check(self._L.gck_ctx_load(self._h, fa, len(arrs)))
+
+    def encode(self, **kw):
+        """Encode a synthetic corpus on the device (gck_encode_corpus)."""
+        c = GckCorpusCfg()
+        d = dict(seed=1, max_file_size=64 * MB, n_ops=0, n_files=1, key_min=16, key_max=16, key_universe=0,
+                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000)
+        d.update(kw)
+        for k, v in d.items():
+            setattr(c, k, v)
+        nf = ctypes.c_uint32()
+        nops = ctypes.c_uint64()
+        sizes = np.zeros(1 << 16, dtype=np.uint64)
+        check(self._L.gck_encode_corpus(self._h, ctypes.byref(c), ctypes.byref(nf), ctypes.byref(nops),
+                                        sizes.ctypes.data, sizes.size))
+        order = np.zeros(nf.value, dtype=np.uint32)
+        self._L.gck_encode_walk_order(self._h, order.ctypes.data, nf.value)
+        return dict(n_files=nf.value, n_ops=nops.value, sizes=sizes[:nf.value].copy(), walk_order=order)
+
+    def run(self):
+        return check(self._L.gck_ctx_run(self._h), (GCK_OK, GCK_EUNEXPECTED_EOF))
+
+    def fetch(self):
+        res = GckResult()
+        check(self._L.gck_ctx_fetch(self._h, ctypes.byref(res)))
+        try:
+            return _result(res)
+        finally:
+            self._L.gck_result_free(ctypes.byref(res))
+
+    def stats(self):
+        s = GckStats()
+        check(self._L.gck_ctx_stats(self._h, ctypes.byref(s)))
+        phases = {self._L.gck_phase_name(i).decode(): s.ms_kernel[i] for i in range(9)}
+        return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
+                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases)
+
+    def read_file(self, file, off=0, length=None):
+        n = length
+        buf = np.zeros(n, dtype=np.uint8)
+        if n:
+            check(self._L.gck_ctx_read_file(self._h, file, off, buf.ctypes.data, n))
+        return buf
+
+    def close(self):
+        if self._h:
+            self._L.gck_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def zipf_table():
+    t = np.zeros(65472, dtype=np.uint32)
+    _lib.load().gck_encode_zipf_table(t.ctypes.data)
+    return t
+
+
+def device_count():
+    return _lib.load().gck_device_count()

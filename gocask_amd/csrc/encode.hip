@@ -1,0 +1,217 @@
+// encode.hip — device record encoder for bulk corpus builds.
+//
+// Writes records byte-for-byte as the reference's write path does:
+//   Put:    header{CRC32(val), t, len(key), len(val)} || key || val
+//           (core/db.go:185-212, serializeEntry core/db.go:272-284,
+//            newKVHeader core/header.go:18-28, encode core/header.go:38-48)
+//   Delete: header{CRC32(key), t, 0, len(key)} || key      (core/db.go:245-247)
+//   Rotate: new file when size + entrySize > MaxDataFileSize (core/db.go:214-232),
+//           named data_<n>_<unix>.csk (internal/fs/disk.go:71-82).
+// The op stream is the synthetic corpus spec of DESIGN.md "Corpus"; the host
+// plans offsets (a sequential rotation rule), the device writes the bytes and
+// computes each CRC.  tests/ cross-check it against the oracle's CPU generator.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "gck_internal.h"
+
+namespace gck {
+
+constexpr uint32_t kZipfN = 65473;
+
+static std::vector<uint32_t> &zipf_thr() {
+    static std::vector<uint32_t> thr;
+    if (thr.empty()) {
+        std::vector<double> cum(kZipfN);
+        double acc = 0.0;
+        for (uint32_t r = 1; r <= kZipfN; ++r) {
+            acc += std::pow((double)r, -1.1);
+            cum[r - 1] = acc;
+        }
+        thr.resize(kZipfN - 1);
+        for (uint32_t k = 0; k + 1 < kZipfN; ++k) {
+            const double v = std::floor(cum[k] / acc * 4294967296.0);
+            thr[k] = v >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)v;
+        }
+    }
+    return thr;
+}
+
+static uint32_t zipf_sample(const std::vector<uint32_t> &thr, uint32_t u) {
+    // r = 1 + #{k : thr[k] <= u}
+    return 1u + (uint32_t)(std::upper_bound(thr.begin(), thr.end(), u) - thr.begin());
+}
+
+struct OpDesc {
+    uint64_t dst;    // arena offset of the record
+    uint64_t keyid;
+    uint32_t vlen;
+    uint32_t klen;   // bit 31: tombstone
+};
+
+// One lane per op: key, value (generated, CRC'd on the fly, optionally one bit
+// flipped after the CRC), then the header.
+__global__ __launch_bounds__(256) void k_encode(uint8_t *__restrict__ arena, const OpDesc *__restrict__ ops,
+                                                uint64_t n_ops, uint64_t seed, uint32_t ts_base,
+                                                uint32_t flip_permille) {
+    __shared__ uint32_t T[256];
+    for (uint32_t n = threadIdx.x; n < 256; n += blockDim.x) {
+        uint32_t c = n;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+        T[n] = c;
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_ops) return;
+    const OpDesc o = ops[i];
+    const bool tomb = (o.klen >> 31) != 0;
+    const uint32_t klen = o.klen & 0x7FFFFFFFu, vlen = o.vlen;
+    uint8_t *p = arena + o.dst;
+    uint8_t *key = p + 16;
+    const uint64_t w0 = mix64(o.keyid ^ H(seed, 7, 0));
+    uint32_t kc = 0xFFFFFFFFu;
+    for (uint32_t j = 0; j < klen; ++j) {
+        const uint64_t w = j < 8 ? w0 : H(seed, 8, o.keyid * 64 + j / 8);
+        const uint8_t b = (uint8_t)(w >> (8 * (j % 8)));
+        key[j] = b;
+        kc = T[(kc ^ b) & 0xff] ^ (kc >> 8);
+    }
+    uint32_t crc, ks;
+    if (tomb) {
+        crc = ~kc;
+        ks = 0;
+    } else {
+        uint8_t *v = key + klen;
+        uint64_t flip_byte = ~0ull;
+        uint8_t flip_mask = 0;
+        if (flip_permille && vlen && (H(seed, 4, i) % 1000u) < flip_permille) {
+            const uint64_t bit = H(seed, 9, i) % (8ull * vlen);
+            flip_byte = bit / 8;
+            flip_mask = (uint8_t)(1u << (bit % 8));
+        }
+        uint32_t c = 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < vlen; j += 8) {
+            const uint64_t w = H(seed, 5, (i << 20) | (j / 8));
+            const uint32_t nb = vlen - j < 8 ? vlen - j : 8;
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint8_t x = (uint8_t)(w >> (8 * b));
+                c = T[(c ^ x) & 0xff] ^ (c >> 8);
+                v[j + b] = (j + b == flip_byte) ? (uint8_t)(x ^ flip_mask) : x;
+            }
+        }
+        crc = ~c;
+        ks = klen;
+    }
+    const uint32_t ts = ts_base + (uint32_t)i;
+    const uint32_t hv[4] = {crc, ts, ks, vlen};
+    for (int k = 0; k < 16; ++k) p[k] = (uint8_t)(hv[k / 4] >> (8 * (k % 4)));
+}
+
+// Host plan: op sizes from the spec, greedy rotation, lexical walk order.
+static int plan(const gck_corpus_cfg *cfg, std::vector<OpDesc> &ops, std::vector<uint32_t> &op_file,
+                std::vector<uint64_t> &sizes) {
+    if (cfg->key_min < 8 || cfg->key_max > 512 || cfg->key_max < cfg->key_min) return GCK_EINVAL;
+    if (!cfg->n_ops && !cfg->n_files) return GCK_EINVAL;
+    if (!cfg->val_fixed && cfg->max_file_size == 0) return GCK_EINVAL;
+    if (cfg->val_fixed >= (1u << 23)) return GCK_EINVAL;
+    const auto &thr = zipf_thr();
+    uint32_t cur = 0;
+    uint64_t size = 0;
+    sizes.clear();
+    for (uint64_t i = 0;; ++i) {
+        if (cfg->n_ops && i >= cfg->n_ops) break;
+        const bool tomb = cfg->tomb_permille && (H(cfg->seed, 3, i) % 1000u) < cfg->tomb_permille;
+        const uint64_t keyid = cfg->key_universe ? H(cfg->seed, 1, i) % cfg->key_universe : i;
+        const uint32_t klen =
+            cfg->key_min +
+            (cfg->key_max > cfg->key_min ? (uint32_t)(H(cfg->seed, 6, keyid) % (cfg->key_max - cfg->key_min + 1)) : 0);
+        const uint32_t vlen =
+            tomb ? klen : (cfg->val_fixed ? cfg->val_fixed : 63u + zipf_sample(thr, (uint32_t)(H(cfg->seed, 2, i) >> 32)));
+        const uint64_t entry = 16ull + (tomb ? 0 : klen) + vlen;
+        if (size + entry > cfg->max_file_size) {  // rotateDataFile (core/db.go:214-232)
+            if (cfg->n_files && cur + 1 >= cfg->n_files) break;
+            sizes.push_back(size);
+            ++cur;
+            size = 0;
+        }
+        OpDesc o;
+        o.dst = size;  // file-relative for now
+        o.keyid = keyid;
+        o.vlen = vlen;
+        o.klen = klen | (tomb ? 0x80000000u : 0u);
+        ops.push_back(o);
+        op_file.push_back(cur);
+        size += entry;
+    }
+    sizes.push_back(size);
+    return GCK_OK;
+}
+
+}  // namespace gck
+
+using namespace gck;
+
+extern "C" {
+
+void gck_encode_zipf_table(uint32_t *thr) {
+    const auto &t = zipf_thr();
+    memcpy(thr, t.data(), t.size() * 4);
+}
+
+int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files_out, uint64_t *n_ops_out,
+                      uint64_t *file_sizes, uint32_t max_files) {
+    if (!ctx || !cfg) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    std::vector<OpDesc> ops;
+    std::vector<uint32_t> op_file;
+    std::vector<uint64_t> sizes;
+    int rc = plan(cfg, ops, op_file, sizes);
+    if (rc) return rc;
+    const uint32_t nf = (uint32_t)sizes.size();
+    // walk order = names sorted bytewise (filepath.Walk)
+    std::vector<std::string> names(nf);
+    for (uint32_t n = 0; n < nf; ++n)
+        names[n] = "data_" + std::to_string(n) + "_" + std::to_string((uint32_t)(cfg->ts_base + n)) + ".csk";
+    std::vector<uint32_t> order(nf);
+    for (uint32_t n = 0; n < nf; ++n) order[n] = n;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return names[a] < names[b]; });
+    std::vector<uint32_t> walkpos(nf);
+    for (uint32_t w = 0; w < nf; ++w) walkpos[order[w]] = w;
+    std::vector<uint64_t> lens(nf);
+    std::vector<uint8_t> reset(nf);
+    for (uint32_t w = 0; w < nf; ++w) {
+        lens[w] = sizes[order[w]];
+        reset[w] = w + 1 < nf ? 1 : 0;  // the active file is the lexically last entry
+    }
+    rc = ctx_layout(c, lens.data(), nf, reset.data());
+    if (rc) return rc;
+    c->walk_to_creation = order;
+    for (size_t i = 0; i < ops.size(); ++i) ops[i].dst += c->f_base[walkpos[op_file[i]]];
+    DBuf d_ops;
+    if ((rc = d_ops.ensure(ops.size() * sizeof(OpDesc) + 16))) return rc;
+    GCK_HIP(hipMemcpy(d_ops.p, ops.data(), ops.size() * sizeof(OpDesc), hipMemcpyHostToDevice));
+    if (!ops.empty()) {
+        const uint32_t grid = (uint32_t)((ops.size() + 255) / 256);
+        k_encode<<<grid, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), d_ops.as<OpDesc>(), ops.size(), cfg->seed,
+                                             cfg->ts_base, cfg->flip_permille);
+        GCK_HIP(hipGetLastError());
+    }
+    GCK_HIP(hipStreamSynchronize(c->stream));
+    d_ops.release();
+    if (n_files_out) *n_files_out = nf;
+    if (n_ops_out) *n_ops_out = ops.size();
+    if (file_sizes)
+        for (uint32_t n = 0; n < nf && n < max_files; ++n) file_sizes[n] = sizes[n];
+    return GCK_OK;
+}
+
+int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n) {
+    if (!ctx || !creation_index) return GCK_EINVAL;
+    const auto &o = ctx->c.walk_to_creation;
+    for (uint32_t i = 0; i < n && i < o.size(); ++i) creation_index[i] = o[i];
+    return GCK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+// gck_internal.h — device context shared by the replay pipeline and the encoder.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/gocask_hip.h"
+#include "gck_math.h"
+
+#define GCK_HIP(x)                                         \
+    do {                                                   \
+        hipError_t e_ = (x);                               \
+        if (e_ != hipSuccess) {                            \
+            gck::set_error(#x, e_, __FILE__, __LINE__);    \
+            return GCK_EDEVICE;                            \
+        }                                                  \
+    } while (0)
+
+namespace gck {
+
+void set_error(const char *what, hipError_t e, const char *file, int line);
+const char *last_error();
+
+// Grow-only device buffer.
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return GCK_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 256 ? 256 : bytes;
+        if (hipMalloc(&p, want) != hipSuccess) return GCK_ENOMEM;
+        cap = want;
+        return GCK_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+};
+
+enum Phase {
+    PH_SPEC = 0,   // k_spec_entry: speculative record start per chunk
+    PH_WALK,       // k_walk: header chain per chunk
+    PH_VALIDATE,   // k_validate + k_fixup
+    PH_SCAN,       // k_scan_chunks: record slots + per-file summary
+    PH_HOST,       // D2H summary + host bookkeeping
+    PH_COMPACT,    // k_compact: record table
+    PH_ROWIDX,     // k_row_index
+    PH_CRC,        // k_crc_rows: value CRC partials (the HBM-bound kernel)
+    PH_FINAL,      // k_finalize: CRC verdict + tuples
+    PH_COUNT
+};
+
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    gck_opts opts{};
+    int n_cu = 256;
+
+    // arena: files in walk order, each at a kRow-aligned offset
+    DBuf arena;
+    uint64_t arena_len = 0;  // bytes covered by rows (multiple of kRow)
+    uint32_t nfiles = 0;
+    std::vector<uint64_t> f_base, f_len;
+    std::vector<uint8_t> f_reset;
+    std::vector<uint32_t> f_first_chunk, f_nchunks;
+    uint64_t data_bytes = 0;
+
+    // chunk metadata
+    uint32_t n_chunks = 0;
+    DBuf d_fbase, d_flen, d_ffirst, d_fnch, d_fbad, d_fterm, d_ftpos, d_fnrec, d_ffirstrec, d_carry;
+    DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos;
+    DBuf d_rec_base, d_scratch_off, d_scratch_hdr, d_counters;
+
+    // records
+    uint64_t n_recs = 0;
+    DBuf d_rec_off, d_rec_hdr, d_rec_file, d_e, d_pre, d_out;
+    // rows
+    uint64_t n_rows = 0;
+    DBuf d_row_first, d_rend;
+
+    // constant tables
+    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb;
+
+    // results of the last run
+    int32_t status = 0;
+    uint32_t err_file = 0, files_walked = 0, final_last_offset = 0;
+    uint64_t err_off = 0, n_crc_fail = 0, n_fixups = 0, n_overflow = 0;
+    double ms_total = 0, ms_phase[PH_COUNT] = {};
+    hipEvent_t ev[PH_COUNT + 1] = {};
+
+    // encoder bookkeeping
+    std::vector<uint32_t> walk_to_creation;
+};
+
+int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after);
+
+}  // namespace gck
+
+struct gck_ctx {
+    gck::Ctx c;
+};

@@ -1,0 +1,202 @@
+/*
+ * gocask_hip.h — C-ABI of libgocask_hip.so, the MI355X-native replacement for
+ * aneshas/gocask's cold-start log replay.
+ *
+ * What it replaces (reference file:line):
+ *   - gck_replay / gck_ctx_*  replace the body of the unexported
+ *     (*DB).init(activeFile File) (core/db.go:110-123) together with
+ *     walkFile/readEntry (core/db.go:125-178), keyDir.set/unset/resetOffset
+ *     (core/keydir.go:22-53) and, per record, the crc.CalcCRC32 check that
+ *     (*DB).get applies lazily (core/db.go:304-313, internal/crc/crc.go:8-10).
+ *   - gck_db_*  mirror the public surface that sits on top of that seam:
+ *     core.NewDB (core/db.go:90-108) / gocask.Open (db.go:29-59) with the Disk
+ *     and InMemory file systems (internal/fs/disk.go:50-145,
+ *     internal/fs/memory.go:46-80), DB.Get (core/db.go:287-316) and DB.Keys
+ *     (core/db.go:318-324).
+ *   - gck_encode_* is the device-side record encoder (serializeEntry,
+ *     core/db.go:272-284, core/header.go:18-48) used for bulk corpus builds.
+ *
+ * Plain pointers and sizes only; no framework types cross this boundary.  The
+ * Go-side cgo binding a maintainer would add is shown in INTEGRATION.md.
+ *
+ * Errors never fall back to a CPU path: without a usable gfx950 device every
+ * compute entry point returns GCK_EDEVICE.
+ */
+#ifndef GOCASK_HIP_H
+#define GOCASK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes --------------------------------------------------------- */
+enum {
+    GCK_OK = 0,
+    GCK_EUNEXPECTED_EOF = 1, /* "gocask: startup error: unexpected EOF" (core/db.go:138)   */
+    GCK_EDEVICE = 2,         /* no gfx950 device / HIP runtime failure                       */
+    GCK_EINVAL = 3,          /* bad argument                                                 */
+    GCK_ENOMEM = 4,          /* device or host allocation failed                             */
+    GCK_EIO = 5,             /* file system error (open/stat/mmap/readdir)                   */
+    GCK_EKEY_NOT_FOUND = 6,  /* core.ErrKeyNotFound (core/db.go:17)                          */
+    GCK_ECRC_FAILED = 7,     /* core.ErrCRCFailed (core/db.go:24)                            */
+    GCK_EINVALID_KEY = 8,    /* core.ErrInvalidKey (core/db.go:27)                           */
+    GCK_ENOT_DIR = 9         /* "file exists and it's not a folder" (internal/fs/disk.go:116) */
+};
+
+/* ---- replay input / output ---------------------------------------------- */
+
+/* One data file, in FS.Walk order (internal/fs/disk.go:122-145).  data must stay
+ * valid for the whole call (mmap'd or host memory).  reset_after mirrors
+ * `file.Name() != activeFile.Name()` (core/db.go:117): 1 = lastOffset resets to 0
+ * after this file. */
+typedef struct gck_file {
+    const uint8_t *data;
+    uint64_t len;
+    uint8_t reset_after;
+} gck_file;
+
+#define GCK_F_TOMBSTONE 1u /* header KeySize == 0 (core/header.go:54-56)              */
+#define GCK_F_CRC_OK 2u    /* CRC-32/IEEE(last ValueSize bytes) == header CRC           */
+
+/* One record per header decoded, in walk order (superseded records and tombstones
+ * included).  40 bytes, no padding. */
+typedef struct gck_rec {
+    uint64_t rec_off;    /* header offset within its file                                  */
+    uint32_t file;       /* index into files[] (walk order); kdEntry.File = its Name()      */
+    uint32_t key_len;    /* KeySize, or ValueSize for a tombstone (core/db.go:151-155)     */
+    uint32_t value_pos;  /* kdEntry.ValuePos = lastOffset + 16 + KeySize mod 2^32          */
+    uint32_t value_size; /* header ValueSize (kdEntry.ValueSize)                           */
+    uint32_t crc;        /* header CRC (kdEntry.CRC)                                       */
+    uint32_t ts;         /* header Timestamp (kdEntry.Timestamp)                           */
+    uint32_t flags;      /* GCK_F_*                                                        */
+    uint32_t crc_calc;   /* CRC-32/IEEE of the record's last ValueSize bytes               */
+} gck_rec;
+
+typedef struct gck_opts {
+    int32_t device;        /* HIP device ordinal (default 0)                               */
+    uint32_t chunk_bytes;  /* boundary-speculation chunk (default 256 KiB, power of two)  */
+    uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
+    uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
+    uint32_t flags;        /* reserved, 0                                                  */
+} gck_opts;
+
+typedef struct gck_result {
+    gck_rec *recs;              /* library-owned host array; free with gck_result_free  */
+    uint64_t n;                 /* records in recs                                      */
+    uint64_t n_crc_fail;        /* records whose verdict is a reject                    */
+    uint32_t final_last_offset; /* keyDir.lastOffset after replay (later Puts use it)   */
+    int32_t status;             /* GCK_OK or GCK_EUNEXPECTED_EOF                        */
+    uint32_t err_file;          /* file index of the startup error                      */
+    uint32_t files_walked;      /* files the reference would have walked                */
+    uint64_t err_off;           /* header offset of the record that hit the error       */
+} gck_result;
+
+/* One-shot host-in/host-out replay (H2D, device pipeline, D2H). */
+int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
+void gck_result_free(gck_result *res);
+
+/* ---- device-resident context (benchmarks, repeated replays) ---------------- */
+typedef struct gck_ctx gck_ctx;
+
+typedef struct gck_stats {
+    uint64_t bytes;         /* data-file bytes replayed                               */
+    uint64_t n_recs;        /* records decoded                                         */
+    uint64_t n_crc_fail;    /* verdict rejects                                         */
+    uint64_t n_chunks;      /* speculation chunks                                      */
+    uint64_t n_fixups;      /* chunks whose speculative entry was wrong (re-walked)   */
+    uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
+    double ms_total;        /* last gck_ctx_run wall time (host clock)                */
+    double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
+} gck_stats;
+
+int gck_ctx_create(const gck_opts *opts, gck_ctx **out);
+void gck_ctx_destroy(gck_ctx *ctx);
+/* Copy files into the device arena (H2D). */
+int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles);
+/* Run the device pipeline on the resident arena.  Blocks until done. */
+int gck_ctx_run(gck_ctx *ctx);
+/* Copy the tuples of the last run to host memory. */
+int gck_ctx_fetch(gck_ctx *ctx, gck_result *out);
+int gck_ctx_stats(gck_ctx *ctx, gck_stats *out);
+const char *gck_phase_name(int phase);
+/* Device pointers of the last run's outputs (gck_rec array, n records) and the
+ * HIP stream the pipeline runs on (hipStream_t, as void*). */
+int gck_ctx_device_recs(gck_ctx *ctx, const gck_rec **recs, uint64_t *n);
+void *gck_ctx_stream(gck_ctx *ctx);
+/* Copy `len` bytes of file `file` (as resident in the arena) back to host. */
+int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, uint64_t len);
+
+/* ---- device record encoder (serializeEntry, core/db.go:272-284) ----------- */
+/* Synthetic corpus spec (DESIGN.md "Corpus"): op i is a Put (or, with
+ * tomb_permille, a Delete) written exactly as DB.Put/DB.Delete serialize it;
+ * files rotate when size + entry > max_file_size (core/db.go:214-232). */
+typedef struct gck_corpus_cfg {
+    uint64_t seed;
+    uint64_t max_file_size;
+    uint64_t n_ops;         /* stop after n ops (0: use n_files)                  */
+    uint32_t n_files;       /* stop when this many files are full                 */
+    uint32_t key_min, key_max;
+    uint64_t key_universe;  /* 0: unique keys                                     */
+    uint32_t val_fixed;     /* >0: fixed value size; 0: bounded Zipf(1.1) 64..64K */
+    uint32_t tomb_permille;
+    uint32_t flip_permille; /* single-bit flips inside values, after the CRC     */
+    uint32_t ts_base;
+} gck_corpus_cfg;
+
+/* Plan the corpus (host) and encode it straight into the context's device arena.
+ * Files are placed in lexical (walk) order of their names data_<n>_<ts_base+n>;
+ * the lexically last one is the active file.  n_files_out / file_sizes (creation
+ * order, may be NULL) report the layout. */
+int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files_out,
+                      uint64_t *n_ops_out, uint64_t *file_sizes, uint32_t max_files);
+/* Walk-order index -> creation index n of file data_<n>_... in the last encoded corpus. */
+int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n);
+/* The encoder's Zipf threshold table (65472 u32), for cross-checks. */
+void gck_encode_zipf_table(uint32_t *thr);
+
+/* ---- host-side DB mirror (core.NewDB / gocask.Open / Get / Keys) ------------ */
+typedef struct gck_db gck_db;
+
+typedef struct gck_config {
+    int64_t max_data_file_size; /* core.Config.MaxDataFileSize (core/db.go:84-87)     */
+    const char *data_dir;       /* core.Config.DataDir; joined with db_path           */
+} gck_config;
+
+/* core.NewDB(dbpath, fs.NewDisk(), time, cfg): create the dir if needed, pick the
+ * active file (lexically last entry, created as data_<n>_<unix>.csk when the dir is
+ * empty), walk every *.csk in lexical order and replay them on the GPU.  On a
+ * startup error *out is still set (like NewDB returning &db, err) and the
+ * message "gocask: startup error: unexpected EOF" is written to errbuf. */
+int gck_db_open(const char *db_path, const gck_config *cfg, const gck_opts *opts, gck_db **out,
+                char *errbuf, size_t errlen);
+/* In-memory file system (internal/fs/memory.go): one file "data" (also active). */
+int gck_db_open_mem(const uint8_t *data, uint64_t len, const gck_opts *opts, gck_db **out,
+                    char *errbuf, size_t errlen);
+/* DB.Get: GCK_EINVALID_KEY for an empty key, GCK_EKEY_NOT_FOUND, GCK_ECRC_FAILED.
+ * On success *val (library-owned until the next call or close) holds *vlen bytes. */
+int gck_db_get(gck_db *db, const uint8_t *key, uint32_t klen, const uint8_t **val, uint64_t *vlen);
+/* DB.Keys: number of live keys; gck_db_key(i) returns the i-th (any order). */
+uint64_t gck_db_keys(gck_db *db);
+int gck_db_key(gck_db *db, uint64_t i, const uint8_t **key, uint32_t *klen);
+/* kdEntry of a key (CRC, Timestamp, ValuePos, ValueSize, file name). */
+int gck_db_entry(gck_db *db, const uint8_t *key, uint32_t klen, uint32_t *crc, uint32_t *ts,
+                 uint32_t *value_pos, uint32_t *value_size, const char **file);
+uint32_t gck_db_last_offset(gck_db *db);
+const char *gck_db_active_file(gck_db *db);
+uint32_t gck_db_nfiles(gck_db *db);
+const char *gck_db_file_name(gck_db *db, uint32_t i);
+void gck_db_close(gck_db *db);
+
+/* Library/device info. */
+int gck_device_count(void);
+const char *gck_version(void);
+/* Text of the last HIP failure on this thread (GCK_EDEVICE diagnostics). */
+const char *gck_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,277 @@
+"""Parity of the HIP replay path against the CPU oracle (GPU box only).
+
+Everything goes through the C-ABI (libgocask_hip.so).  Bit-exact bar: every
+field of every record tuple, the CRC accept/reject verdict, the keydir, the
+error status and keyDir.lastOffset must equal the oracle's.
+"""
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import oracle as orc_mod
+from golden_cases import case_names, check_case, load_case
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("rec_off", "file", "key_len", "value_pos", "value_size", "crc", "ts", "flags", "crc_calc")
+
+
+@pytest.fixture(scope="module")
+def g():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    import gocask_amd
+
+    assert gocask_amd.device_count() > 0, "no GPU visible"
+    return gocask_amd
+
+
+def assert_same(got, gst, want, wst):
+    assert gst["status"] == wst["status"], (gst, wst)
+    if wst["status"]:
+        assert gst["err_off"] == wst["err_off"] and gst["err_file"] == wst["err_file"]
+    assert gst["final_last_offset"] == wst["final_last_offset"]
+    assert len(got) == len(want), (len(got), len(want))
+    for f in FIELDS:
+        if not np.array_equal(got[f], want[f]):
+            bad = np.nonzero(got[f] != want[f])[0][:5]
+            raise AssertionError(f"field {f} differs at {bad}: got {got[f][bad]} want {want[f][bad]}")
+
+
+def walk_sorted(files, names):
+    walk = sorted(range(len(files)), key=lambda i: names[i])
+    wf = [files[i] for i in walk]
+    reset = [i + 1 < len(wf) for i in range(len(wf))]  # the lexically last file is active
+    return wf, reset
+
+
+# ------------------------------------------------------------------ golden ---
+@pytest.mark.parametrize("name", case_names())
+def test_golden_cases(g, orc, name):
+    meta, files, reset = load_case(name)
+    got, gst = g.replay(files, reset)
+    check_case(meta, files, got, g.keydir(files, got), gst)
+    want, wst = orc.replay(files, reset)
+    assert_same(got, gst, want, wst)
+
+
+@pytest.mark.parametrize("chunk", [4096, 1 << 16])
+@pytest.mark.parametrize("name", ["datatxt_1000_puts", "existing_after_startup", "partial_write_desync"])
+def test_golden_small_chunks(g, orc, name, chunk):
+    meta, files, reset = load_case(name)
+    got, gst = g.replay(files, reset, chunk_bytes=chunk, chunk_cap=8)
+    want, wst = orc.replay(files, reset)
+    assert_same(got, gst, want, wst)
+
+
+# -------------------------------------------------------- NewDB / Open API ---
+def test_newdb_in_memory_deleted_key(g):
+    # core/db_test.go:375-393: Put foo, Delete foo, re-open -> ErrKeyNotFound
+    data = orc_mod.entry(12345, b"foo", b"bar") + orc_mod.tombstone(12345, b"foo")
+    db, err = g.NewDB("", g.NewInMemory(data))
+    assert err is None
+    v, err = db.Get(b"foo")
+    assert err is g.ErrKeyNotFound and v is None
+    assert db.Keys() == []
+    assert db.last_offset == 41
+
+
+def test_newdb_in_memory_datatxt(g):
+    meta, files, reset = load_case("datatxt_1000_puts")
+    db, err = g.NewDB("", g.NewInMemory(files[0].tobytes()))
+    assert err is None
+    assert sorted(db.Keys()) == sorted(meta["expect"])
+    for k, e in meta["expect"].items():
+        v, err = db.Get(k.encode())
+        assert err is None and v == e["value"].encode()
+    _, err = db.Get(b"")
+    assert err is g.ErrInvalidKey
+
+
+def test_newdb_crc_failed(g):
+    meta, files, reset = load_case("crc_fail")
+    db, err = g.NewDB("", g.NewInMemory(files[0].tobytes()))
+    assert err is None
+    v, err = db.Get(b"foo")
+    assert err is g.ErrCRCFailed and v is None
+
+
+def test_newdb_startup_error(g):
+    meta, files, reset = load_case("partial_write_desync")
+    db, err = g.NewDB("", g.NewInMemory(files[0].tobytes()))
+    assert isinstance(err, g.StartupError) and str(err) == "gocask: startup error: unexpected EOF"
+    assert db is not None and sorted(db.Keys()) == ["key", "user"]
+
+
+def test_open_disk_lexical_walk_and_active_file(g, orc, tmp_path):
+    # data_<n>_<unix>.csk names, 12 files, lexical walk + foo.txt skipped
+    files, names = orc.gen_corpus(seed=21, val_fixed=0, key_min=8, key_max=12, key_universe=500,
+                                  tomb_permille=30, max_file_size=1 << 16, n_files=12)
+    d = tmp_path / "mydb"
+    d.mkdir()
+    for f, n in zip(files, names):
+        (d / (n + ".csk")).write_bytes(f.tobytes())
+    (d / "foo.txt").write_bytes(b"not a data file")
+    db, err = g.Open("mydb", g.WithDataDir(str(tmp_path)))
+    assert err is None
+    assert db.active_file == "foo"  # lexically last entry of any kind (internal/fs/disk.go:56-67)
+    assert db.files() == sorted(names)
+    wf, _ = walk_sorted(files, names)
+    want, wst = orc.replay(wf, [True] * len(wf))  # active "foo" never matches: always reset
+    kd = orc.keydir(wf, want, [True] * len(wf))
+    assert sorted(k.encode("utf-8", "surrogateescape") for k in db.Keys()) == sorted(kd)
+    for k, r in list(kd.items())[:200]:
+        e = db.Entry(k)
+        assert e["ValuePos"] == int(r["value_pos"]) and e["CRC"] == int(r["crc"])
+        assert e["File"] == sorted(names)[int(r["file"])]
+        v, err = db.Get(k)
+        assert err is None and zlib.crc32(v) == int(r["crc"])
+    assert db.last_offset == wst["final_last_offset"]
+
+
+def test_open_creates_active_file(g, tmp_path):
+    db, err = g.Open("fresh", g.WithDataDir(str(tmp_path)))
+    assert err is None and db.Keys() == []
+    made = os.listdir(tmp_path / "fresh")
+    assert len(made) == 1 and made[0].startswith("data_0_") and made[0].endswith(".csk")
+
+
+# ------------------------------------------------------- device encoder (f4) --
+@pytest.mark.parametrize("kw", [
+    dict(seed=31, val_fixed=0, key_min=8, key_max=24, key_universe=1000, tomb_permille=10, flip_permille=10,
+         max_file_size=1 << 20, n_files=5),
+    dict(seed=32, val_fixed=1024, key_min=16, key_max=16, max_file_size=1 << 20, n_files=1),
+])
+def test_device_encoder_matches_oracle_generator(g, orc, kw):
+    files, names = orc.gen_corpus(**kw)
+    with g.ReplayContext() as ctx:
+        info = ctx.encode(**kw)
+        assert info["n_files"] == len(files)
+        assert list(info["sizes"]) == [len(f) for f in files]
+        for w, n in enumerate(info["walk_order"]):
+            got = ctx.read_file(w, 0, len(files[n]))
+            assert np.array_equal(got, files[n]), names[n]
+
+
+# ------------------------------------------------------ randomised parity ---
+CORPORA = [
+    dict(seed=41, val_fixed=0, key_min=8, key_max=24, key_universe=2000, tomb_permille=10, flip_permille=10,
+         max_file_size=4 << 20, n_files=4),
+    dict(seed=42, val_fixed=100, key_min=8, key_max=8, key_universe=50, tomb_permille=200, max_file_size=1 << 18,
+         n_files=6),
+    dict(seed=43, val_fixed=4096, key_min=16, key_max=16, max_file_size=8 << 20, n_files=2),
+]
+
+
+@pytest.mark.parametrize("chunk,cap", [(4096, 2), (1 << 15, 256), (1 << 18, 256)])
+@pytest.mark.parametrize("ci", range(len(CORPORA)))
+def test_random_corpora(g, orc, ci, chunk, cap):
+    files, names = orc.gen_corpus(**CORPORA[ci])
+    wf, reset = walk_sorted(files, names)
+    want, wst = orc.replay(wf, reset)
+    got, gst = g.replay(wf, reset, chunk_bytes=chunk, chunk_cap=cap)
+    assert_same(got, gst, want, wst)
+    assert np.array_equal(got["flags"] & 2 == 0, want["crc_calc"] != want["crc"])
+
+
+def test_tiny_records_and_empty_values(g, orc):
+    rng = np.random.default_rng(7)
+    recs = []
+    for i in range(3000):
+        k = bytes(rng.integers(0, 256, int(rng.integers(1, 4)), dtype=np.uint8))
+        r = int(rng.integers(0, 10))
+        if r == 0:
+            recs.append(orc_mod.tombstone(i, k))
+        elif r == 1:
+            recs.append(orc_mod.entry(i, k, b""))
+        else:
+            recs.append(orc_mod.entry(i, k, bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8))))
+    data = b"".join(recs)
+    for chunk in (4096, 1 << 16):
+        want, wst = orc.replay([data], [False])
+        got, gst = g.replay([data], [False], chunk_bytes=chunk, chunk_cap=16)
+        assert_same(got, gst, want, wst)
+
+
+def test_values_that_look_like_records(g, orc):
+    # values that are themselves serialized records: speculation will land inside
+    # them; validation + fixup must still produce the reference's chain
+    rng = np.random.default_rng(9)
+    parts = []
+    for i in range(400):
+        inner = b"".join(orc_mod.entry(j, b"inner%d" % j, bytes(rng.integers(0, 256, 300, dtype=np.uint8)))
+                         for j in range(int(rng.integers(1, 30))))
+        parts.append(orc_mod.entry(i, b"outer%05d" % i, inner))
+    data = b"".join(parts)
+    want, wst = orc.replay([data], [True])
+    for chunk in (4096, 1 << 14):
+        got, gst = g.replay([data], [True], chunk_bytes=chunk)
+        assert_same(got, gst, want, wst)
+
+
+def test_eof_classes_at_every_chunk_phase(g, orc):
+    base = b"".join(orc_mod.entry(i, b"key%04d" % i, b"v" * (i % 97)) for i in range(300))
+    tails = [b"", b"\x01" * 9, struct.pack("<IIII", 0, 1, 5, 5), struct.pack("<IIII", 0, 1, 5, 5) + b"ab",
+             orc_mod.entry(1, b"kk", b"value")[:-2]]
+    for cut in (0, 1, 17, 4000):
+        for t in tails:
+            files = [base[:len(base) - cut] if cut else base, t + b"", base]
+            reset = [True, False, True]
+            want, wst = orc.replay(files, reset)
+            got, gst = g.replay(files, reset, chunk_bytes=4096)
+            assert_same(got, gst, want, wst)
+
+
+# ------------------------------------------------------------ config sizes ---
+def test_config1_64mib_vs_oracle(g, orc):
+    kw = dict(seed=1, val_fixed=1024, key_min=16, key_max=16, max_file_size=64 << 20, n_files=1)
+    files, names = orc.gen_corpus(**kw)
+    assert len(files[0]) == 67108800
+    want, wst = orc.replay(files, [False])
+    with g.ReplayContext() as ctx:
+        ctx.encode(**kw)
+        ctx.run()
+        got, gst = ctx.fetch()
+    assert_same(got, gst, want, wst)
+    assert len(got) == 63550
+
+
+def test_config2_8gib_value_pos_wraps(g):
+    # 1 x 8 GiB, 4 KiB values: ValuePos is uint32 and wraps (core/keydir.go:25)
+    kw = dict(seed=2, val_fixed=4096, key_min=16, key_max=16, max_file_size=8 << 30, n_files=1)
+    with g.ReplayContext() as ctx:
+        info = ctx.encode(**kw)
+        assert info["n_ops"] == 2080895 and int(info["sizes"][0]) == 8589934560
+        ctx.run()
+        got, gst = ctx.fetch()
+        st = ctx.stats()
+    assert gst["status"] == 0 and len(got) == 2080895 and st["n_crc_fail"] == 0
+    i = np.arange(len(got), dtype=np.uint64)
+    assert np.array_equal(got["rec_off"], i * np.uint64(4128))
+    assert np.array_equal(got["value_pos"], ((i * np.uint64(4128) + np.uint64(32)) % np.uint64(1 << 32)).astype(np.uint32))
+    assert (got["flags"] & 2).all()
+    assert np.array_equal(got["ts"], (np.uint64(1700000000) + i).astype(np.uint32))
+
+
+def test_config5_bitflips_reject_set(g):
+    # C5 shape at 1/8 scale (4 GiB): rejects must be exactly the flipped records
+    import spec
+
+    kw = dict(seed=5, val_fixed=0, key_min=8, key_max=24, key_universe=600000, tomb_permille=10,
+              flip_permille=10, max_file_size=2 << 30, n_files=2)
+    with g.ReplayContext() as ctx:
+        ctx.encode(**kw)
+        ctx.run()
+        got, gst = ctx.fetch()
+    assert gst["status"] == 0 and len(got) > 100000
+    ops = (got["ts"].astype(np.uint64) - np.uint64(1700000000)) % np.uint64(1 << 32)
+    flipped = spec.expected_flips(5, ops, 10, 10)
+    rejected = (got["flags"] & 2) == 0
+    assert flipped.sum() > 1000
+    assert np.array_equal(rejected, flipped)
+    tomb = (got["flags"] & 1) == 1
+    assert np.array_equal(tomb, (spec.H(5, 3, ops) % np.uint64(1000)) < np.uint64(10))
