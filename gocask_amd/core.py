@@ -301,6 +301,13 @@ class ReplayContext:
         return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
                     n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases)
 
+    def stream_read_ceiling(self, iters=10):
+        """Plain streaming read of the resident arena: (ms per pass, GB/s)."""
+        ms = ctypes.c_double()
+        gbs = ctypes.c_double()
+        check(self._L.gck_diag_stream_read(self._h, iters, ctypes.byref(ms), ctypes.byref(gbs)))
+        return ms.value, gbs.value
+
     def read_file(self, file, off=0, length=None):
         n = length
         buf = np.zeros(n, dtype=np.uint8)

@@ -1,0 +1,53 @@
+// diag.hip — measurement helpers (not on the replay path).
+//
+// gck_diag_stream_read: a plain streaming read of the resident arena (16 B per
+// lane, grid-stride, XOR-reduced so nothing is dead-code eliminated).  It is
+// the practical HBM read ceiling that k_crc_rows is compared against in
+// bench.py / DESIGN.md (SURVEY.md §8d asks for the fraction of a measured
+// streaming-read kernel besides the spec peak).
+#include "gck_internal.h"
+
+namespace gck {
+
+__global__ __launch_bounds__(256) void k_stream_read(const uint4 *__restrict__ p, uint64_t n16, uint32_t *sink) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    uint32_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; i < n16; i += stride) {
+        uint4 a = p[i];
+        uint4 b = i + 256 < n16 ? p[i + 256] : make_uint4(0, 0, 0, 0);
+        uint4 c = i + 512 < n16 ? p[i + 512] : make_uint4(0, 0, 0, 0);
+        uint4 d = i + 768 < n16 ? p[i + 768] : make_uint4(0, 0, 0, 0);
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;  // practically never: keeps the loads live
+}
+
+}  // namespace gck
+
+using namespace gck;
+
+extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs) {
+    if (!ctx || iters <= 0) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    const uint64_t n16 = c->arena_len / 16;
+    if (!n16) return GCK_EINVAL;
+    const uint32_t grid = (uint32_t)c->n_cu * 8;
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    k_stream_read<<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);  // warm-up
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) k_stream_read<<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    const double per = ms / iters;
+    if (ms_per_iter) *ms_per_iter = per;
+    if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
+    return GCK_OK;
+}

@@ -76,7 +76,7 @@ struct Ctx {
     // chunk metadata
     uint32_t n_chunks = 0;
     DBuf d_fbase, d_flen, d_ffirst, d_fnch, d_fbad, d_fterm, d_ftpos, d_fnrec, d_ffirstrec, d_carry;
-    DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos;
+    DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
     DBuf d_rec_base, d_scratch_off, d_scratch_hdr, d_counters;
 
     // records
@@ -87,7 +87,7 @@ struct Ctx {
     DBuf d_row_first, d_rend;
 
     // constant tables
-    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb;
+    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;
 
     // results of the last run
     int32_t status = 0;

@@ -33,7 +33,7 @@ void set_error(const char *what, hipError_t e, const char *file, int line) {
 const char *last_error() { return g_err.c_str(); }
 
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
-constexpr int kHops = 3;          // extra headers a speculative start must chain through
+constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 constexpr uint32_t kNibBase = 32768;
 
@@ -60,17 +60,20 @@ __device__ __forceinline__ Hdr ld_hdr(const uint8_t *__restrict__ arena, uint64_
     return h;
 }
 
-// Follow the header chain from q: plausible sizes, records inside the file.
+// Follow the header chain from q for kHops+1 headers: key length in
+// [1, max_key] and every record inside the file.  A chain may only end exactly
+// at the file end.  (A record straddling the file end is rejected: that only
+// costs a fixup for the one chunk where it is real.)
 __device__ bool chain_ok(const uint8_t *__restrict__ arena, uint64_t base, uint64_t len, uint64_t q,
                          uint32_t max_key) {
     for (int h = 0; h <= kHops; ++h) {
-        if (q == len) return true;
-        if (q + 16 > len) return h > 0;
+        if (q == len) return h > 0;
+        if (q + 16 > len) return false;
         const Hdr hd = ld_hdr(arena, base + q);
         const uint32_t klen = hd.ks ? hd.ks : hd.vs;
         if (klen == 0 || klen > max_key) return false;
         const uint64_t end = q + 16 + (uint64_t)hd.ks + hd.vs;
-        if (end > len) return h > 0;
+        if (end > len) return false;
         q = end;
     }
     return true;
@@ -110,8 +113,12 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
 }
 
 // ------------------------------------------------------------------ kernels ---
-// One wavefront per chunk: the first byte position >= chunk start whose header
-// and the next kHops headers are plausible.  Chunk 0 of a file starts at 0.
+// One wavefront per chunk finds the first byte position >= chunk start whose
+// header and the next kHops headers are plausible (chunk 0 of a file starts at
+// 0).  Each pass tests 1 KiB of positions: lane l loads bytes [16l, 16l+32) of
+// the window and checks its 16 candidate offsets in registers.  A hit at p is
+// replaced by p+1 when p+1 chains too: every true header has a plausible
+// "shadow" one byte earlier (Timestamp's top byte + KeySize<<8, ValueSize<<8).
 __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ fbase,
                                                     const uint64_t *__restrict__ flen,
@@ -129,29 +136,38 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     if (cs == 0) {
         found = 0;
     } else {
-        for (uint64_t p0 = cs; p0 < ce && found == kNone; p0 += 64) {
-            const uint64_t p = p0 + lane;
-            bool cand = false;
-            if (p < ce && p + 16 <= len) {
-                const uint64_t o = base + p + 8;
-                const uint32_t *w = reinterpret_cast<const uint32_t *>(arena + (o & ~3ull));
-                const uint32_t sh = (uint32_t)o & 3u;
-                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-                const uint32_t ks = ab(w1, w0, sh), vs = ab(w2, w1, sh);
+        for (uint64_t b0 = cs; b0 < ce && found == kNone; b0 += 1024) {
+            const uint64_t p0 = b0 + 16ull * lane;
+            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + p0);  // 16 B aligned
+            const uint4 m0 = src[0], m1 = src[1];
+            const uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+            uint32_t cm = 0;
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int o = t + 8, k = o >> 2, sh = o & 3;
+                const uint32_t ks = ab(w[k + 1], w[k], sh), vs = ab(w[k + 2], w[k + 1], sh);
                 const uint32_t klen = ks ? ks : vs;
-                cand = klen != 0 && klen <= max_key && p + 16 + (uint64_t)ks + vs <= len;
+                const uint64_t p = p0 + t;
+                const bool ok = p < ce && klen != 0 && klen <= max_key && p + 16 + (uint64_t)ks + vs <= len;
+                cm |= (ok ? 1u : 0u) << t;
             }
-            uint64_t mask = __ballot(cand);
-            while (mask) {
-                const int l = __ffsll((long long)mask) - 1;
-                const uint64_t q = p0 + (uint64_t)l;
-                if (chain_ok(arena, base, len, q, max_key)) {
-                    found = q;
-                    break;
+            uint64_t lanes = __ballot(cm != 0);
+            while (lanes && found == kNone) {
+                const int l = __ffsll((long long)lanes) - 1;
+                uint32_t lm = __builtin_amdgcn_readlane(cm, l);
+                while (lm) {
+                    const int t = __ffs(lm) - 1;
+                    const uint64_t q = b0 + 16ull * l + t;
+                    if (chain_ok(arena, base, len, q, max_key)) {
+                        found = q;
+                        break;
+                    }
+                    lm &= lm - 1;
                 }
-                mask &= mask - 1;
+                lanes &= lanes - 1;
             }
         }
+        if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, max_key)) found += 1;
     }
     if (lane == 0) ch_entry[c] = found;
 }
@@ -200,8 +216,10 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                     ch_exit, ch_term, ch_tpos);
 }
 
-// Chunk c is consistent iff its entry equals the record start the nearest
-// earlier non-empty chunk's chain reaches (or none if that chain ended).
+// Chunk c is consistent iff its entry equals the record start that the chain
+// of the nearest earlier non-empty chunk reaches (none if that chain ended).
+// If every chunk is consistent, every chunk is correct (chunk 0 of each file
+// is true by construction): induction over the chunk order.
 __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ ch_file,
                                                   const uint64_t *__restrict__ ch_start,
                                                   const uint64_t *__restrict__ ch_end,
@@ -209,64 +227,59 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
                                                   const uint64_t *__restrict__ ch_exit,
                                                   const uint32_t *__restrict__ ch_term,
                                                   const uint32_t *__restrict__ f_first_chunk,
-                                                  uint32_t *f_first_bad, uint32_t *counters,
+                                                  uint32_t *__restrict__ ch_bad, uint32_t *counter,
                                                   uint32_t n_chunks) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
-    if (c == fc) return;
     bool bad = false;
-    uint32_t j = c - 1;
-    int steps = 0;
-    while (j > fc && ch_entry[j] == kNone && steps < 256) { --j; ++steps; }
-    uint64_t expect = kNone;
-    if (ch_entry[j] == kNone) {
-        bad = true;
-    } else if (ch_term[j] == T_NONE) {
-        const uint64_t x = ch_exit[j];
-        if (x < ch_start[c]) bad = true;
-        else expect = x < ch_end[c] ? x : kNone;
+    if (c != fc) {
+        uint32_t j = c - 1;
+        while (j > fc && ch_entry[j] == kNone) --j;
+        uint64_t expect = kNone;
+        if (ch_entry[j] == kNone) {
+            bad = true;
+        } else if (ch_term[j] == T_NONE) {
+            const uint64_t x = ch_exit[j];
+            if (x < ch_start[c]) bad = true;
+            else expect = x < ch_end[c] ? x : kNone;
+        }
+        if (!bad && ch_entry[c] != expect) bad = true;
     }
-    if (!bad && ch_entry[c] != expect) bad = true;
-    if (bad) {
-        atomicMin(&f_first_bad[f], c - fc);
-        atomicAdd(&counters[0], 1u);
-    }
+    ch_bad[c] = bad ? 1u : 0u;
+    const uint64_t m = __ballot(bad);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (uint32_t)__popcll(m));
 }
 
-// One lane per file with an inconsistent chunk: re-derive entries sequentially
-// from the last good chunk and re-walk every chunk whose entry changes.
-__global__ void k_fixup(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
-                        const uint64_t *__restrict__ flen, const uint32_t *__restrict__ f_first_chunk,
-                        const uint32_t *__restrict__ f_nchunks, uint32_t *f_first_bad,
-                        const uint64_t *__restrict__ ch_end, uint64_t *ch_entry, uint32_t *ch_count,
-                        uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *s_off,
-                        uint4 *s_hdr, uint32_t cap, uint32_t nfiles, uint32_t *counters) {
-    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nfiles) return;
-    const uint32_t fb = f_first_bad[f];
-    if (fb == kNone32) return;
-    const uint32_t fc = f_first_chunk[f], nc = f_nchunks[f];
-    bool ended = false;
-    uint64_t expect = kNone;
-    int64_t j = (int64_t)fc + fb - 1;
-    while (j > (int64_t)fc && ch_entry[j] == kNone) --j;
-    if (ch_term[j] != T_NONE) ended = true;
-    else expect = ch_exit[j];
-    for (uint32_t k = fc + fb; k < fc + nc; ++k) {
-        const uint64_t e_new = (!ended && expect < ch_end[k]) ? expect : kNone;
-        if (e_new != ch_entry[k]) {
-            ch_entry[k] = e_new;
-            atomicAdd(&counters[1], 1u);
-            walk_into_chunk(arena, fbase, flen, k, f, ch_end[k], e_new, cap, s_off, s_hdr, ch_count, ch_exit,
-                            ch_term, ch_tpos);
-        }
-        if (ch_entry[k] != kNone) {
-            if (ch_term[k] != T_NONE) ended = true;
-            else expect = ch_exit[k];
-        }
+// One lane per inconsistent chunk: take the entry from the nearest earlier
+// non-empty chunk and re-walk.  Chunks whose look-back crosses another
+// inconsistent chunk wait for a later round (the next k_validate decides),
+// so no lane reads state another lane is rewriting.
+__global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena,
+                                               const uint64_t *__restrict__ fbase,
+                                               const uint64_t *__restrict__ flen,
+                                               const uint32_t *__restrict__ ch_file,
+                                               const uint64_t *__restrict__ ch_end,
+                                               const uint32_t *__restrict__ f_first_chunk,
+                                               const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
+                                               uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
+                                               uint64_t *ch_tpos, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
+                                               uint32_t n_chunks, uint32_t *counter) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks || !ch_bad[c]) return;
+    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
+    uint32_t j = c - 1;
+    while (j > fc && ch_entry[j] == kNone && !ch_bad[j]) --j;
+    if (ch_bad[j] || ch_entry[j] == kNone) return;
+    uint64_t e_new = kNone;
+    if (ch_term[j] == T_NONE) {
+        const uint64_t x = ch_exit[j];
+        if (x < ch_end[c]) e_new = x;
     }
-    f_first_bad[f] = kNone32;
+    ch_entry[c] = e_new;
+    atomicAdd(counter, 1u);
+    walk_into_chunk(arena, fbase, flen, c, f, ch_end[c], e_new, cap, s_off, s_hdr, ch_count, ch_exit, ch_term,
+                    ch_tpos);
 }
 
 // Exclusive scan of per-chunk record counts (single workgroup; n <= ~1M).
@@ -403,18 +416,51 @@ __device__ __forceinline__ uint32_t slice4(const uint32_t *lds, uint32_t l31, ui
            lds[8192 + (((c >> 11) & 0x1FE0u) | l31)] ^ lds[((c >> 19) & 0x1FE0u) | l31];
 }
 
-__device__ __forceinline__ uint32_t bytemask(int32_t lo, int32_t hi) {
-    return (uint32_t)(((1ull << (8 * hi)) - 1) & ~((1ull << (8 * lo)) - 1));
+// Raw candidate record of a row: arena offset of the record and {KeySize,
+// ValueSize}.  Loaded one row ahead; converted to row-relative positions only
+// when the row is processed, so the loads never force an early wait.
+struct RawRec {
+    uint64_t off;
+    uint2 kv;
+};
+
+__device__ __forceinline__ RawRec load_raw(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
+                                           uint64_t r) {
+    RawRec x;
+    x.off = rec_off[r];
+    x.kv = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint32_t *>(rec_hdr + r) + 2);
+    return x;
+}
+
+// Record start and end relative to row start rs, clamped to [-1, kRow+1]
+// (every comparison with a position inside the row is preserved).
+__device__ __forceinline__ void to_span(const RawRec &x, uint64_t rs, int32_t &st_out, int32_t &ve_out) {
+    const int64_t st = (int64_t)x.off - (int64_t)rs;
+    const int64_t ve = st + 16 + (int64_t)x.kv.x + (int64_t)x.kv.y;
+    st_out = (int32_t)max(min(st, (int64_t)kRow + 1), (int64_t)-1);
+    ve_out = (int32_t)max(min(ve, (int64_t)kRow + 1), (int64_t)-1);
+}
+
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xF, false);
 }
 
 // The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns bytes
-// [64k, 64k+64).  Each lane runs the CRC register over the value bytes of its
-// slab (non-value bytes masked to zero, the register cut at every value end),
-// references its open tail to the row end with a per-lane constant shift
-// Z_{64(63-k)} (8 nibble lookups), and a segmented XOR over lanes joins the
-// pieces of each value.  Outputs per record: e (state at the value's last
-// word), pre (its run just before the cut lane); per row: the run open at
-// the row end.  k_finalize stitches rows (DESIGN.md §CRC algebra).
+// [64k, 64k+64).  Every byte enters a CRC register, no masking: records tile
+// the file, so lane k's register simply runs over whole records and is closed
+// exactly at every record end (the last partial word byte-wise) and restarted
+// at the next word.  The chain of record r therefore covers
+// [align4(start_r), end_r) = header/key prefix || value; k_finalize removes the
+// prefix by linearity.  An open register at the slab end belongs to the record
+// containing that position; it is referenced to the row end with the per-lane
+// constant shift Z_{64(63-k)} (8 nibble lookups) and a segmented XOR over the
+// wave (DPP prefix scan) joins each record's lanes.  Outputs: e per record
+// (state at its end, carry-free), pre per record (its run just before the cut
+// lane), per row the run open at the row end.  Loads for row i+1 (data,
+// candidate records) and row_first of row i+2 are issued before row i is
+// processed.  MODE != 0 are ablation variants for gck_diag_crc_variant.
+template <int MODE>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
                                                    const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint64_t *__restrict__ rec_off,
@@ -433,130 +479,193 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
-    const int32_t s_rel = (int32_t)lane * kSlab;
-    const uint64_t n_waves = (uint64_t)gridDim.x * kWaves;
-    constexpr int32_t BIG = INT_MAX / 2;
+    const int32_t s_rel = (int32_t)lane * kSlab, e_rel = s_rel + kSlab;
+    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    const uint64_t last_rec = n_total - 1;  // only launched with n_total > 0
 
-    for (uint64_t row = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6); row < n_rows; row += n_waves) {
+    uint64_t row = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (row >= n_rows) return;
+    uint32_t ra = row_first[row], rb = row_first[row + 1];
+    uint64_t nrow = row + stride;
+    const uint64_t nrow_c = min(nrow, n_rows - 1);
+    uint32_t nra = row_first[nrow_c], nrb = row_first[nrow_c + 1];
+    // lanes past the row's last candidate load the last one again (same line)
+    RawRec cur = load_raw(rec_off, rec_hdr, min((uint64_t)ra + lane, min((uint64_t)rb, last_rec)));
+    const uint4 *src = reinterpret_cast<const uint4 *>(arena + row * kRow + s_rel);
+    uint4 d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+
+    for (;;) {
         const uint64_t rs = row * kRow;
-        const uint4 *src = reinterpret_cast<const uint4 *>(arena + rs + s_rel);
-        const uint4 d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
-        const uint32_t ra = row_first[row], rb = row_first[row + 1];
+        // ---- issue: row_first of row i+2, candidates and data of row i+1 (all
+        // unconditional, clamped indices, so the waits stay counted)
+        const uint64_t nnrow = nrow + stride;
+        const uint64_t nnrow_c = min(nnrow, n_rows - 1);
+        const uint32_t nnra = row_first[nnrow_c], nnrb = row_first[nnrow_c + 1];
+        const RawRec nxt = load_raw(rec_off, rec_hdr, min((uint64_t)nra + lane, min((uint64_t)nrb, last_rec)));
+        const uint4 *ns = reinterpret_cast<const uint4 *>(arena + min(nrow, n_rows - 1) * kRow + s_rel);
+        const uint4 n0 = ns[0], n1 = ns[1], n2 = ns[2], n3 = ns[3];
 
-        // value intervals (row-relative, clamped) of records touching this slab
-        int nint = 0;
-        int32_t v0s = BIG, v0e = BIG, v1s = BIG, v1e = BIG, v2s = BIG, v2e = BIG, v3s = BIG, v3e = BIG;
+        // ---- record ends inside this slab (<= 4) and the record open at its end
+        int ncut = 0;
+        int32_t c0 = 99, c1 = 99, c2 = 99, c3 = 99;  // end offset within the slab, 1..64
         uint32_t i0 = 0, i1 = 0, i2 = 0, i3 = 0;
-        if (ra < n_total) {
-            const uint32_t last = rb < n_total ? rb : (uint32_t)(n_total - 1);
+        uint32_t t = kNone32;
+        if (!(MODE & 1) && ra < n_total) {
+            const uint32_t last = rb < n_total ? rb : (uint32_t)last_rec;
             for (uint32_t b0 = ra; b0 <= last; b0 += 64) {
-                const uint32_t r = b0 + lane;
-                int32_t my_s = 0, my_e = 0;
-                if (r <= last) {
-                    const uint4 h = rec_hdr[r];
-                    const int64_t vs = (int64_t)(rec_off[r] + 16 + h.z) - (int64_t)rs;
-                    const int64_t ve = vs + (int64_t)h.w;
-                    my_s = (int32_t)max(min(vs, (int64_t)kRow + 1), (int64_t)-1);
-                    my_e = (int32_t)max(min(ve, (int64_t)kRow + 1), (int64_t)-1);
-                }
+                int32_t bs, be;
+                if (b0 == ra) to_span(cur, rs, bs, be);
+                else to_span(load_raw(rec_off, rec_hdr, min((uint64_t)b0 + lane, (uint64_t)last)), rs, bs, be);
                 const uint32_t cnt = min(64u, last - b0 + 1);
                 for (uint32_t j = 0; j < cnt; ++j) {
-                    const int32_t js = __builtin_amdgcn_readlane(my_s, j);
-                    const int32_t je = __builtin_amdgcn_readlane(my_e, j);
-                    if (je > js && js < s_rel + kSlab && je > s_rel) {
-                        const uint32_t id = b0 + j;
-                        if (nint == 0) { v0s = js; v0e = je; i0 = id; }
-                        else if (nint == 1) { v1s = js; v1e = je; i1 = id; }
-                        else if (nint == 2) { v2s = js; v2e = je; i2 = id; }
-                        else if (nint == 3) { v3s = js; v3e = je; i3 = id; }
-                        ++nint;
+                    const int32_t js = __builtin_amdgcn_readlane(bs, j);
+                    const int32_t je = __builtin_amdgcn_readlane(be, j);
+                    const uint32_t id = b0 + j;
+                    if (je > s_rel && je <= e_rel) {
+                        const int32_t c = je - s_rel;
+                        if (ncut == 0) { c0 = c; i0 = id; }
+                        else if (ncut == 1) { c1 = c; i1 = id; }
+                        else if (ncut == 2) { c2 = c; i2 = id; }
+                        else if (ncut == 3) { c3 = c; i3 = id; }
+                        ++ncut;
                     }
+                    if (js < e_rel && je > e_rel) t = id;
                 }
             }
         }
 
-        uint32_t crc = 0, first_cut = kNone32;
         int q = 0;
-        int32_t cvs = v0s, cve = v0e;
         uint32_t cid = i0;
+        int32_t cc = c0;
+        int32_t cj = (cc - 1) >> 2;  // word holding the record's last byte (99 -> never)
+        uint32_t crc = 0, first_cut = kNone32;
         const uint32_t words[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w,
                                     d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-            const int32_t o = s_rel + 4 * j;
-            const int32_t lo = min(max(cvs - o, 0), 4), hi = min(max(cve - o, 0), 4);
-            crc = slice4(lds, l31, crc ^ (words[j] & bytemask(lo, hi)));
-            if (cve > o && cve <= o + 4) {  // this word holds the value's last byte
-                out_e[cid] = crc;
+            const uint32_t x = words[j];
+            uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
+                                     : slice4(lds, l31, crc ^ x);
+            if (j == cj) {  // a record ends in this word: close it exactly (byte-wise for 1-3 bytes)
+                const int nb = cc - 4 * j;
+                if (nb < 4) {
+                    nc = crc;
+                    uint32_t y = x;
+                    for (int b = 0; b < nb; ++b) {
+                        nc = lds[(((nc ^ y) & 0xFFu) << 5) | l31] ^ (nc >> 8);
+                        y >>= 8;
+                    }
+                }
+                out_e[cid] = nc;
                 if (first_cut == kNone32) first_cut = cid;
-                else out_pre[cid] = 0;     // started inside this slab: nothing before it
-                crc = 0;
+                else out_pre[cid] = 0;  // started inside this slab: nothing before it
+                nc = 0;
                 ++q;
-                cvs = q == 1 ? v1s : q == 2 ? v2s : q == 3 ? v3s : BIG;
-                cve = q == 1 ? v1e : q == 2 ? v2e : q == 3 ? v3e : BIG;
                 cid = q == 1 ? i1 : q == 2 ? i2 : i3;
+                cc = q == 1 ? c1 : q == 2 ? c2 : c3;
+                cj = (cc - 1) >> 2;
             }
+            crc = nc;
         }
-        const bool tail = q < nint && cvs < s_rel + kSlab && cve > s_rel + kSlab;
-        const uint32_t t = tail ? cid : kNone32;
-        const uint32_t z = tail ? crc : 0u;
-        // Z_{64(63-lane)}(z): reference the open tail to the row end
-        uint32_t cz = 0;
+        const uint32_t z = t != kNone32 ? crc : 0u;
+        if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
+            asm volatile("" ::"v"(crc), "v"(z));
+            if (lane == 63) out_rend[row] = crc ^ t;
+        } else {
+            // Z_{64(63-lane)}(z): reference the open register to the row end
+            uint32_t cz = 0;
 #pragma unroll
-        for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
-        // segmented XOR over runs of equal t
-        uint32_t P = cz;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t v = __shfl_up(P, d);
-            if ((int)lane >= d) P ^= v;
+            for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
+            // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
+            uint32_t P = cz;
+            P ^= dpp<0x111, 0xF>(P);  // row_shr:1
+            P ^= dpp<0x112, 0xF>(P);  // row_shr:2
+            P ^= dpp<0x114, 0xF>(P);  // row_shr:4
+            P ^= dpp<0x118, 0xF>(P);  // row_shr:8
+            P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
+            P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
+            const uint32_t tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
+            const bool start = lane == 0 || t != tprev;
+            const uint64_t B = __ballot(start);
+            const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+            const int rsl = 63 - __clzll((long long)(B & upto));
+            const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
+            const uint32_t runv = P ^ (rsl > 0 ? Pp : 0u);
+            const uint32_t runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
+            if (lane == 63) out_rend[row] = t != kNone32 ? runv : 0u;
+            if (first_cut != kNone32) out_pre[first_cut] = (lane > 0 && tprev == first_cut) ? runprev : 0u;
         }
-        const uint32_t tprev = __shfl_up(t, 1);
-        const bool start = lane == 0 || t != tprev;
-        const uint64_t B = __ballot(start);
-        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        const int rsl = 63 - __clzll((long long)(B & upto));
-        const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
-        const uint32_t runv = P ^ (rsl > 0 ? Pp : 0u);
-        const uint32_t runprev = __shfl_up(runv, 1);
-        if (lane == 63) out_rend[row] = t != kNone32 ? runv : 0u;
-        if (first_cut != kNone32) out_pre[first_cut] = (lane > 0 && tprev == first_cut) ? runprev : 0u;
+
+        if (nrow >= n_rows) break;
+        row = nrow;
+        nrow = nnrow;
+        ra = nra;
+        rb = nrb;
+        nra = nnra;
+        nrb = nnrb;
+        d0 = n0;
+        d1 = n1;
+        d2 = n2;
+        d3 = n3;
+        cur = nxt;
     }
 }
 
-// Per record: stitch rows (Horner with Z_4096), undo the masked tail bytes
-// (Z_-m), add the init/xorout term, compare with the header CRC
-// (core/db.go:311), compute ValuePos = lastOffset + 16 + KeySize mod 2^32
-// (core/keydir.go:25, lastOffset = carry + offset within the file).
-__global__ __launch_bounds__(256) void k_finalize(const uint64_t *__restrict__ rec_off,
+// Per record (core/db.go:311 applied to every record):
+//   chain = F(0, [align4(start), end)) = e ^ Z_-(row_end-end)(stitched runs),
+//           runs stitched over rows by Horner with Z_4096 (LDS byte tables);
+//   F(0, value) = chain ^ Z_V(F(0, prefix)), prefix = header bytes from
+//           align4(start) plus the key (bytes the chain saw before the value);
+//   crc = F(0, value) ^ crc32(0^V)  (table for V < 2^17).
+// ValuePos = lastOffset + 16 + KeySize mod 2^32 (core/keydir.go:25), with
+// lastOffset = carry + offset within the file.
+__global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ arena,
+                                                  const uint64_t *__restrict__ rec_off,
                                                   const uint4 *__restrict__ rec_hdr,
                                                   const uint32_t *__restrict__ rec_file,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint32_t *__restrict__ carry, uint64_t n_total,
                                                   const uint32_t *__restrict__ e, const uint32_t *__restrict__ pre,
                                                   const uint32_t *__restrict__ rend,
-                                                  const uint32_t *__restrict__ xinv, const uint32_t *__restrict__ xa,
-                                                  const uint32_t *__restrict__ xb, uint32_t x_row,
-                                                  gck_rec *__restrict__ out, uint32_t *counters) {
+                                                  const uint32_t *__restrict__ g_slice,
+                                                  const uint32_t *__restrict__ xinv, const uint32_t *__restrict__ zrow,
+                                                  const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
+                                                  const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
+                                                  uint32_t *counters) {
+    __shared__ uint32_t Tz[1024];
+    __shared__ uint32_t T0[256];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) Tz[i] = zrow[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) T0[i] = g_slice[i];
+    __syncthreads();
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool reject = false;
     if (r < n_total) {
-        const uint64_t off = rec_off[r];
+        const uint64_t start = rec_off[r];
         const uint4 h = rec_hdr[r];
         const uint32_t f = rec_file[r];
-        const uint64_t vs = off + 16 + h.z, L = h.w, ve = vs + L;
-        uint32_t raw0 = 0;
-        if (L) {
-            const uint64_t fr = vs / kRow, lr = (ve - 1) / kRow;
-            uint32_t acc = 0;
-            for (uint64_t row = fr; row < lr; ++row) acc = multmodp(x_row, acc) ^ rend[row];
-            acc = multmodp(x_row, acc) ^ pre[r];
-            const uint64_t row_end = (lr + 1) * kRow;
-            raw0 = multmodp(xinv[(4 - (ve & 3)) & 3], e[r]) ^ multmodp(xinv[row_end - ve], acc);
+        const uint32_t V = h.w;
+        const uint64_t vs = start + 16 + h.z, ve = vs + V;
+        const uint64_t w0 = (start + 3) & ~3ull;
+        const uint64_t fr = w0 / kRow, lr = (ve - 1) / kRow;
+        uint32_t acc = 0;
+        for (uint64_t row = fr; row <= lr; ++row) {
+            acc = Tz[acc & 0xFF] ^ Tz[256 + ((acc >> 8) & 0xFF)] ^ Tz[512 + ((acc >> 16) & 0xFF)] ^ Tz[768 + (acc >> 24)];
+            acc ^= row < lr ? rend[row] : pre[r];
         }
-        const uint32_t zl = multmodp(multmodp(xa[L >> 16], xb[L & 0xFFFF]), 0xFFFFFFFFu);
-        const uint32_t calc = raw0 ^ zl ^ 0xFFFFFFFFu;
-        const uint64_t fo = off - fbase[f];
+        const uint64_t row_end = (lr + 1) * kRow;
+        const uint32_t chain = e[r] ^ (acc ? multmodp(xinv[row_end - ve], acc) : 0u);
+        // F(0, prefix): header bytes [w0 - start, 16) then the key
+        uint32_t p = 0;
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+        for (uint32_t i = (uint32_t)(w0 - start); i < 16; ++i)
+            p = T0[(p ^ (hw[i >> 2] >> (8 * (i & 3)))) & 0xFF] ^ (p >> 8);
+        const uint8_t *key = arena + start + 16;
+        for (uint32_t i = 0; i < h.z; ++i) p = T0[(p ^ key[i]) & 0xFF] ^ (p >> 8);
+        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
+        const uint32_t raw0 = chain ^ (p ? multmodp(xv, p) : 0u);
+        const uint32_t z = V < (1u << 17) ? zl[V] : multmodp(multmodp(xa[V >> 16], xb[V & 0xFFFF]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        const uint32_t calc = raw0 ^ z;
+        const uint64_t fo = start - fbase[f];
         const bool tomb = h.z == 0;
         gck_rec o;
         o.rec_off = fo;
@@ -577,7 +686,8 @@ __global__ __launch_bounds__(256) void k_finalize(const uint64_t *__restrict__ r
 
 // ------------------------------------------------------------- host side ---
 static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib, std::vector<uint32_t> &xinv,
-                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, uint32_t &x_row) {
+                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
+                        std::vector<uint32_t> &zl) {
     slice.assign(4 * 256, 0);
     for (uint32_t n = 0; n < 256; ++n) {
         uint32_t c = n;
@@ -606,10 +716,17 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
         xa[i] = multmodp(xa[i - 1], s16);
         xb[i] = multmodp(xb[i - 1], s1);
     }
-    x_row = xpow8n(kRow);
+    const uint32_t x_row = xpow8n(kRow);
+    zrow.assign(1024, 0);
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t b = 1; b < 256; ++b) zrow[k * 256 + b] = multmodp(x_row, b << (8 * k));
+    zl.assign(1u << 17, 0);  // crc32 of L zero bytes
+    uint32_t st = 0xFFFFFFFFu;
+    for (uint32_t L = 0; L < (1u << 17); ++L) {
+        zl[L] = st ^ 0xFFFFFFFFu;
+        st = slice[st & 0xff] ^ (st >> 8);
+    }
 }
-
-static uint32_t g_xrow = 0;
 
 static int ctx_init(Ctx *c, const gck_opts *o) {
     gck_opts d{};
@@ -643,13 +760,16 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
-    std::vector<uint32_t> slice, nib, xinv, xa, xb;
-    make_tables(slice, nib, xinv, xa, xb, g_xrow);
+    std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow, zl;
+    make_tables(slice, nib, xinv, xa, xb, zrow, zl);
     int rc;
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
-        (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_counters.ensure(64)))
+        (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
+        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)))
         return rc;
+    GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
+    GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_slice.p, slice.data(), slice.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xinv.p, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
@@ -661,10 +781,10 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
 static void ctx_free(Ctx *c) {
     DBuf *all[] = {&c->arena, &c->d_fbase, &c->d_flen, &c->d_ffirst, &c->d_fnch, &c->d_fbad, &c->d_fterm,
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
-                   &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos,
+                   &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend,
-                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb};
+                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -715,7 +835,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_file.ensure((nc + 1) * 4)) || (rc = c->d_ch_start.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_end.ensure((nc + 1) * 8)) || (rc = c->d_ch_entry.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
-        (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) ||
+        (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 1) * 4)))
@@ -763,48 +883,83 @@ static int ctx_run(Ctx *c) {
                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, nc);
     }
     GCK_HIP(hipEventRecord(c->ev[PH_VALIDATE], s));
-    if (nc) {
+    // validation rounds: validate -> fixup -> validate -> fixup -> validate
+    auto validate = [&](uint32_t *counter) {
         k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
                                                  c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
                                                  c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-                                                 c->d_ffirst.as<uint32_t>(), c->d_fbad.as<uint32_t>(), cnt, nc);
-        k_fixup<<<nblk(nf, 64), 64, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
-                                            c->d_flen.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
-                                            c->d_fnch.as<uint32_t>(), c->d_fbad.as<uint32_t>(),
-                                            c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                            c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
-                                            c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                            c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, nf,
-                                            cnt);
-    }
-    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
+                                                 c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(), counter, nc);
+    };
+    auto fixup = [&]() {
+        k_fixup<<<nblk(nc, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
+                                              c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
+                                              c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
+                                              c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
+                                              c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
+                                              c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
+                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, nc,
+                                              cnt + 1);
+    };
+    constexpr int kRounds = 2;
     if (nc) {
-        k_scan_chunks<<<1, 1024, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), nc);
-    } else {
-        GCK_HIP(hipMemsetAsync(c->d_rec_base.p, 0, 8, s));
+        for (int r = 0; r < kRounds; ++r) {
+            validate(cnt + 8 + r);
+            fixup();
+        }
+        validate(cnt + 8 + kRounds);
     }
-    if (nf) {
-        k_file_summary<<<nblk(nf, 64), 64, 0, s>>>(c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(),
-                                                   c->d_rec_base.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                   c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                                   c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(),
-                                                   c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(), nf);
-    }
+    auto summarize = [&]() {
+        if (nc) {
+            k_scan_chunks<<<1, 1024, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), nc);
+        } else {
+            (void)hipMemsetAsync(c->d_rec_base.p, 0, 8, s);
+        }
+        if (nf) {
+            k_file_summary<<<nblk(nf, 64), 64, 0, s>>>(c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(),
+                                                       c->d_rec_base.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
+                                                       c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
+                                                       c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(),
+                                                       c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(), nf);
+        }
+    };
+    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
+    summarize();
     GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
 
     // ---- host: EOF classification + lastOffset carries (core/db.go:110-140) ----
     std::vector<uint32_t> fterm(nf), carry(nf);
     std::vector<uint64_t> ftpos(nf), ffirst(nf), fnrec(nf);
-    uint32_t hc[4] = {0, 0, 0, 0};
     if (nf) {
         GCK_HIP(hipMemcpyAsync(fterm.data(), c->d_fterm.p, nf * 4, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipMemcpyAsync(ftpos.data(), c->d_ftpos.p, nf * 8, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipMemcpyAsync(ffirst.data(), c->d_ffirstrec.p, nf * 8, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipMemcpyAsync(fnrec.data(), c->d_fnrec.p, nf * 8, hipMemcpyDeviceToHost, s));
     }
-    GCK_HIP(hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, s));
+    uint32_t hcnt[16] = {};
+    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
-    c->n_fixups = hc[1];
+    // rare: inconsistencies left after the device rounds (cascading mis-speculation)
+    for (uint32_t left = hcnt[8 + kRounds]; left;) {
+        fixup();
+        GCK_HIP(hipMemsetAsync(cnt + 15, 0, 4, s));
+        validate(cnt + 15);
+        uint32_t v = 0;
+        GCK_HIP(hipMemcpyAsync(&v, cnt + 15, 4, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        left = v;
+        if (!left) {
+            summarize();
+            if (nf) {
+                GCK_HIP(hipMemcpyAsync(fterm.data(), c->d_fterm.p, nf * 4, hipMemcpyDeviceToHost, s));
+                GCK_HIP(hipMemcpyAsync(ftpos.data(), c->d_ftpos.p, nf * 8, hipMemcpyDeviceToHost, s));
+                GCK_HIP(hipMemcpyAsync(ffirst.data(), c->d_ffirstrec.p, nf * 8, hipMemcpyDeviceToHost, s));
+                GCK_HIP(hipMemcpyAsync(fnrec.data(), c->d_fnrec.p, nf * 8, hipMemcpyDeviceToHost, s));
+            }
+            GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
+            GCK_HIP(hipStreamSynchronize(s));
+        }
+    }
+    c->n_fixups = hcnt[1];
     c->status = GCK_OK;
     c->err_file = 0;
     c->err_off = 0;
@@ -857,7 +1012,7 @@ static int ctx_run(Ctx *c) {
     if (c->n_rows && n_total) {
         const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-        k_crc_rows<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_row_first.as<uint32_t>(), n_total,
+        k_crc_rows<0><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_row_first.as<uint32_t>(), n_total,
                                          c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                          c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
                                          c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
@@ -865,17 +1020,18 @@ static int ctx_run(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     if (n_total) {
         k_finalize<<<nblk(n_total, 256), 256, 0, s>>>(
-            c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), c->d_rec_file.as<uint32_t>(),
+            c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), c->d_rec_file.as<uint32_t>(),
             c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(), n_total, c->d_e.as<uint32_t>(),
-            c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_xa.as<uint32_t>(),
-            c->d_xb.as<uint32_t>(), g_xrow, c->d_out.as<gck_rec>(), cnt);
+            c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>(), c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
+            c->d_zrow.as<uint32_t>(),
+            c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(), c->d_out.as<gck_rec>(), cnt);
     }
     GCK_HIP(hipEventRecord(c->ev[PH_COUNT], s));
-    GCK_HIP(hipMemcpyAsync(hc, cnt, 16, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
     GCK_HIP(hipGetLastError());
-    c->n_overflow = hc[2];
-    c->n_crc_fail = hc[3];
+    c->n_overflow = hcnt[2];
+    c->n_crc_fail = hcnt[3];
     for (int p = 0; p < PH_COUNT; ++p) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
@@ -1027,5 +1183,45 @@ int gck_device_count(void) {
 const char *gck_version(void) { return "gocask_hip 0.1 (gfx950)"; }
 
 const char *gck_last_error(void) { return gck::last_error(); }
+
+// Measurement helper: time ablated variants of k_crc_rows on the state left by
+// the last gck_ctx_run (outputs are clobbered; rerun before fetching).
+// mode bits: 1 = no record intervals, 2 = no LDS table chain, 4 = no tail
+// shift / segmented scan.
+int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
+    if (!ctx || iters <= 0 || mode < 0 || mode > 7) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    if (!c->n_rows || !c->n_recs) return GCK_EINVAL;
+    GCK_HIP(hipSetDevice(c->device));
+    const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
+    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) {
+#define GCK_VARIANT(M)                                                                                              \
+    case M:                                                                                                         \
+        k_crc_rows<M><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_row_first.as<uint32_t>(), \
+                                                    c->n_recs, c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),   \
+                                                    c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),                 \
+                                                    c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
+                                                    c->d_rend.as<uint32_t>());                                          \
+        break;
+        switch (mode) {
+            GCK_VARIANT(0) GCK_VARIANT(1) GCK_VARIANT(2) GCK_VARIANT(3) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6)
+            GCK_VARIANT(7)
+        }
+#undef GCK_VARIANT
+    }
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_per_iter = ms / iters;
+    return GCK_OK;
+}
 
 }  // extern "C"

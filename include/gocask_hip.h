@@ -126,6 +126,13 @@ const char *gck_phase_name(int phase);
  * HIP stream the pipeline runs on (hipStream_t, as void*). */
 int gck_ctx_device_recs(gck_ctx *ctx, const gck_rec **recs, uint64_t *n);
 void *gck_ctx_stream(gck_ctx *ctx);
+/* Measurement helper (not on the replay path): time a plain streaming read of
+ * the resident arena, the practical HBM read ceiling k_crc_rows is compared to. */
+int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs);
+/* Measurement helper: time ablated variants of the CRC kernel on the last run's
+ * state (mode bits 1 = no record intervals, 2 = no LDS table chain, 4 = no
+ * tail shift / segmented scan).  Clobbers the last run's outputs. */
+int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter);
 /* Copy `len` bytes of file `file` (as resident in the arena) back to host. */
 int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, uint64_t len);
 

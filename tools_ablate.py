@@ -1,0 +1,18 @@
+"""Ablation timing of k_crc_rows variants (diagnostic; not part of the bench)."""
+import ctypes, json, sys
+sys.path.insert(0, ".")
+import gocask_amd as g
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
+import bench
+ctx = g.ReplayContext()
+ctx.encode(**bench.CONFIGS[cfg])
+for _ in range(3):
+    ctx.run()
+st = ctx.stats()
+out = {"cfg": cfg, "bytes": st["bytes"], "phase_ms": st["ms_phase"], "stream": ctx.stream_read_ceiling(5)}
+ms = ctypes.c_double()
+for mode in range(8):
+    g._lib.check(ctx._L.gck_diag_crc_variant(ctx._h, mode, 5, ctypes.byref(ms)))
+    out[f"mode{mode}_ms"] = round(ms.value, 3)
+    out[f"mode{mode}_gbs"] = round(st["bytes"] / ms.value / 1e6, 1)
+print(json.dumps(out))
