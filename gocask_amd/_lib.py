@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgocask_hip.so")
+LIB_PATH = os.environ.get("GCK_LIB_PATH") or os.path.join(HERE, "libgocask_hip.so")
 
 GCK_OK = 0
 GCK_EUNEXPECTED_EOF = 1

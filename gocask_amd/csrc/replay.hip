@@ -408,6 +408,45 @@ __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *_
         for (uint64_t row = hi; row <= n_rows; ++row) row_first[row] = (uint32_t)n_total;
 }
 
+constexpr int kPlanWords = 16;  // 64 B per row
+constexpr int kPlanEnds = 28;   // record ends stored inline; more -> slow path
+
+// Per-row plan for k_crc_rows, read with scalar loads (no vector-memory wait
+// couples it to the row data):
+//   w0     ra = first record whose end lies past the row start
+//   w1     n_ends (records ending inside the row) | tail_start << 16, where
+//          tail_start = row-relative start of record ra + n_ends (the record
+//          open at the row end), kRow if there is none
+//   w2..15 row-relative end offsets (1..kRow) of records ra .. ra+27 as u16
+__global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
+                           uint64_t n_total, uint64_t n_rows, const uint32_t *__restrict__ row_first,
+                           uint4 *__restrict__ plan, uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+    const uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n_rows) return;
+    const uint32_t ra = row_first[row], rb = row_first[row + 1];
+    const uint64_t rs = row * kRow;
+    const uint32_t n = rb - ra;
+    uint32_t w[kPlanWords];
+#pragma unroll
+    for (int i = 0; i < kPlanWords; ++i) w[i] = 0;
+    uint32_t tail = kRow;
+    if (rb < n_total) {
+        const int64_t st = (int64_t)rec_off[rb] - (int64_t)rs;
+        tail = (uint32_t)max(min(st, (int64_t)kRow), (int64_t)0);
+    }
+    w[0] = ra;
+    w[1] = min(n, 0xFFFFu) | (tail << 16);
+    if (n > (uint32_t)kPlanEnds) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
+    const uint32_t m = min(n, (uint32_t)kPlanEnds);
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint32_t end = (uint32_t)(value_end(rec_off, rec_hdr, ra + i) - rs);
+        w[2 + i / 2] |= end << (16 * (i & 1));
+    }
+#pragma unroll
+    for (int i = 0; i < kPlanWords / 4; ++i)
+        plan[row * (kPlanWords / 4) + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
 // Slicing-by-4 step through the LDS tables.  Table t, entry b, copy l31 lives
 // at index t*8192 + b*32 + l31: every lane of a 32-lane LDS group reads its own
 // bank, so the lookups are bank-conflict free (MI355X_MICROARCH.md §LDS).
@@ -441,173 +480,327 @@ __device__ __forceinline__ void to_span(const RawRec &x, uint64_t rs, int32_t &s
     ve_out = (int32_t)max(min(ve, (int64_t)kRow + 1), (int64_t)-1);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef GCK_NT
+#define GCK_NT 0
+#endif
+#ifndef GCK_DEPTH
+#define GCK_DEPTH 1
+#endif
+
+// 16-byte row load (GCK_NT: non-temporal hint, the row bytes are read once).
+__device__ __forceinline__ uint4 ld_stream(const uint8_t *p) {
+#if GCK_NT
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *reinterpret_cast<const uint4 *>(p);
+#endif
+}
+
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xF, false);
 }
 
+// LDS image of the CRC tables (identical in every k_crc_rows* workgroup).
+__device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__restrict__ g_slice,
+                                             const uint32_t *__restrict__ g_nib) {
+    for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) lds[i] = g_slice[(i >> 13) * 256 + ((i >> 5) & 255)];
+    for (uint32_t i = threadIdx.x; i < 8192; i += blockDim.x) {
+        const uint32_t l = (i >> 12) * 32 + (i & 31), v = (i >> 5) & 15, q = (i >> 9) & 7;
+        lds[kNibBase + i] = g_nib[(l * 8 + q) * 16 + v];
+    }
+    __syncthreads();
+}
+
+// Per-lane state of one row (see k_crc_rows).
+struct RowCuts {
+    int ncut = 0;
+    int32_t c0 = 99, c1 = 99, c2 = 99, c3 = 99;  // record end offsets inside the slab (1..64); named
+    uint32_t id0 = 0, id1 = 0, id2 = 0, id3 = 0;  // registers, never an indexed array (no scratch)
+    uint32_t n_le = 0;                             // record ends at or before the slab end
+    int32_t my_end = 0;                            // row-relative end of record ra + lane
+    __device__ __forceinline__ void take(uint32_t end, uint32_t j, uint32_t ra, uint32_t lane, int32_t s_rel) {
+        const int32_t cc = (int32_t)end - s_rel;
+        if (cc > 0 && cc <= kSlab) {
+            const uint32_t id = ra + j;
+            c0 = ncut == 0 ? cc : c0;
+            c1 = ncut == 1 ? cc : c1;
+            c2 = ncut == 2 ? cc : c2;
+            c3 = ncut == 3 ? cc : c3;
+            id0 = ncut == 0 ? id : id0;
+            id1 = ncut == 1 ? id : id1;
+            id2 = ncut == 2 ? id : id2;
+            id3 = ncut == 3 ? id : id3;
+            ++ncut;
+        }
+        n_le += (int32_t)end <= s_rel + kSlab ? 1u : 0u;
+        my_end = lane == j ? (int32_t)end : my_end;
+    }
+};
+
+struct RowOut {
+    uint32_t e[4] = {0, 0, 0, 0};  // register at each record end in the slab
+    uint32_t pre_first = 0;         // run just before the first record end of the slab
+    uint32_t rend = 0;              // (lane 63) run open at the row end
+};
+
+// The per-row work of k_crc_rows: every byte of the slab enters the CRC
+// register; it is closed at each record end (exactly: the last partial word
+// byte-wise), the open register at the slab end is shifted to the row end and
+// a segmented XOR over the wave joins each record's lanes.
+template <int MODE>
+__device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, uint32_t l31, uint32_t nbase,
+                                          int32_t s_rel, uint64_t rs, uint32_t (&words)[16], const RowCuts &rc,
+                                          uint32_t t) {
+    RowOut o;
+    int q = 0;
+    int32_t cc = rc.c0, n1 = rc.c1, n2 = rc.c2, n3 = rc.c3;  // pending cuts, shifted down at each cut
+    int32_t cj = (cc - 1) >> 2;  // word holding the record's last byte (99 -> never)
+    uint32_t crc = 0;
+    if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded row
+#pragma unroll
+        for (int j = 0; j < 16; ++j) words[j] = (uint32_t)(rs >> 4) * 2654435761u + lane * 97u + j;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t x = words[j];
+        uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
+                                 : slice4(lds, l31, crc ^ x);
+        if (j == cj) {
+            const int nb = cc - 4 * j;
+            if (nb < 4) {
+                nc = crc;
+                uint32_t y = x;
+                for (int b = 0; b < nb; ++b) {
+                    nc = lds[(((nc ^ y) & 0xFFu) << 5) | l31] ^ (nc >> 8);
+                    y >>= 8;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o.e[k] = q == k ? nc : o.e[k];
+            nc = 0;
+            ++q;
+            cc = n1;
+            n1 = n2;
+            n2 = n3;
+            n3 = 99;
+            cj = (cc - 1) >> 2;
+        }
+        crc = nc;
+    }
+    const uint32_t z = t != kNone32 ? crc : 0u;
+    o.rend = crc ^ t;
+    if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
+        asm volatile("" ::"v"(crc), "v"(z));
+    } else {
+        // Z_{64(63-lane)}(z): reference the open register to the row end
+        uint32_t cz = 0;
+#pragma unroll
+        for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
+        // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
+        uint32_t P = cz;
+        P ^= dpp<0x111, 0xF>(P);  // row_shr:1
+        P ^= dpp<0x112, 0xF>(P);  // row_shr:2
+        P ^= dpp<0x114, 0xF>(P);  // row_shr:4
+        P ^= dpp<0x118, 0xF>(P);  // row_shr:8
+        P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
+        P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
+        const uint32_t tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
+        const bool start = lane == 0 || t != tprev;
+        const uint64_t B = __ballot(start);
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        const int rsl = 63 - __clzll((long long)(B & upto));
+        const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
+        const uint32_t runv = P ^ (rsl > 0 ? Pp : 0u);
+        const uint32_t runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
+        o.rend = t != kNone32 ? runv : 0u;
+        // the first record closing in this slab continues the run of the lane before
+        o.pre_first = (rc.ncut > 0 && lane > 0 && tprev == rc.id0) ? runprev : 0u;
+    }
+    return o;
+}
+
+// 16-byte load issued by inline asm: the compiler neither tracks nor waits for
+// it; k_crc_rows waits explicitly (see there).
+__device__ __forceinline__ void ld_async(u32x4 &x, const uint8_t *p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
+}
+
 // The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns bytes
 // [64k, 64k+64).  Every byte enters a CRC register, no masking: records tile
 // the file, so lane k's register simply runs over whole records and is closed
-// exactly at every record end (the last partial word byte-wise) and restarted
-// at the next word.  The chain of record r therefore covers
-// [align4(start_r), end_r) = header/key prefix || value; k_finalize removes the
-// prefix by linearity.  An open register at the slab end belongs to the record
-// containing that position; it is referenced to the row end with the per-lane
-// constant shift Z_{64(63-k)} (8 nibble lookups) and a segmented XOR over the
-// wave (DPP prefix scan) joins each record's lanes.  Outputs: e per record
-// (state at its end, carry-free), pre per record (its run just before the cut
-// lane), per row the run open at the row end.  Loads for row i+1 (data,
-// candidate records) and row_first of row i+2 are issued before row i is
-// processed.  MODE != 0 are ablation variants for gck_diag_crc_variant.
+// exactly at every record end and restarted at the next word.  The chain of
+// record r therefore covers [align4(start_r), end_r) = header/key prefix ||
+// value; k_finalize removes the prefix by linearity.  An open register at the
+// slab end belongs to the record containing that position; it is referenced to
+// the row end with the per-lane constant shift Z_{64(63-k)} (8 nibble lookups)
+// and a segmented XOR over the wave (DPP prefix scan) joins each record's
+// lanes.  Outputs: e and pre per record (gathered so lane j stores record
+// ra+j: two coalesced stores per row), the run open at the row end per row.
+//
+// Memory pipeline: the row plan (k_row_plan) comes by scalar loads two rows
+// ahead; the row data by inline-asm loads one row ahead.  The only compiler-
+// visible vector-memory ops are the 3 stores per row, so the compiler inserts
+// no vmcnt waits; the single explicit `s_waitcnt vmcnt(0)` sits after the row
+// is processed and before its stores, where everything outstanding (the next
+// row's data and the previous row's stores) was issued a whole row earlier.
+// Rows where more than kPlanEnds records end are left to k_crc_rows_big (their
+// stores here go to scratch slots so the per-row store count stays fixed).
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint32_t *__restrict__ row_first, uint64_t n_total,
-                                                   const uint64_t *__restrict__ rec_off,
-                                                   const uint4 *__restrict__ rec_hdr,
+                                                   const uint32_t *__restrict__ plan, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib,
                                                    uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
                                                    uint32_t *__restrict__ out_rend) {
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
-    for (uint32_t i = threadIdx.x; i < 32768; i += 1024) lds[i] = g_slice[(i >> 13) * 256 + ((i >> 5) & 255)];
-    for (uint32_t i = threadIdx.x; i < 8192; i += 1024) {
-        const uint32_t l = (i >> 12) * 32 + (i & 31), v = (i >> 5) & 15, q = (i >> 9) & 7;
-        lds[kNibBase + i] = g_nib[(l * 8 + q) * 16 + v];
-    }
-    __syncthreads();
-
+    fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
-    const int32_t s_rel = (int32_t)lane * kSlab, e_rel = s_rel + kSlab;
+    const int32_t s_rel = (int32_t)lane * kSlab;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
-    const uint64_t last_rec = n_total - 1;  // only launched with n_total > 0
 
-    uint64_t row = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+    uint64_t row = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     if (row >= n_rows) return;
-    uint32_t ra = row_first[row], rb = row_first[row + 1];
-    uint64_t nrow = row + stride;
-    const uint64_t nrow_c = min(nrow, n_rows - 1);
-    uint32_t nra = row_first[nrow_c], nrb = row_first[nrow_c + 1];
-    // lanes past the row's last candidate load the last one again (same line)
-    RawRec cur = load_raw(rec_off, rec_hdr, min((uint64_t)ra + lane, min((uint64_t)rb, last_rec)));
-    const uint4 *src = reinterpret_cast<const uint4 *>(arena + row * kRow + s_rel);
-    uint4 d0 = src[0], d1 = src[1], d2 = src[2], d3 = src[3];
+    auto ldplan = [&](uint64_t r, uint32_t (&w)[kPlanWords]) {
+        const uint32_t *p_ = plan + min(r, n_rows - 1) * kPlanWords;
+#pragma unroll
+        for (int i = 0; i < kPlanWords; ++i) w[i] = p_[i];
+    };
+    auto ldrow = [&](uint64_t r, u32x4 (&x)[4]) {
+        const uint8_t *p_ = arena + min(r, n_rows - 1) * kRow + s_rel;
+        ld_async(x[0], p_);
+        ld_async(x[1], p_ + 16);
+        ld_async(x[2], p_ + 32);
+        ld_async(x[3], p_ + 48);
+    };
+    uint32_t pw[kPlanWords], pw1[kPlanWords];
+    ldplan(row, pw);
+    ldplan(row + stride, pw1);
+    u32x4 d[4], nx[4] = {};
+    ldrow(row, d);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 
     for (;;) {
         const uint64_t rs = row * kRow;
-        // ---- issue: row_first of row i+2, candidates and data of row i+1 (all
-        // unconditional, clamped indices, so the waits stay counted)
-        const uint64_t nnrow = nrow + stride;
-        const uint64_t nnrow_c = min(nnrow, n_rows - 1);
-        const uint32_t nnra = row_first[nnrow_c], nnrb = row_first[nnrow_c + 1];
-        const RawRec nxt = load_raw(rec_off, rec_hdr, min((uint64_t)nra + lane, min((uint64_t)nrb, last_rec)));
-        const uint4 *ns = reinterpret_cast<const uint4 *>(arena + min(nrow, n_rows - 1) * kRow + s_rel);
-        const uint4 n0 = ns[0], n1 = ns[1], n2 = ns[2], n3 = ns[3];
+        const uint64_t row1 = row + stride;
+        // ---- issue the next row's data and the plan of the row after it
+        if constexpr ((MODE & 8) == 0) ldrow(row1, nx);
+        uint32_t pw2[kPlanWords];
+        ldplan(row1 + stride, pw2);
 
-        // ---- record ends inside this slab (<= 4) and the record open at its end
-        int ncut = 0;
-        int32_t c0 = 99, c1 = 99, c2 = 99, c3 = 99;  // end offset within the slab, 1..64
-        uint32_t i0 = 0, i1 = 0, i2 = 0, i3 = 0;
-        uint32_t t = kNone32;
-        if (!(MODE & 1) && ra < n_total) {
-            const uint32_t last = rb < n_total ? rb : (uint32_t)last_rec;
-            for (uint32_t b0 = ra; b0 <= last; b0 += 64) {
-                int32_t bs, be;
-                if (b0 == ra) to_span(cur, rs, bs, be);
-                else to_span(load_raw(rec_off, rec_hdr, min((uint64_t)b0 + lane, (uint64_t)last)), rs, bs, be);
-                const uint32_t cnt = min(64u, last - b0 + 1);
-                for (uint32_t j = 0; j < cnt; ++j) {
-                    const int32_t js = __builtin_amdgcn_readlane(bs, j);
-                    const int32_t je = __builtin_amdgcn_readlane(be, j);
-                    const uint32_t id = b0 + j;
-                    if (je > s_rel && je <= e_rel) {
-                        const int32_t c = je - s_rel;
-                        if (ncut == 0) { c0 = c; i0 = id; }
-                        else if (ncut == 1) { c1 = c; i1 = id; }
-                        else if (ncut == 2) { c2 = c; i2 = id; }
-                        else if (ncut == 3) { c3 = c; i3 = id; }
-                        ++ncut;
-                    }
-                    if (js < e_rel && je > e_rel) t = id;
-                }
+        const uint32_t ra = pw[0], n_ends = pw[1] & 0xFFFFu, tail_start = pw[1] >> 16;
+        const bool small = n_ends <= (uint32_t)kPlanEnds;  // wave-uniform
+        RowCuts rc;
+        if constexpr ((MODE & 1) == 0) {
+#pragma unroll
+            for (int j = 0; j < kPlanEnds; ++j) {
+                if ((uint32_t)j >= n_ends) break;
+                rc.take((pw[2 + j / 2] >> (16 * (j & 1))) & 0xFFFFu, j, ra, lane, s_rel);
             }
         }
-
-        int q = 0;
-        uint32_t cid = i0;
-        int32_t cc = c0;
-        int32_t cj = (cc - 1) >> 2;  // word holding the record's last byte (99 -> never)
-        uint32_t crc = 0, first_cut = kNone32;
-        const uint32_t words[16] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w,
-                                    d2.x, d2.y, d2.z, d2.w, d3.x, d3.y, d3.z, d3.w};
+        // the record open at the slab end: the next one after the ends counted;
+        // it exists if it ends inside the row, or it is the row's tail record and
+        // starts before the slab end (not padding after a file's last record)
+        const uint32_t t = (rc.n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + rc.n_le : kNone32;
+        uint32_t words[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const uint32_t x = words[j];
-            uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
-                                     : slice4(lds, l31, crc ^ x);
-            if (j == cj) {  // a record ends in this word: close it exactly (byte-wise for 1-3 bytes)
-                const int nb = cc - 4 * j;
-                if (nb < 4) {
-                    nc = crc;
-                    uint32_t y = x;
-                    for (int b = 0; b < nb; ++b) {
-                        nc = lds[(((nc ^ y) & 0xFFu) << 5) | l31] ^ (nc >> 8);
-                        y >>= 8;
-                    }
-                }
-                out_e[cid] = nc;
-                if (first_cut == kNone32) first_cut = cid;
-                else out_pre[cid] = 0;  // started inside this slab: nothing before it
-                nc = 0;
-                ++q;
-                cid = q == 1 ? i1 : q == 2 ? i2 : i3;
-                cc = q == 1 ? c1 : q == 2 ? c2 : c3;
-                cj = (cc - 1) >> 2;
-            }
-            crc = nc;
+        for (int k = 0; k < 4; ++k) {
+            words[4 * k] = d[k].x;
+            words[4 * k + 1] = d[k].y;
+            words[4 * k + 2] = d[k].z;
+            words[4 * k + 3] = d[k].w;
         }
-        const uint32_t z = t != kNone32 ? crc : 0u;
-        if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
-            asm volatile("" ::"v"(crc), "v"(z));
-            if (lane == 63) out_rend[row] = crc ^ t;
-        } else {
-            // Z_{64(63-lane)}(z): reference the open register to the row end
-            uint32_t cz = 0;
-#pragma unroll
-            for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
-            // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
-            uint32_t P = cz;
-            P ^= dpp<0x111, 0xF>(P);  // row_shr:1
-            P ^= dpp<0x112, 0xF>(P);  // row_shr:2
-            P ^= dpp<0x114, 0xF>(P);  // row_shr:4
-            P ^= dpp<0x118, 0xF>(P);  // row_shr:8
-            P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
-            P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
-            const uint32_t tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
-            const bool start = lane == 0 || t != tprev;
-            const uint64_t B = __ballot(start);
-            const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-            const int rsl = 63 - __clzll((long long)(B & upto));
-            const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
-            const uint32_t runv = P ^ (rsl > 0 ? Pp : 0u);
-            const uint32_t runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
-            if (lane == 63) out_rend[row] = t != kNone32 ? runv : 0u;
-            if (first_cut != kNone32) out_pre[first_cut] = (lane > 0 && tprev == first_cut) ? runprev : 0u;
-        }
+        const RowOut o = crc_row<MODE>(lds, lane, l31, nbase, s_rel, rs, words, rc, t);
 
-        if (nrow >= n_rows) break;
-        row = nrow;
-        nrow = nnrow;
-        ra = nra;
-        rb = nrb;
-        nra = nnra;
-        nrb = nnrb;
-        d0 = n0;
-        d1 = n1;
-        d2 = n2;
-        d3 = n3;
-        cur = nxt;
+        // record ra+j's e / pre gathered onto lane j
+        const int32_t src = (max(rc.my_end, 1) - 1) >> 6;  // lane whose slab holds record ra+lane's end
+        uint32_t before = 0;                               // earlier records ending in that slab
+#pragma unroll
+        for (int j = 0; j < kPlanEnds; ++j) {
+            if ((uint32_t)j >= n_ends) break;
+            const int32_t end = (int32_t)((pw[2 + j / 2] >> (16 * (j & 1))) & 0xFFFFu);
+            before += ((uint32_t)j < lane && ((end - 1) >> 6) == src) ? 1u : 0u;
+        }
+        const uint32_t g0 = __shfl(o.e[0], src), g1 = __shfl(o.e[1], src), g2 = __shfl(o.e[2], src),
+                       g3 = __shfl(o.e[3], src), gp = __shfl(o.pre_first, src);
+        const uint32_t ev = before == 0 ? g0 : before == 1 ? g1 : before == 2 ? g2 : g3;
+        const uint32_t pv = before == 0 ? gp : 0u;
+        const uint32_t rend_row = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+
+        // ---- everything outstanding was issued one row ago: the next row's
+        // data (needed now) and the previous row's stores
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t slot = (small && lane < n_ends) ? (uint64_t)ra + lane : n_total;  // n_total: scratch
+        out_e[slot] = ev;
+        out_pre[slot] = pv;
+        if (lane == 0) out_rend[small ? row : n_rows] = rend_row;
+
+        if (row1 >= n_rows) break;
+        row = row1;
+#pragma unroll
+        for (int i = 0; i < kPlanWords; ++i) {
+            pw[i] = pw1[i];
+            pw1[i] = pw2[i];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = nx[k];
+    }
+}
+
+// Rows where more than kPlanEnds records end (tiny records): one wavefront per
+// listed row, record ends read from the record table, direct stores.
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict__ arena,
+                                                       const uint32_t *__restrict__ big_rows,
+                                                       const uint32_t *__restrict__ big_count,
+                                                       const uint32_t *__restrict__ plan, uint64_t n_total,
+                                                       const uint64_t *__restrict__ rec_off,
+                                                       const uint4 *__restrict__ rec_hdr,
+                                                       const uint32_t *__restrict__ g_slice,
+                                                       const uint32_t *__restrict__ g_nib,
+                                                       uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
+                                                       uint32_t *__restrict__ out_rend) {
+    const uint32_t nbig = *big_count;
+    if (blockIdx.x * kWaves >= nbig) return;
+    __shared__ uint32_t lds[40960];
+    fill_crc_lds(lds, g_slice, g_nib);
+    const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
+    const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
+    const int32_t s_rel = (int32_t)lane * kSlab;
+    for (uint32_t bi = blockIdx.x * kWaves + (threadIdx.x >> 6); bi < nbig; bi += gridDim.x * kWaves) {
+        const uint64_t row = big_rows[bi], rs = row * kRow;
+        const uint32_t *pw = plan + row * kPlanWords;
+        const uint32_t ra = pw[0], n_ends = pw[1] & 0xFFFFu, tail_start = pw[1] >> 16;
+        RowCuts rc;
+        for (uint32_t j0 = 0; j0 < n_ends; j0 += 64) {
+            const uint32_t cnt = min(64u, n_ends - j0);
+            const uint64_t r = min((uint64_t)ra + j0 + min(lane, cnt - 1), n_total - 1);
+            const int32_t e_ = (int32_t)(value_end(rec_off, rec_hdr, r) - rs);
+            for (uint32_t j = 0; j < cnt; ++j) rc.take((uint32_t)__builtin_amdgcn_readlane(e_, j), j0 + j, ra, lane, s_rel);
+        }
+        const uint32_t t = (rc.n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + rc.n_le : kNone32;
+        const uint4 *src = reinterpret_cast<const uint4 *>(arena + rs + s_rel);
+        uint32_t words[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = src[k];
+            words[4 * k] = v.x;
+            words[4 * k + 1] = v.y;
+            words[4 * k + 2] = v.z;
+            words[4 * k + 3] = v.w;
+        }
+        const RowOut o = crc_row<MODE>(lds, lane, l31, nbase, s_rel, rs, words, rc, t);
+        if (rc.ncut > 0) out_e[rc.id0] = o.e[0], out_pre[rc.id0] = o.pre_first;
+        if (rc.ncut > 1) out_e[rc.id1] = o.e[1], out_pre[rc.id1] = 0u;
+        if (rc.ncut > 2) out_e[rc.id2] = o.e[2], out_pre[rc.id2] = 0u;
+        if (rc.ncut > 3) out_e[rc.id3] = o.e[3], out_pre[rc.id3] = 0u;
+        if (lane == 63) out_rend[row] = o.rend;
     }
 }
 
@@ -783,7 +976,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
-                   &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend,
+                   &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
@@ -838,7 +1031,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)))
+        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -986,7 +1179,7 @@ static int ctx_run(Ctx *c) {
     const uint64_t nr = n_total ? n_total : 1;
     int rc;
     if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_hdr.ensure(nr * 16)) ||
-        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_e.ensure(nr * 4)) || (rc = c->d_pre.ensure(nr * 4)) ||
+        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_e.ensure((nr + 1) * 4)) || (rc = c->d_pre.ensure((nr + 1) * 4)) ||
         (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
         return rc;
     if (n_total > 0xFFFFFFF0ull) return GCK_EINVAL;
@@ -1005,6 +1198,9 @@ static int ctx_run(Ctx *c) {
     if (n_total) {
         k_row_index<<<nblk(n_total, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                                       n_total, c->n_rows, c->d_row_first.as<uint32_t>());
+        k_row_plan<<<nblk(c->n_rows, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+                                                       n_total, c->n_rows, c->d_row_first.as<uint32_t>(),
+                                                       c->d_plan.as<uint4>(), c->d_big.as<uint32_t>(), cnt + 5);
     } else {
         GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, (c->n_rows + 1) * 4, s));
     }
@@ -1012,10 +1208,14 @@ static int ctx_run(Ctx *c) {
     if (c->n_rows && n_total) {
         const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-        k_crc_rows<0><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_row_first.as<uint32_t>(), n_total,
-                                         c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+        k_crc_rows<0><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint32_t>(), n_total,
                                          c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
                                          c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
+        k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>(), cnt + 5,
+                                                  c->d_plan.as<uint32_t>(), n_total, c->d_rec_off.as<uint64_t>(),
+                                                  c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
+                                                  c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
+                                                  c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
     }
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     if (n_total) {
@@ -1189,7 +1389,7 @@ const char *gck_last_error(void) { return gck::last_error(); }
 // mode bits: 1 = no record intervals, 2 = no LDS table chain, 4 = no tail
 // shift / segmented scan.
 int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
-    if (!ctx || iters <= 0 || mode < 0 || mode > 7) return GCK_EINVAL;
+    if (!ctx || iters <= 0 || mode < 0 || mode > 15) return GCK_EINVAL;
     Ctx *c = &ctx->c;
     if (!c->n_rows || !c->n_recs) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
@@ -1202,15 +1402,14 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     for (int i = 0; i < iters; ++i) {
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
-        k_crc_rows<M><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_row_first.as<uint32_t>(), \
-                                                    c->n_recs, c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),   \
-                                                    c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),                 \
+        k_crc_rows<M><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint32_t>(), \
+                                                    c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
                                                     c->d_rend.as<uint32_t>());                                          \
         break;
         switch (mode) {
-            GCK_VARIANT(0) GCK_VARIANT(1) GCK_VARIANT(2) GCK_VARIANT(3) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6)
-            GCK_VARIANT(7)
+            GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6) GCK_VARIANT(7) GCK_VARIANT(8)
+            default: return GCK_EINVAL;
         }
 #undef GCK_VARIANT
     }
