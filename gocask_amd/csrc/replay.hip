@@ -35,6 +35,10 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
+#ifndef GCK_DEPTH
+#define GCK_DEPTH 2
+#endif
+constexpr int kDepth = GCK_DEPTH;  // rows in flight per k_crc_rows wavefront
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -408,16 +412,26 @@ __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *_
         for (uint64_t row = hi; row <= n_rows; ++row) row_first[row] = (uint32_t)n_total;
 }
 
-constexpr int kPlanWords = 16;  // 64 B per row
-constexpr int kPlanEnds = 28;   // record ends stored inline; more -> slow path
+constexpr int kPlanBytes = 64;  // per row: one byte per 64 B slab (= per k_crc_rows lane)
 
-// Per-row plan for k_crc_rows, read with scalar loads (no vector-memory wait
-// couples it to the row data):
-//   w0     ra = first record whose end lies past the row start
-//   w1     n_ends (records ending inside the row) | tail_start << 16, where
-//          tail_start = row-relative start of record ra + n_ends (the record
-//          open at the row end), kRow if there is none
-//   w2..15 row-relative end offsets (1..kRow) of records ra .. ra+27 as u16
+// Tail start of row `row`: row-relative start of record rb (the record open at
+// the row end), clamped to [0, kRow]; kRow if there is none.
+__device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ rec_off, uint64_t n_total,
+                                                   uint32_t rb, uint64_t rs) {
+    if (rb >= n_total) return kRow;
+    const int64_t st = (int64_t)rec_off[rb] - (int64_t)rs;
+    return (uint32_t)max(min(st, (int64_t)kRow), (int64_t)0);
+}
+
+// Per-row plan for k_crc_rows, 64 bytes, byte k for lane k (slab k):
+//   bits 0..6  cut: offset (1..64) inside slab k where a record ends, 0 = none
+//   bit  7     bit k of the row header H, recovered with one ballot:
+//              H[0..31] = ra, the first record whose end lies past the row start
+//              H[32..44] = tail start (row_tail_start)
+//              H[45] = slow: some slab holds 2+ record ends (records < 64 B);
+//                      such rows are listed for k_crc_rows_big
+// Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
+// plan carries no ids or counts.
 __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
                            uint64_t n_total, uint64_t n_rows, const uint32_t *__restrict__ row_first,
                            uint4 *__restrict__ plan, uint32_t *__restrict__ big_rows, uint32_t *big_count) {
@@ -425,79 +439,56 @@ __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__
     if (row >= n_rows) return;
     const uint32_t ra = row_first[row], rb = row_first[row + 1];
     const uint64_t rs = row * kRow;
-    const uint32_t n = rb - ra;
-    uint32_t w[kPlanWords];
+    uint32_t w[16];
 #pragma unroll
-    for (int i = 0; i < kPlanWords; ++i) w[i] = 0;
-    uint32_t tail = kRow;
-    if (rb < n_total) {
-        const int64_t st = (int64_t)rec_off[rb] - (int64_t)rs;
-        tail = (uint32_t)max(min(st, (int64_t)kRow), (int64_t)0);
-    }
-    w[0] = ra;
-    w[1] = min(n, 0xFFFFu) | (tail << 16);
-    if (n > (uint32_t)kPlanEnds) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
-    const uint32_t m = min(n, (uint32_t)kPlanEnds);
-    for (uint32_t i = 0; i < m; ++i) {
-        const uint32_t end = (uint32_t)(value_end(rec_off, rec_hdr, ra + i) - rs);
-        w[2 + i / 2] |= end << (16 * (i & 1));
-    }
+    for (int i = 0; i < 16; ++i) w[i] = 0;
+    bool slow = false;
+    int32_t prev = -1;
+    for (uint32_t r = ra; r < rb; ++r) {
+        const uint32_t end = (uint32_t)(value_end(rec_off, rec_hdr, r) - rs);  // 1..kRow
+        const int32_t slab = (int32_t)((end - 1) >> 6);
+        slow |= slab == prev;
+        prev = slab;
+        const uint32_t cc = end - (uint32_t)slab * kSlab;
+        // w[] is indexed by a loop-variant value: keep it in registers by selects
 #pragma unroll
-    for (int i = 0; i < kPlanWords / 4; ++i)
-        plan[row * (kPlanWords / 4) + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+        for (int i = 0; i < 16; ++i) w[i] |= (slab >> 2) == i ? cc << (8 * (slab & 3)) : 0u;
+    }
+    if (slow) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
+    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, n_total, rb, rs) << 32) |
+                       ((uint64_t)slow << 45);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) w[k >> 2] |= (uint32_t)((H >> k) & 1u) << (8 * (k & 3) + 7);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) plan[row * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-// Slicing-by-4 step through the LDS tables.  Table t, entry b, copy l31 lives
-// at index t*8192 + b*32 + l31: every lane of a 32-lane LDS group reads its own
-// bank, so the lookups are bank-conflict free (MI355X_MICROARCH.md §LDS).
-__device__ __forceinline__ uint32_t slice4(const uint32_t *lds, uint32_t l31, uint32_t c) {
-    return lds[24576 + (((c << 5) & 0x1FE0u) | l31)] ^ lds[16384 + (((c >> 3) & 0x1FE0u) | l31)] ^
-           lds[8192 + (((c >> 11) & 0x1FE0u) | l31)] ^ lds[((c >> 19) & 0x1FE0u) | l31];
+// LDS image of the slicing-by-4 tables: two 64 KiB regions; in region r,
+// entry b of half h, copy l31 sits at byte address r*65536 + b*256 + h*128 +
+// l31*4 (tables T3, T2 in region 0, T1, T0 in region 1).  Every lane of a
+// 32-lane LDS group reads its own bank, so lookups are conflict free
+// (MI355X_MICROARCH.md §LDS), and the address of a lookup is ONE v_perm_b32:
+// byte 0 = the lane's l31*4, byte 1 = the index byte, byte 2 = the region
+// (from the lane base lb0 = l31*4 or lb1 = 65536 + l31*4); the half is the
+// ds_read immediate offset.
+__device__ __forceinline__ uint32_t lds_at(const uint32_t *lds, uint32_t byte_addr) {
+    return *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(lds) + byte_addr);
 }
-
-// Raw candidate record of a row: arena offset of the record and {KeySize,
-// ValueSize}.  Loaded one row ahead; converted to row-relative positions only
-// when the row is processed, so the loads never force an early wait.
-struct RawRec {
-    uint64_t off;
-    uint2 kv;
-};
-
-__device__ __forceinline__ RawRec load_raw(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                                           uint64_t r) {
-    RawRec x;
-    x.off = rec_off[r];
-    x.kv = *reinterpret_cast<const uint2 *>(reinterpret_cast<const uint32_t *>(rec_hdr + r) + 2);
-    return x;
+template <int K>
+__device__ __forceinline__ uint32_t tbl_addr(uint32_t c, uint32_t lb) {
+    return __builtin_amdgcn_perm(c, lb, 0x0C020000u | ((4u + K) << 8));
 }
-
-// Record start and end relative to row start rs, clamped to [-1, kRow+1]
-// (every comparison with a position inside the row is preserved).
-__device__ __forceinline__ void to_span(const RawRec &x, uint64_t rs, int32_t &st_out, int32_t &ve_out) {
-    const int64_t st = (int64_t)x.off - (int64_t)rs;
-    const int64_t ve = st + 16 + (int64_t)x.kv.x + (int64_t)x.kv.y;
-    st_out = (int32_t)max(min(st, (int64_t)kRow + 1), (int64_t)-1);
-    ve_out = (int32_t)max(min(ve, (int64_t)kRow + 1), (int64_t)-1);
+// crc' = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3] for c = crc ^ word.
+__device__ __forceinline__ uint32_t slice4(const uint32_t *lds, uint32_t lb0, uint32_t lb1, uint32_t c) {
+    return lds_at(lds, tbl_addr<0>(c, lb0)) ^ lds_at(lds, tbl_addr<1>(c, lb0) + 128) ^
+           lds_at(lds, tbl_addr<2>(c, lb1)) ^ lds_at(lds, tbl_addr<3>(c, lb1) + 128);
+}
+// One byte through T0: crc' = T0[(crc ^ b) & 0xFF] ^ crc >> 8.
+__device__ __forceinline__ uint32_t byte1(const uint32_t *lds, uint32_t lb1, uint32_t crc, uint32_t b) {
+    return lds_at(lds, tbl_addr<0>(crc ^ b, lb1) + 128) ^ (crc >> 8);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-#ifndef GCK_NT
-#define GCK_NT 0
-#endif
-#ifndef GCK_DEPTH
-#define GCK_DEPTH 1
-#endif
-
-// 16-byte row load (GCK_NT: non-temporal hint, the row bytes are read once).
-__device__ __forceinline__ uint4 ld_stream(const uint8_t *p) {
-#if GCK_NT
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *reinterpret_cast<const uint4 *>(p);
-#endif
-}
 
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -507,7 +498,8 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 // LDS image of the CRC tables (identical in every k_crc_rows* workgroup).
 __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__restrict__ g_slice,
                                              const uint32_t *__restrict__ g_nib) {
-    for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x) lds[i] = g_slice[(i >> 13) * 256 + ((i >> 5) & 255)];
+    for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x)
+        lds[i] = g_slice[(3 - ((i >> 13) & 2) - ((i >> 5) & 1)) * 256 + ((i >> 6) & 255)];
     for (uint32_t i = threadIdx.x; i < 8192; i += blockDim.x) {
         const uint32_t l = (i >> 12) * 32 + (i & 31), v = (i >> 5) & 15, q = (i >> 9) & 7;
         lds[kNibBase + i] = g_nib[(l * 8 + q) * 16 + v];
@@ -547,12 +539,40 @@ struct RowOut {
     uint32_t rend = 0;              // (lane 63) run open at the row end
 };
 
+// Z_{64(63-lane)}(z) (the open register referenced to the row end, 8 nibble
+// lookups in the lane's LDS table), then a segmented inclusive XOR over the
+// wave: lanes whose open register belongs to the same record t form a run.
+// runv = run value up to this lane, runprev = the previous lane's, tprev = its t.
+__device__ __forceinline__ void wave_runs(const uint32_t *lds, uint32_t lane, uint32_t nbase, uint32_t z,
+                                          uint32_t t, uint32_t &runv, uint32_t &runprev, uint32_t &tprev) {
+    // Z_{64(63-lane)}(z): reference the open register to the row end
+    uint32_t cz = 0;
+#pragma unroll
+    for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
+    // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
+    uint32_t P = cz;
+    P ^= dpp<0x111, 0xF>(P);  // row_shr:1
+    P ^= dpp<0x112, 0xF>(P);  // row_shr:2
+    P ^= dpp<0x114, 0xF>(P);  // row_shr:4
+    P ^= dpp<0x118, 0xF>(P);  // row_shr:8
+    P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
+    P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
+    tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
+    const bool start = lane == 0 || t != tprev;
+    const uint64_t B = __ballot(start);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int rsl = 63 - __clzll((long long)(B & upto));
+    const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
+    runv = P ^ (rsl > 0 ? Pp : 0u);
+    runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
+}
+
 // The per-row work of k_crc_rows: every byte of the slab enters the CRC
 // register; it is closed at each record end (exactly: the last partial word
 // byte-wise), the open register at the slab end is shifted to the row end and
 // a segmented XOR over the wave joins each record's lanes.
 template <int MODE>
-__device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, uint32_t l31, uint32_t nbase,
+__device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1, uint32_t nbase,
                                           int32_t s_rel, uint64_t rs, uint32_t (&words)[16], const RowCuts &rc,
                                           uint32_t t) {
     RowOut o;
@@ -568,14 +588,14 @@ __device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, ui
     for (int j = 0; j < 16; ++j) {
         const uint32_t x = words[j];
         uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
-                                 : slice4(lds, l31, crc ^ x);
+                                 : slice4(lds, lb0, lb1, crc ^ x);
         if (j == cj) {
             const int nb = cc - 4 * j;
             if (nb < 4) {
                 nc = crc;
                 uint32_t y = x;
                 for (int b = 0; b < nb; ++b) {
-                    nc = lds[(((nc ^ y) & 0xFFu) << 5) | l31] ^ (nc >> 8);
+                    nc = byte1(lds, lb1, nc, y);
                     y >>= 8;
                 }
             }
@@ -596,26 +616,8 @@ __device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, ui
     if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
         asm volatile("" ::"v"(crc), "v"(z));
     } else {
-        // Z_{64(63-lane)}(z): reference the open register to the row end
-        uint32_t cz = 0;
-#pragma unroll
-        for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
-        // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
-        uint32_t P = cz;
-        P ^= dpp<0x111, 0xF>(P);  // row_shr:1
-        P ^= dpp<0x112, 0xF>(P);  // row_shr:2
-        P ^= dpp<0x114, 0xF>(P);  // row_shr:4
-        P ^= dpp<0x118, 0xF>(P);  // row_shr:8
-        P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
-        P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
-        const uint32_t tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
-        const bool start = lane == 0 || t != tprev;
-        const uint64_t B = __ballot(start);
-        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        const int rsl = 63 - __clzll((long long)(B & upto));
-        const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
-        const uint32_t runv = P ^ (rsl > 0 ? Pp : 0u);
-        const uint32_t runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
+        uint32_t runv, runprev, tprev;
+        wave_runs(lds, lane, nbase, z, t, runv, runprev, tprev);
         o.rend = t != kNone32 ? runv : 0u;
         // the first record closing in this slab continues the run of the lane before
         o.pre_first = (rc.ncut > 0 && lane > 0 && tprev == rc.id0) ? runprev : 0u;
@@ -623,10 +625,65 @@ __device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, ui
     return o;
 }
 
-// 16-byte load issued by inline asm: the compiler neither tracks nor waits for
-// it; k_crc_rows waits explicitly (see there).
-__device__ __forceinline__ void ld_async(u32x4 &x, const uint8_t *p) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p) : "memory");
+struct RowOut1 {
+    uint32_t e = 0;    // register at the record end in the slab
+    uint32_t pre = 0;  // run of the lanes before, for the record ending in the slab
+    uint32_t rend = 0; // run open at the slab end, referenced to the row end (lane 63: the row's)
+};
+
+// The per-row work of k_crc_rows for rows with at most one record end per
+// slab: every byte of the slab enters the CRC register; it is closed at the
+// record end cc (the last partial word byte-wise), the open register at the
+// slab end is shifted to the row end and a segmented XOR over the wave joins
+// each record's lanes.
+template <int MODE>
+__device__ __forceinline__ RowOut1 crc_row1(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1,
+                                            uint32_t nbase, uint64_t rs, uint32_t (&words)[16], int32_t cc,
+                                            uint32_t my_id, uint32_t t) {
+    RowOut1 o;
+    const int32_t cj = cc ? (cc - 1) >> 2 : 99;  // word holding the record's last byte
+    uint32_t crc = 0;
+    if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded row
+#pragma unroll
+        for (int j = 0; j < 16; ++j) words[j] = (uint32_t)(rs >> 4) * 2654435761u + lane * 97u + j;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t x = words[j];
+        uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
+                                 : slice4(lds, lb0, lb1, crc ^ x);
+        if (j == cj) {
+            const int nb = cc - 4 * j;
+            if (nb < 4) {
+                nc = crc;
+                uint32_t y = x;
+                for (int b = 0; b < nb; ++b) {
+                    nc = byte1(lds, lb1, nc, y);
+                    y >>= 8;
+                }
+            }
+            o.e = nc;
+            nc = 0;
+        }
+        crc = nc;
+    }
+    const uint32_t z = t != kNone32 ? crc : 0u;
+    o.rend = crc ^ t;
+    if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
+        asm volatile("" ::"v"(crc), "v"(z));
+    } else {
+        uint32_t runv, runprev, tprev;
+        wave_runs(lds, lane, nbase, z, t, runv, runprev, tprev);
+        o.rend = t != kNone32 ? runv : 0u;
+        // the record closing in this slab continues the run of the lane before
+        o.pre = (cc && lane > 0 && tprev == my_id) ? runprev : 0u;
+    }
+    return o;
+}
+
+// Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
 }
 
 // The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns bytes
@@ -638,20 +695,22 @@ __device__ __forceinline__ void ld_async(u32x4 &x, const uint8_t *p) {
 // slab end belongs to the record containing that position; it is referenced to
 // the row end with the per-lane constant shift Z_{64(63-k)} (8 nibble lookups)
 // and a segmented XOR over the wave (DPP prefix scan) joins each record's
-// lanes.  Outputs: e and pre per record (gathered so lane j stores record
-// ra+j: two coalesced stores per row), the run open at the row end per row.
+// lanes.  Outputs: per record e (the register at its end) and pre (the run of
+// the lanes before its closing slab), stored by the lane whose slab holds the
+// record end (slot ra + mbcnt of the cut ballot); per row the run open at the
+// row end.  A slab holds at most one record end here; rows where one holds
+// more (records under 64 B) are flagged by k_row_plan and done by
+// k_crc_rows_big (their stores here go to the scratch slots).
 //
-// Memory pipeline: the row plan (k_row_plan) comes by scalar loads two rows
-// ahead; the row data by inline-asm loads one row ahead.  The only compiler-
-// visible vector-memory ops are the 3 stores per row, so the compiler inserts
-// no vmcnt waits; the single explicit `s_waitcnt vmcnt(0)` sits after the row
-// is processed and before its stores, where everything outstanding (the next
-// row's data and the previous row's stores) was issued a whole row earlier.
-// Rows where more than kPlanEnds records end are left to k_crc_rows_big (their
-// stores here go to scratch slots so the per-row store count stays fixed).
-template <int MODE>
+// Memory pipeline: the row data (4 x 16 B per lane) and the row plan byte are
+// buffer loads (row base in a scalar resource, lane offset in a fixed VGPR)
+// issued DEPTH rows ahead.  No scalar loads in the loop: an outstanding SMEM
+// load would make every LDS wait (lgkmcnt(0)) wait for HBM too.  Control flow
+// around the stores is uniform and their number fixed, so the compiler's vmcnt
+// waits land rows after the loads they wait for.
+template <int MODE, int DEPTH>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint32_t *__restrict__ plan, uint64_t n_total,
+                                                   const uint8_t *__restrict__ plan, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib,
                                                    uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
@@ -660,106 +719,94 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
+    const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
 
     uint64_t row = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
     if (row >= n_rows) return;
-    auto ldplan = [&](uint64_t r, uint32_t (&w)[kPlanWords]) {
-        const uint32_t *p_ = plan + min(r, n_rows - 1) * kPlanWords;
-#pragma unroll
-        for (int i = 0; i < kPlanWords; ++i) w[i] = p_[i];
+    struct RowBuf {
+        u32x4 x[4];
+        uint32_t pv;
     };
-    auto ldrow = [&](uint64_t r, u32x4 (&x)[4]) {
-        const uint8_t *p_ = arena + min(r, n_rows - 1) * kRow + s_rel;
-        ld_async(x[0], p_);
-        ld_async(x[1], p_ + 16);
-        ld_async(x[2], p_ + 32);
-        ld_async(x[3], p_ + 48);
+    auto issue = [&](uint64_t r, RowBuf &b) {
+        if constexpr ((MODE & 8) != 0) return;
+        // buffer loads: the row base lives in a scalar resource, the lane
+        // offset in one VGPR that never changes (no per-load VGPR address)
+        r = min(r, n_rows - 1);
+        const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
+        const __amdgpu_buffer_rsrc_t rplan = make_rsrc(plan + r * kPlanBytes, kPlanBytes);
+        b.x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel, 0, 0);
+        b.x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 16, 0, 0);
+        b.x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 32, 0, 0);
+        b.x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 48, 0, 0);
+        b.pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
     };
-    uint32_t pw[kPlanWords], pw1[kPlanWords];
-    ldplan(row, pw);
-    ldplan(row + stride, pw1);
-    u32x4 d[4], nx[4] = {};
-    ldrow(row, d);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-
-    for (;;) {
+    auto process = [&](uint64_t row, const RowBuf &b) {
         const uint64_t rs = row * kRow;
-        const uint64_t row1 = row + stride;
-        // ---- issue the next row's data and the plan of the row after it
-        if constexpr ((MODE & 8) == 0) ldrow(row1, nx);
-        uint32_t pw2[kPlanWords];
-        ldplan(row1 + stride, pw2);
-
-        const uint32_t ra = pw[0], n_ends = pw[1] & 0xFFFFu, tail_start = pw[1] >> 16;
-        const bool small = n_ends <= (uint32_t)kPlanEnds;  // wave-uniform
-        RowCuts rc;
-        if constexpr ((MODE & 1) == 0) {
-#pragma unroll
-            for (int j = 0; j < kPlanEnds; ++j) {
-                if ((uint32_t)j >= n_ends) break;
-                rc.take((pw[2 + j / 2] >> (16 * (j & 1))) & 0xFFFFu, j, ra, lane, s_rel);
-            }
-        }
+        // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
+        const uint64_t H = __ballot(b.pv & 0x80u);
+        const uint32_t ra = (uint32_t)H, hh = (uint32_t)(H >> 32);
+        const uint32_t tail_start = hh & 0x1FFFu;
+        const bool slow = (hh >> 13) & 1u;  // wave-uniform: k_crc_rows_big owns the row
+        const int32_t cc = (MODE & 1) ? 0 : (int32_t)(b.pv & 0x7Fu);
+        const uint64_t C = __ballot(cc != 0);
+        const uint32_t n_ends = (uint32_t)__popcll(C);
+        const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
+        const uint32_t n_le = idx + (cc != 0);  // record ends at or before the slab end
         // the record open at the slab end: the next one after the ends counted;
         // it exists if it ends inside the row, or it is the row's tail record and
         // starts before the slab end (not padding after a file's last record)
-        const uint32_t t = (rc.n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + rc.n_le : kNone32;
+        const uint32_t t = (n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + n_le : kNone32;
         uint32_t words[16];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            words[4 * k] = d[k].x;
-            words[4 * k + 1] = d[k].y;
-            words[4 * k + 2] = d[k].z;
-            words[4 * k + 3] = d[k].w;
+            words[4 * k] = b.x[k].x;
+            words[4 * k + 1] = b.x[k].y;
+            words[4 * k + 2] = b.x[k].z;
+            words[4 * k + 3] = b.x[k].w;
         }
-        const RowOut o = crc_row<MODE>(lds, lane, l31, nbase, s_rel, rs, words, rc, t);
-
-        // record ra+j's e / pre gathered onto lane j
-        const int32_t src = (max(rc.my_end, 1) - 1) >> 6;  // lane whose slab holds record ra+lane's end
-        uint32_t before = 0;                               // earlier records ending in that slab
+        const RowOut1 o = crc_row1<MODE>(lds, lane, lb0, lb1, nbase, rs, words, cc, ra + idx, t);
+        // every lane stores: the cut lanes to their record's slot, the rest to
+        // the scratch slot n_total (no branch around a store)
+        const uint64_t slot = (cc != 0 && !slow) ? (uint64_t)ra + idx : n_total;
+        out_e[slot] = o.e;
+        out_pre[slot] = o.pre;
+        out_rend[slow ? n_rows : row] = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+    };
+    // DEPTH rows in flight while one is processed; the loop is unrolled over
+    // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
+    // force a wait on loads still in flight).
+    RowBuf buf[DEPTH + 1] = {};
 #pragma unroll
-        for (int j = 0; j < kPlanEnds; ++j) {
-            if ((uint32_t)j >= n_ends) break;
-            const int32_t end = (int32_t)((pw[2 + j / 2] >> (16 * (j & 1))) & 0xFFFFu);
-            before += ((uint32_t)j < lane && ((end - 1) >> 6) == src) ? 1u : 0u;
+    for (int i = 0; i < DEPTH; ++i) {
+        issue(row + i * stride, buf[i]);
+        // the 3 stores of a processed row, to the scratch slots: the loop is
+        // entered with the same vector-memory queue shape as its back edge, so
+        // the compiler's waits at the loop head are as late as in the body
+        out_e[n_total] = 0;
+        out_pre[n_total] = 0;
+        out_rend[n_rows] = 0;
+    }
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i <= DEPTH; ++i) {
+            issue(row + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
+            process(row, buf[i]);
+            row += stride;
+            if (row >= n_rows) return;
         }
-        const uint32_t g0 = __shfl(o.e[0], src), g1 = __shfl(o.e[1], src), g2 = __shfl(o.e[2], src),
-                       g3 = __shfl(o.e[3], src), gp = __shfl(o.pre_first, src);
-        const uint32_t ev = before == 0 ? g0 : before == 1 ? g1 : before == 2 ? g2 : g3;
-        const uint32_t pv = before == 0 ? gp : 0u;
-        const uint32_t rend_row = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
-
-        // ---- everything outstanding was issued one row ago: the next row's
-        // data (needed now) and the previous row's stores
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        const uint64_t slot = (small && lane < n_ends) ? (uint64_t)ra + lane : n_total;  // n_total: scratch
-        out_e[slot] = ev;
-        out_pre[slot] = pv;
-        if (lane == 0) out_rend[small ? row : n_rows] = rend_row;
-
-        if (row1 >= n_rows) break;
-        row = row1;
-#pragma unroll
-        for (int i = 0; i < kPlanWords; ++i) {
-            pw[i] = pw1[i];
-            pw1[i] = pw2[i];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = nx[k];
     }
 }
 
-// Rows where more than kPlanEnds records end (tiny records): one wavefront per
-// listed row, record ends read from the record table, direct stores.
+// Rows where a slab holds 2+ record ends (records shorter than 64 B): one
+// wavefront per listed row, record ends read from the record table, direct
+// stores; up to 4 ends per slab (a record is at least 16 B).
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict__ arena,
                                                        const uint32_t *__restrict__ big_rows,
                                                        const uint32_t *__restrict__ big_count,
-                                                       const uint32_t *__restrict__ plan, uint64_t n_total,
+                                                       const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                        const uint64_t *__restrict__ rec_off,
                                                        const uint4 *__restrict__ rec_hdr,
                                                        const uint32_t *__restrict__ g_slice,
@@ -772,11 +819,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
+    const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
     for (uint32_t bi = blockIdx.x * kWaves + (threadIdx.x >> 6); bi < nbig; bi += gridDim.x * kWaves) {
         const uint64_t row = big_rows[bi], rs = row * kRow;
-        const uint32_t *pw = plan + row * kPlanWords;
-        const uint32_t ra = pw[0], n_ends = pw[1] & 0xFFFFu, tail_start = pw[1] >> 16;
+        const uint32_t ra = row_first[row], rb = row_first[row + 1], n_ends = rb - ra;
+        const uint32_t tail_start = row_tail_start(rec_off, n_total, rb, rs);
         RowCuts rc;
         for (uint32_t j0 = 0; j0 < n_ends; j0 += 64) {
             const uint32_t cnt = min(64u, n_ends - j0);
@@ -795,7 +843,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
             words[4 * k + 2] = v.z;
             words[4 * k + 3] = v.w;
         }
-        const RowOut o = crc_row<MODE>(lds, lane, l31, nbase, s_rel, rs, words, rc, t);
+        const RowOut o = crc_row<MODE>(lds, lane, lb0, lb1, nbase, s_rel, rs, words, rc, t);
         if (rc.ncut > 0) out_e[rc.id0] = o.e[0], out_pre[rc.id0] = o.pre_first;
         if (rc.ncut > 1) out_e[rc.id1] = o.e[1], out_pre[rc.id1] = 0u;
         if (rc.ncut > 2) out_e[rc.id2] = o.e[2], out_pre[rc.id2] = 0u;
@@ -1208,11 +1256,11 @@ static int ctx_run(Ctx *c) {
     if (c->n_rows && n_total) {
         const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-        k_crc_rows<0><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint32_t>(), n_total,
+        k_crc_rows<0, kDepth><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), n_total,
                                          c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
                                          c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
         k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>(), cnt + 5,
-                                                  c->d_plan.as<uint32_t>(), n_total, c->d_rec_off.as<uint64_t>(),
+                                                  c->d_row_first.as<uint32_t>(), n_total, c->d_rec_off.as<uint64_t>(),
                                                   c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
                                                   c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
                                                   c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
@@ -1402,7 +1450,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     for (int i = 0; i < iters; ++i) {
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
-        k_crc_rows<M><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint32_t>(), \
+        k_crc_rows<M, kDepth><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
                                                     c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
                                                     c->d_rend.as<uint32_t>());                                          \

@@ -1,9 +1,20 @@
 #!/bin/bash
-# PMC passes on the bench command (counters in separate passes, kernel-trace only)
+# Profiling passes on the bench command (run on the GPU box from the repo root):
+#   1. kernel trace + stats (per-kernel average durations)
+#   2..n. PMC counters, one pass each (never combined with runtime/sys traces)
+# Usage: tools/pmc.sh <tag> [bench args...]   -> gpurun_out/prof_<tag>/
 set -o pipefail
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+tag=${1:-r1}; shift
+args=${*:---steps 5 --warmup 2 --no-cpu-baseline}
+export TMPDIR=/tmp
+out=gpurun_out/prof_$tag
+mkdir -p $out
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/trace -o run -- \
+  python3 bench.py $args > $out/trace.log 2>&1 || exit $?
 i=0
-for ctrs in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS" "FETCH_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_SALU" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for ctrs in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-include-regex "k_crc_rows|k_stream_read" --output-format csv -d gpurun_out/pmc_r1/p$i -o run -- python bench.py --steps 2 --warmup 0 --no-cpu-baseline > gpurun_out/pmc_r1/p$i.log 2>&1 || exit $?
+  timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-include-regex "k_crc_rows|k_stream_read|k_spec_entry|k_finalize|k_walk" \
+    --output-format csv -d $out/pmc$i -o run -- python3 bench.py --steps 2 --warmup 0 --no-cpu-baseline \
+    > $out/pmc$i.log 2>&1 || exit $?
 done
