@@ -65,6 +65,27 @@ def cpu_baseline(cfg_name, sample_bytes):
                        f" single-thread oracle replay + CRC verdict + hash-map keydir, {reps} pass(es)")
 
 
+def shard_config(cfg_name, rank):
+    """The corpus rank `rank` replays: its own C3-shaped shard of independent
+    files (seed + rank), so no data-path collective is needed."""
+    cfg = dict(CONFIGS[cfg_name])
+    cfg["seed"] = cfg["seed"] + rank
+    return cfg
+
+
+def reduce_over_ranks(dist, elapsed, nbytes, device):
+    """Whole-job timing: the slowest rank's time and the bytes of all ranks."""
+    if dist is None:
+        return elapsed, float(nbytes)
+    import torch
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    b = torch.tensor([float(nbytes)], dtype=torch.float64, device=device)
+    dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(b.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,8 +114,7 @@ def main():
 
     import gocask_amd as g
 
-    cfg = dict(CONFIGS[args.config])
-    cfg["seed"] = cfg["seed"] + rank  # each rank: its own shard of independent files
+    cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
     ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10)
     info = ctx.encode(**cfg)
@@ -120,15 +140,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
     my_bytes = st["bytes"]
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        b = torch.tensor([my_bytes], dtype=torch.float64, device="cuda")
-        dist.all_reduce(b, op=dist.ReduceOp.SUM)
-        total_bytes = float(b.item())
-    else:
-        total_bytes = float(my_bytes)
+    elapsed, total_bytes = reduce_over_ranks(dist, elapsed, my_bytes, "cuda")
 
     stream_gbs = None
     if rank == 0:
