@@ -25,6 +25,8 @@ GCK_ECRC_FAILED = 7
 GCK_EINVALID_KEY = 8
 GCK_ENOT_DIR = 9
 
+GCK_OPT_SYNC = 1  # gck_opts.flags: no file-group pipeline
+
 F_TOMBSTONE = 1
 F_CRC_OK = 2
 
@@ -91,6 +93,8 @@ class GckStats(ctypes.Structure):
         ("n_overflow", ctypes.c_uint64),
         ("ms_total", ctypes.c_double),
         ("ms_kernel", ctypes.c_double * 12),
+        ("pipelined", ctypes.c_uint32),
+        ("n_sync_reruns", ctypes.c_uint32),
     ]
 
 

@@ -79,12 +79,13 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
+    o.flags = _lib.GCK_OPT_SYNC if sync else 0
     return o
 
 
@@ -222,14 +223,15 @@ def _result(res: GckResult):
                       files_walked=res.files_walked)
 
 
-def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)), ctypes.byref(res))
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, sync)),
+                      ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
         return _result(res)
@@ -254,10 +256,10 @@ def keydir(files, recs):
 class ReplayContext:
     """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
 
-    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
-        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, sync)),
                                      ctypes.byref(self._h)))
 
     def load(self, files, reset_after=None):
@@ -297,9 +299,15 @@ class ReplayContext:
     def stats(self):
         s = GckStats()
         check(self._L.gck_ctx_stats(self._h, ctypes.byref(s)))
-        phases = {self._L.gck_phase_name(i).decode(): s.ms_kernel[i] for i in range(9)}
+        phases = {}
+        for i in range(12):
+            name = self._L.gck_phase_name(i).decode()
+            if not name:
+                break
+            phases[name] = s.ms_kernel[i]
         return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
-                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases)
+                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
+                    pipelined=bool(s.pipelined), n_sync_reruns=s.n_sync_reruns)
 
     def stream_read_ceiling(self, iters=10):
         """Plain streaming read of the resident arena: (ms per pass, GB/s)."""

@@ -46,17 +46,18 @@ struct DBuf {
 };
 
 enum Phase {
-    PH_SPEC = 0,   // k_spec_entry: speculative record start per chunk
-    PH_WALK,       // k_walk: header chain per chunk
-    PH_VALIDATE,   // k_validate + k_fixup
-    PH_SCAN,       // k_scan_chunks: record slots + per-file summary
-    PH_HOST,       // D2H summary + host bookkeeping
-    PH_COMPACT,    // k_compact: record table
-    PH_ROWIDX,     // k_row_index
-    PH_CRC,        // k_crc_rows: value CRC partials (the HBM-bound kernel)
-    PH_FINAL,      // k_finalize: CRC verdict + tuples
-    PH_COUNT
+    PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
+    PH_SCAN,          // record slots per chunk, per-file summary
+    PH_HOST,          // D2H summary + host bookkeeping (synchronous path)
+    PH_RECORDS,       // k_compact, k_row_fill / k_row_index, k_row_plan
+    PH_CRC,           // k_crc_rows (+ k_crc_rows_big): the HBM-bound kernel
+    PH_FINAL,         // k_finalize: CRC verdict + tuples
+    PH_END,           // (event) end of the run
+    PH_PIPE = PH_END, // (time) device span of the whole run
+    PH_NPHASE
 };
+
+constexpr int kMaxGroups = 16;  // file groups of the pipelined run
 
 struct Ctx {
     int device = 0;
@@ -77,10 +78,13 @@ struct Ctx {
     uint32_t n_chunks = 0;
     DBuf d_fbase, d_flen, d_ffirst, d_fnch, d_fbad, d_fterm, d_ftpos, d_fnrec, d_ffirstrec, d_carry;
     DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
-    DBuf d_rec_base, d_scratch_off, d_scratch_hdr, d_counters;
+    DBuf d_rec_base, d_bsum, d_scratch_off, d_scratch_hdr, d_counters;
+    DBuf d_freset;                   // per file: 1 = lastOffset resets after it
+    DBuf d_gbase, d_gcarry, d_gcnt;  // per file group: record base, lastOffset in, counters
 
     // records
     uint64_t n_recs = 0;
+    uint64_t rec_cap = 0;  // record-table capacity of the current run
     DBuf d_rec_off, d_rec_hdr, d_rec_file, d_e, d_pre, d_out;
     // rows
     uint64_t n_rows = 0;
@@ -93,8 +97,16 @@ struct Ctx {
     int32_t status = 0;
     uint32_t err_file = 0, files_walked = 0, final_last_offset = 0;
     uint64_t err_off = 0, n_crc_fail = 0, n_fixups = 0, n_overflow = 0;
-    double ms_total = 0, ms_phase[PH_COUNT] = {};
-    hipEvent_t ev[PH_COUNT + 1] = {};
+    double ms_total = 0, ms_phase[PH_NPHASE] = {};
+    hipEvent_t ev[PH_END + 1] = {};
+    bool pipelined = false;
+    uint32_t n_sync_reruns = 0;
+
+    // pipelined run: streams, file groups (first file of each, plus nfiles), events
+    hipStream_t s_crc = nullptr, s_fin = nullptr;
+    std::vector<uint32_t> g_file;
+    hipEvent_t ev_start = nullptr, ev_end = nullptr;
+    std::vector<hipEvent_t> ev_bnd, ev_crc0, ev_crc1, ev_fin0, ev_fin1;
 
     // encoder bookkeeping
     std::vector<uint32_t> walk_to_creation;

@@ -117,12 +117,21 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
 }
 
 // ------------------------------------------------------------------ kernels ---
+// Bit 7 of each byte of the result is set iff that byte of w is zero (exact).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {
+    return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+}
+
 // One wavefront per chunk finds the first byte position >= chunk start whose
 // header and the next kHops headers are plausible (chunk 0 of a file starts at
-// 0).  Each pass tests 1 KiB of positions: lane l loads bytes [16l, 16l+32) of
-// the window and checks its 16 candidate offsets in registers.  A hit at p is
-// replaced by p+1 when p+1 chains too: every true header has a plausible
-// "shadow" one byte earlier (Timestamp's top byte + KeySize<<8, ValueSize<<8).
+// 0).  Each pass covers 4 KiB of positions, 64 per lane.  Prefilter: a header
+// at p with KeySize <= 65535 (tombstones: KeySize 0) has bytes p+10 and p+11
+// zero, so the lane flags positions whose bytes 10, 11 are a zero pair (about
+// 2 VALU per position; in value bytes a zero pair is rare) and only flagged
+// positions get the full chain test.  A hit at p is replaced by p+1 when p+1
+// chains too: every true header has a plausible "shadow" one byte earlier
+// (Timestamp's top byte + KeySize<<8, ValueSize<<8).  Keys longer than 65535
+// bytes are never speculated here; validation finds their chunks and re-walks.
 __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ fbase,
                                                     const uint64_t *__restrict__ flen,
@@ -136,33 +145,45 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     if (c >= n_chunks) return;
     const uint32_t f = ch_file[c];
     const uint64_t cs = ch_start[c], ce = ch_end[c], base = fbase[f], len = flen[f];
+    const uint32_t mk = min(max_key, 65535u);
     uint64_t found = kNone;
     if (cs == 0) {
         found = 0;
     } else {
-        for (uint64_t b0 = cs; b0 < ce && found == kNone; b0 += 1024) {
-            const uint64_t p0 = b0 + 16ull * lane;
-            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + p0);  // 16 B aligned
-            const uint4 m0 = src[0], m1 = src[1];
-            const uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
-            uint32_t cm = 0;
+        for (uint64_t b0 = cs; b0 < ce && found == kNone; b0 += 4096) {
+            const uint64_t p0 = b0 + 64ull * lane;
+            // bytes [p0, p0+80): the 64 positions plus their header bytes (arena
+            // is 16 B aligned here and padded past every file)
+            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + p0);
+            uint32_t w[20];
 #pragma unroll
-            for (int t = 0; t < 16; ++t) {
-                const int o = t + 8, k = o >> 2, sh = o & 3;
-                const uint32_t ks = ab(w[k + 1], w[k], sh), vs = ab(w[k + 2], w[k + 1], sh);
-                const uint32_t klen = ks ? ks : vs;
-                const uint64_t p = p0 + t;
-                const bool ok = p < ce && klen != 0 && klen <= max_key && p + 16 + (uint64_t)ks + vs <= len;
-                cm |= (ok ? 1u : 0u) << t;
+            for (int k = 0; k < 5; ++k) {
+                const uint4 v = src[k];
+                w[4 * k] = v.x;
+                w[4 * k + 1] = v.y;
+                w[4 * k + 2] = v.z;
+                w[4 * k + 3] = v.w;
+            }
+            uint32_t zf[20];
+#pragma unroll
+            for (int k = 2; k < 20; ++k) zf[k] = zero_bytes(w[k]);
+            uint64_t cm = 0;  // bit t: bytes p0+t+10, p0+t+11 both zero
+#pragma unroll
+            for (int k = 2; k <= 18; ++k) {
+                const uint32_t pr = zf[k] & ((zf[k] >> 8) | (zf[k + 1] << 24));
+                const uint32_t nib = ((pr >> 7) & 1u) | ((pr >> 14) & 2u) | ((pr >> 21) & 4u) | ((pr >> 28) & 8u);
+                const int t0 = 4 * k - 10;
+                cm |= t0 >= 0 ? (uint64_t)nib << t0 : (uint64_t)(nib >> -t0);
             }
             uint64_t lanes = __ballot(cm != 0);
             while (lanes && found == kNone) {
                 const int l = __ffsll((long long)lanes) - 1;
-                uint32_t lm = __builtin_amdgcn_readlane(cm, l);
+                uint64_t lm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cm >> 32), l) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cm, l);
                 while (lm) {
-                    const int t = __ffs(lm) - 1;
-                    const uint64_t q = b0 + 16ull * l + t;
-                    if (chain_ok(arena, base, len, q, max_key)) {
+                    const int t = __ffsll((long long)lm) - 1;
+                    const uint64_t q = b0 + 64ull * l + t;
+                    if (q < ce && chain_ok(arena, base, len, q, mk)) {
                         found = q;
                         break;
                     }
@@ -171,7 +192,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 lanes &= lanes - 1;
             }
         }
-        if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, max_key)) found += 1;
+        if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, mk)) found += 1;
     }
     if (lane == 0) ch_entry[c] = found;
 }
@@ -232,9 +253,9 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
                                                   const uint32_t *__restrict__ ch_term,
                                                   const uint32_t *__restrict__ f_first_chunk,
                                                   uint32_t *__restrict__ ch_bad, uint32_t *counter,
-                                                  uint32_t n_chunks) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
+                                                  uint32_t c_begin, uint32_t c_end) {
+    const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= c_end) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
     bool bad = false;
     if (c != fc) {
@@ -268,9 +289,9 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                                                const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
                                                uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
                                                uint64_t *ch_tpos, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
-                                               uint32_t n_chunks, uint32_t *counter) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks || !ch_bad[c]) return;
+                                               uint32_t c_begin, uint32_t c_end, uint32_t *counter) {
+    const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= c_end || !ch_bad[c]) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
     uint32_t j = c - 1;
     while (j > fc && ch_entry[j] == kNone && !ch_bad[j]) --j;
@@ -286,29 +307,69 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                     ch_tpos);
 }
 
-// Exclusive scan of per-chunk record counts (single workgroup; n <= ~1M).
-__global__ __launch_bounds__(1024) void k_scan_chunks(const uint32_t *__restrict__ ch_count,
-                                                      uint64_t *__restrict__ rec_base, uint32_t n) {
-    __shared__ uint64_t s[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (n + 1023) / 1024;
-    const uint32_t b = t * per, e = min(b + per, n);
-    uint64_t sum = 0;
-    for (uint32_t i = b; i < e; ++i) sum += ch_count[i];
-    s[t] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const uint64_t v = t >= (uint32_t)d ? s[t - d] : 0;
-        __syncthreads();
-        s[t] += v;
-        __syncthreads();
+// Exclusive scan of per-chunk record counts -> rec_base[0..n], offset by a
+// device-resident base (the records of earlier file groups), without LDS (so
+// the kernels can share CUs with k_crc_rows, which holds all of it):
+// one wavefront per block of 4096 counts, one wavefront over the block totals,
+// then an add-back.  rec_base[n] and *base_out = base + total.
+constexpr uint32_t kScanBlock = 4096;
+
+// Inclusive prefix sum over the 64 lanes (DPP row shifts + row broadcasts).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+__global__ __launch_bounds__(64) void k_scan_local(const uint32_t *__restrict__ ch_count,
+                                                   uint64_t *__restrict__ rec_base, uint64_t *__restrict__ bsum,
+                                                   uint32_t n) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t b0 = blockIdx.x * kScanBlock;
+    uint64_t run = 0;
+    for (uint32_t i0 = b0; i0 < min(b0 + kScanBlock, n); i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t v = i < n ? ch_count[i] : 0u;
+        const uint32_t inc = wave_incl_sum(v);
+        if (i < n) rec_base[i] = run + inc - v;
+        run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
     }
-    uint64_t run = s[t] - sum;
-    for (uint32_t i = b; i < e; ++i) {
-        rec_base[i] = run;
-        run += ch_count[i];
+    if (lane == 0) bsum[blockIdx.x] = run;
+}
+
+__global__ __launch_bounds__(64) void k_scan_top(uint64_t *__restrict__ bsum, uint32_t nb,
+                                                 const uint64_t *__restrict__ base_in, uint64_t *__restrict__ base_out,
+                                                 uint64_t *__restrict__ rec_base, uint32_t n, uint64_t cap,
+                                                 uint32_t *__restrict__ overflow) {
+    const uint32_t lane = threadIdx.x;
+    uint64_t run = *base_in;
+    for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint64_t v = i < nb ? bsum[i] : 0u;
+        // block totals can exceed 32 bits in sum: scan the two halves
+        const uint32_t lo = wave_incl_sum((uint32_t)(v & 0xFFFFFFu));
+        const uint32_t hi = wave_incl_sum((uint32_t)(v >> 24));
+        const uint64_t inc = ((uint64_t)hi << 24) + lo;
+        if (i < nb) bsum[i] = run + inc - v;
+        run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
+               (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
     }
-    if (t == 1023) rec_base[n] = s[1023];
+    if (lane == 0) {
+        // past the record-table capacity the range is clamped (later kernels
+        // stay in bounds) and the run is flagged for the exact synchronous path
+        if (run > cap) atomicAdd(overflow, 1u);
+        rec_base[n] = min(run, cap);
+        *base_out = min(run, cap);
+    }
+}
+
+__global__ void k_scan_add(uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ bsum, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) rec_base[i] += bsum[i / kScanBlock];
 }
 
 // Per-file summary: records of the file and its terminal condition.
@@ -399,17 +460,47 @@ __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uin
     return rec_off[r] + 16 + (uint64_t)h.z + h.w;  // tombstone: KeySize 0, the key is the "value"
 }
 
-// row_first[row] = first record whose value ends after the row's first byte.
+// Record range [rng[0], rng[1]) of one file group (device-resident: the group
+// scans of the pipeline produce them without a host round trip).
+//
+// row_first[row] = first record whose value ends after the row's first byte,
+// for the rows [r0, ...) of the group; rows past the group's last record end
+// keep k_row_fill's value rng[1].  Grid-stride over the device range.
+__global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64_t r1,
+                           const uint64_t *__restrict__ rng) {
+    const uint32_t v = (uint32_t)rng[1];
+    for (uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
+         row += (uint64_t)gridDim.x * blockDim.x)
+        row_first[row] = v;
+}
+
 __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                            uint64_t n_total, uint64_t n_rows, uint32_t *__restrict__ row_first) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_total) return;
-    const uint64_t ve_r = value_end(rec_off, rec_hdr, r);
-    const uint64_t ve_p = r ? value_end(rec_off, rec_hdr, r - 1) : 0;
-    const uint64_t lo = (ve_p + kRow - 1) / kRow, hi = (ve_r + kRow - 1) / kRow;
-    for (uint64_t row = lo; row < hi; ++row) row_first[row] = (uint32_t)r;
-    if (r == n_total - 1)
-        for (uint64_t row = hi; row <= n_rows; ++row) row_first[row] = (uint32_t)n_total;
+                            const uint64_t *__restrict__ rng, uint64_t r0, uint32_t *__restrict__ row_first) {
+    const uint64_t rb = rng[0], re = rng[1];
+    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ve_r = value_end(rec_off, rec_hdr, r);
+        const uint64_t lo = r == rb ? r0 : (value_end(rec_off, rec_hdr, r - 1) + kRow - 1) / kRow;
+        const uint64_t hi = (ve_r + kRow - 1) / kRow;
+        for (uint64_t row = lo; row < hi; ++row) row_first[row] = (uint32_t)r;
+    }
+}
+
+// lastOffset carried into each file of a group (core/db.go:110-123,
+// core/keydir.go:22-53): after a file it is reset iff the file is not the
+// active one, else advanced by the bytes the walk consumed.  One thread; the
+// group's outgoing value feeds the next group.
+__global__ void k_group_carry(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
+                              const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
+                              uint32_t *__restrict__ carry, const uint32_t *__restrict__ carry_in,
+                              uint32_t *__restrict__ carry_out) {
+    uint32_t last = *carry_in;
+    for (uint32_t f = 0; f < nf; ++f) {
+        carry[f] = last;
+        last += (uint32_t)(fterm[f] != T_NONE ? ftpos[f] : flen[f]);
+        if (freset[f]) last = 0;
+    }
+    *carry_out = last;
 }
 
 constexpr int kPlanBytes = 64;  // per row: one byte per 64 B slab (= per k_crc_rows lane)
@@ -433,10 +524,11 @@ __device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ 
 // Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
 // plan carries no ids or counts.
 __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                           uint64_t n_total, uint64_t n_rows, const uint32_t *__restrict__ row_first,
-                           uint4 *__restrict__ plan, uint32_t *__restrict__ big_rows, uint32_t *big_count) {
-    const uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= n_rows) return;
+                           const uint64_t *__restrict__ rng, uint64_t r0, uint64_t nr,
+                           const uint32_t *__restrict__ row_first, uint4 *__restrict__ plan,
+                           uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+    const uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= r0 + nr) return;
     const uint32_t ra = row_first[row], rb = row_first[row + 1];
     const uint64_t rs = row * kRow;
     uint32_t w[16];
@@ -455,7 +547,7 @@ __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__
         for (int i = 0; i < 16; ++i) w[i] |= (slab >> 2) == i ? cc << (8 * (slab & 3)) : 0u;
     }
     if (slow) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
-    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, n_total, rb, rs) << 32) |
+    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, rs) << 32) |
                        ((uint64_t)slow << 45);
 #pragma unroll
     for (int k = 0; k < 64; ++k) w[k >> 2] |= (uint32_t)((H >> k) & 1u) << (8 * (k & 3) + 7);
@@ -702,6 +794,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
 // more (records under 64 B) are flagged by k_row_plan and done by
 // k_crc_rows_big (their stores here go to the scratch slots).
 //
+// Rows are local to the launch: arena, plan and out_rend point at its first
+// row; n_total is the e/pre scratch slot, rend_scratch the rend one.
+//
 // Memory pipeline: the row data (4 x 16 B per lane) and the row plan byte are
 // buffer loads (row base in a scalar resource, lane offset in a fixed VGPR)
 // issued DEPTH rows ahead.  No scalar loads in the loop: an outstanding SMEM
@@ -714,7 +809,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib,
                                                    uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
-                                                   uint32_t *__restrict__ out_rend) {
+                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch) {
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
@@ -772,7 +867,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const uint64_t slot = (cc != 0 && !slow) ? (uint64_t)ra + idx : n_total;
         out_e[slot] = o.e;
         out_pre[slot] = o.pre;
-        out_rend[slow ? n_rows : row] = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+        *(slow ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
     };
     // DEPTH rows in flight while one is processed; the loop is unrolled over
     // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
@@ -786,7 +881,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         // the compiler's waits at the loop head are as late as in the body
         out_e[n_total] = 0;
         out_pre[n_total] = 0;
-        out_rend[n_rows] = 0;
+        *rend_scratch = 0;
     }
     for (;;) {
 #pragma unroll
@@ -806,7 +901,8 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict__ arena,
                                                        const uint32_t *__restrict__ big_rows,
                                                        const uint32_t *__restrict__ big_count,
-                                                       const uint32_t *__restrict__ row_first, uint64_t n_total,
+                                                       const uint32_t *__restrict__ row_first,
+                                                       const uint64_t *__restrict__ rng,
                                                        const uint64_t *__restrict__ rec_off,
                                                        const uint4 *__restrict__ rec_hdr,
                                                        const uint32_t *__restrict__ g_slice,
@@ -815,6 +911,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
                                                        uint32_t *__restrict__ out_rend) {
     const uint32_t nbig = *big_count;
     if (blockIdx.x * kWaves >= nbig) return;
+    const uint64_t n_total = rng[1];
     __shared__ uint32_t lds[40960];
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
@@ -865,7 +962,7 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
                                                   const uint4 *__restrict__ rec_hdr,
                                                   const uint32_t *__restrict__ rec_file,
                                                   const uint64_t *__restrict__ fbase,
-                                                  const uint32_t *__restrict__ carry, uint64_t n_total,
+                                                  const uint32_t *__restrict__ carry, const uint64_t *__restrict__ rng,
                                                   const uint32_t *__restrict__ e, const uint32_t *__restrict__ pre,
                                                   const uint32_t *__restrict__ rend,
                                                   const uint32_t *__restrict__ g_slice,
@@ -873,14 +970,12 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
                                                   const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
-    __shared__ uint32_t Tz[1024];
-    __shared__ uint32_t T0[256];
-    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) Tz[i] = zrow[i];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) T0[i] = g_slice[i];
-    __syncthreads();
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool reject = false;
-    if (r < n_total) {
+    // no LDS: the 5 KiB of tables stay in L1/L2, and the kernel can share CUs
+    // with k_crc_rows (which holds all of the LDS) in the pipelined run
+    const uint32_t *Tz = zrow, *T0 = g_slice;
+    const uint64_t rb = rng[0], re = rng[1];
+    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
+         r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t start = rec_off[r];
         const uint4 h = rec_hdr[r];
         const uint32_t f = rec_file[r];
@@ -919,10 +1014,10 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == h.x ? GCK_F_CRC_OK : 0u);
         o.crc_calc = calc;
         out[r] = o;
-        reject = calc != h.x;
+        const uint64_t m = __ballot(calc != h.x);  // one atomic per wavefront with rejects
+        if (m && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
+            atomicAdd(&counters[3], (uint32_t)__popcll(m));
     }
-    const uint64_t m = __ballot(reject);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&counters[3], (uint32_t)__popcll(m));
 }
 
 // ------------------------------------------------------------- host side ---
@@ -999,7 +1094,14 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // the CRC stream carries the critical path of the pipelined run
+    int prio_lo = 0, prio_hi = 0;
+    GCK_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    GCK_HIP(hipStreamCreateWithPriority(&c->s_crc, hipStreamNonBlocking, prio_hi));
+    GCK_HIP(hipStreamCreateWithFlags(&c->s_fin, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
+    GCK_HIP(hipEventCreate(&c->ev_start));
+    GCK_HIP(hipEventCreate(&c->ev_end));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow, zl;
     make_tables(slice, nib, xinv, xa, xb, zrow, zl);
@@ -1023,14 +1125,23 @@ static void ctx_free(Ctx *c) {
     DBuf *all[] = {&c->arena, &c->d_fbase, &c->d_flen, &c->d_ffirst, &c->d_fnch, &c->d_fbad, &c->d_fterm,
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
-                   &c->d_rec_base, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
+                   &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
-                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl};
+                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    c->stream = nullptr;
+    for (auto *v : {&c->ev_bnd, &c->ev_crc0, &c->ev_crc1, &c->ev_fin0, &c->ev_fin1}) {
+        for (auto e : *v) (void)hipEventDestroy(e);
+        v->clear();
+    }
+    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+    if (c->ev_end) (void)hipEventDestroy(c->ev_end);
+    for (hipStream_t *st : {&c->stream, &c->s_crc, &c->s_fin}) {
+        if (*st) (void)hipStreamDestroy(*st);
+        *st = nullptr;
+    }
 }
 
 // Place files (walk order) in the arena and build the chunk table.
@@ -1077,7 +1188,8 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_end.ensure((nc + 1) * 8)) || (rc = c->d_ch_entry.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
-        (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
+        (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
+        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)))
         return rc;
@@ -1086,6 +1198,8 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         GCK_HIP(hipMemcpy(c->d_flen.p, c->f_len.data(), nfiles * 8, hipMemcpyHostToDevice));
         GCK_HIP(hipMemcpy(c->d_ffirst.p, c->f_first_chunk.data(), nfiles * 4, hipMemcpyHostToDevice));
         GCK_HIP(hipMemcpy(c->d_fnch.p, c->f_nchunks.data(), nfiles * 4, hipMemcpyHostToDevice));
+        std::vector<uint32_t> rs(reset_after, reset_after + nfiles);
+        GCK_HIP(hipMemcpy(c->d_freset.p, rs.data(), nfiles * 4, hipMemcpyHostToDevice));
     }
     if (nc) {
         GCK_HIP(hipMemcpy(c->d_ch_file.p, ch_file.data(), nc * 4, hipMemcpyHostToDevice));
@@ -1097,110 +1211,137 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
 
 static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-static int ctx_run(Ctx *c) {
-    const auto t0 = std::chrono::steady_clock::now();
-    GCK_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint32_t nc = c->n_chunks, nf = c->nfiles, cap = c->opts.chunk_cap;
-    uint32_t *cnt = c->d_counters.as<uint32_t>();
-    GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
-    if (nf) {
-        GCK_HIP(hipMemsetAsync(c->d_fbad.p, 0xFF, nf * 4, s));
-    }
-    GCK_HIP(hipEventRecord(c->ev[PH_SPEC], s));
-    if (nc) {
-        k_spec_entry<<<nblk(nc, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
-                                                 c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                                 c->d_ch_start.as<uint64_t>(), c->d_ch_end.as<uint64_t>(),
-                                                 c->d_ch_entry.as<uint64_t>(), nc, c->opts.max_key);
-    }
-    GCK_HIP(hipEventRecord(c->ev[PH_WALK], s));
-    if (nc) {
-        k_walk<<<nblk(nc, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
+// Counter slots (d_counters, u32): 1 fixups, 2 chunks whose stage overflowed
+// (re-walked by k_compact), 3 CRC rejects, 5 big rows (sync path), 6 record-
+// table capacity overflow (pipelined path), 8.. validation rounds (sync path),
+// 15 host validation loop.
+enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_BIG = 5, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
+// Per-group counter slots (d_gcnt, 8 x u32 per group).
+enum : int { G_BIG = 0, G_VAL = 1 };  // G_VAL + round: validation rounds, the last one must be 0
+constexpr int kRounds = 2;             // device validation/fixup rounds
+
+// Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
+// kRounds validate/fixup rounds and a final validation counted at val_cnt[kRounds].
+static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt) {
+    const uint32_t n = c1 - c0, cap = c->opts.chunk_cap;
+    if (!n) return;
+    k_spec_entry<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+                                            c->d_ch_file.as<uint32_t>() + c0, c->d_ch_start.as<uint64_t>() + c0,
+                                            c->d_ch_end.as<uint64_t>() + c0, c->d_ch_entry.as<uint64_t>() + c0, n,
+                                            c->opts.max_key);
+    k_walk<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+                                        c->d_ch_file.as<uint32_t>() + c0, c->d_ch_end.as<uint64_t>() + c0,
+                                        c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
+                                        c->d_ch_exit.as<uint64_t>() + c0, c->d_ch_term.as<uint32_t>() + c0,
+                                        c->d_ch_tpos.as<uint64_t>() + c0,
+                                        c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * cap,
+                                        c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * cap, cap, n);
+    for (int r = 0; r <= kRounds; ++r) {
+        k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
+                                                c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
+                                                c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
+                                                c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(), val_cnt + r, c0,
+                                                c1);
+        if (r == kRounds) break;
+        k_fixup<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
                                              c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                             c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
+                                             c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
+                                             c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
                                              c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
                                              c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                             c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, nc);
+                                             c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, c0, c1,
+                                             c->d_counters.as<uint32_t>() + CNT_FIXUP);
     }
-    GCK_HIP(hipEventRecord(c->ev[PH_VALIDATE], s));
-    // validation rounds: validate -> fixup -> validate -> fixup -> validate
-    auto validate = [&](uint32_t *counter) {
-        k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
-                                                 c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                 c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-                                                 c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(), counter, nc);
-    };
-    auto fixup = [&]() {
-        k_fixup<<<nblk(nc, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
-                                              c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                              c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
-                                              c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
-                                              c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
-                                              c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, nc,
-                                              cnt + 1);
-    };
-    constexpr int kRounds = 2;
-    if (nc) {
-        for (int r = 0; r < kRounds; ++r) {
-            validate(cnt + 8 + r);
-            fixup();
-        }
-        validate(cnt + 8 + kRounds);
-    }
-    auto summarize = [&]() {
-        if (nc) {
-            k_scan_chunks<<<1, 1024, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), nc);
-        } else {
-            (void)hipMemsetAsync(c->d_rec_base.p, 0, 8, s);
-        }
-        if (nf) {
-            k_file_summary<<<nblk(nf, 64), 64, 0, s>>>(c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(),
-                                                       c->d_rec_base.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                       c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                                       c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(),
-                                                       c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(), nf);
-        }
-    };
-    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
-    summarize();
-    GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
+}
 
-    // ---- host: EOF classification + lastOffset carries (core/db.go:110-140) ----
-    std::vector<uint32_t> fterm(nf), carry(nf);
-    std::vector<uint64_t> ftpos(nf), ffirst(nf), fnrec(nf);
-    if (nf) {
-        GCK_HIP(hipMemcpyAsync(fterm.data(), c->d_fterm.p, nf * 4, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipMemcpyAsync(ftpos.data(), c->d_ftpos.p, nf * 8, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipMemcpyAsync(ffirst.data(), c->d_ffirstrec.p, nf * 8, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipMemcpyAsync(fnrec.data(), c->d_fnrec.p, nf * 8, hipMemcpyDeviceToHost, s));
-    }
-    uint32_t hcnt[16] = {};
-    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
-    GCK_HIP(hipStreamSynchronize(s));
-    // rare: inconsistencies left after the device rounds (cascading mis-speculation)
-    for (uint32_t left = hcnt[8 + kRounds]; left;) {
-        fixup();
-        GCK_HIP(hipMemsetAsync(cnt + 15, 0, 4, s));
-        validate(cnt + 15);
-        uint32_t v = 0;
-        GCK_HIP(hipMemcpyAsync(&v, cnt + 15, 4, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipStreamSynchronize(s));
-        left = v;
-        if (!left) {
-            summarize();
-            if (nf) {
-                GCK_HIP(hipMemcpyAsync(fterm.data(), c->d_fterm.p, nf * 4, hipMemcpyDeviceToHost, s));
-                GCK_HIP(hipMemcpyAsync(ftpos.data(), c->d_ftpos.p, nf * 8, hipMemcpyDeviceToHost, s));
-                GCK_HIP(hipMemcpyAsync(ffirst.data(), c->d_ffirstrec.p, nf * 8, hipMemcpyDeviceToHost, s));
-                GCK_HIP(hipMemcpyAsync(fnrec.data(), c->d_fnrec.p, nf * 8, hipMemcpyDeviceToHost, s));
-            }
-            GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
-            GCK_HIP(hipStreamSynchronize(s));
-        }
-    }
-    c->n_fixups = hcnt[1];
+// Record slots of chunks [c0, c1) after the records of earlier groups
+// (gbase[0] -> gbase[1]), and the summary of files [f0, f1).
+static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t f0, uint32_t f1, uint64_t *gbase,
+                        uint64_t cap) {
+    const uint32_t n = c1 - c0, nb = nblk(n, kScanBlock);
+    uint64_t *bsum = c->d_bsum.as<uint64_t>() + c0 / kScanBlock + f0;  // disjoint per group
+    if (nb) k_scan_local<<<nb, 64, 0, s>>>(c->d_ch_count.as<uint32_t>() + c0, c->d_rec_base.as<uint64_t>() + c0, bsum, n);
+    k_scan_top<<<1, 64, 0, s>>>(bsum, nb, gbase, gbase + 1, c->d_rec_base.as<uint64_t>() + c0, n, cap,
+                                c->d_counters.as<uint32_t>() + CNT_CAP);
+    if (n) k_scan_add<<<nblk(n, 256), 256, 0, s>>>(c->d_rec_base.as<uint64_t>() + c0, bsum, n);
+    if (f1 > f0)
+        k_file_summary<<<nblk(f1 - f0, 64), 64, 0, s>>>(
+            c->d_ffirst.as<uint32_t>() + f0, c->d_fnch.as<uint32_t>() + f0, c->d_rec_base.as<uint64_t>(),
+            c->d_ch_entry.as<uint64_t>(), c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
+            c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0, c->d_ffirstrec.as<uint64_t>() + f0,
+            c->d_fnrec.as<uint64_t>() + f0, f1 - f0);
+}
+
+// Record table of chunks [c0, c1), row index and row plan of rows [r0, r1).
+static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
+                           const uint64_t *rng, uint64_t cap, uint32_t *big_count) {
+    const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
+    if (n)
+        k_compact<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_end.as<uint64_t>() + c0,
+                                             c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
+                                             c->d_rec_base.as<uint64_t>() + c0,
+                                             c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * ccap,
+                                             c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * ccap, ccap, n, cap,
+                                             c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+                                             c->d_rec_file.as<uint32_t>(), c->d_counters.as<uint32_t>());
+    const uint32_t grid = (uint32_t)c->n_cu * 4;
+    k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
+    k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
+                                     c->d_row_first.as<uint32_t>());
+    if (r1 > r0)
+        k_row_plan<<<nblk(r1 - r0, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
+                                                      r1 - r0, c->d_row_first.as<uint32_t>(), c->d_plan.as<uint4>(),
+                                                      c->d_big.as<uint32_t>() + r0, big_count);
+}
+
+// CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
+// k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
+static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
+                       const uint32_t *big_count) {
+    if (r1 <= r0) return;
+    const uint64_t nr = r1 - r0, want = (nr + kWaves - 1) / kWaves;
+    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
+    k_crc_rows<0, kDepth><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>() + r0 * kRow, nr,
+                                                c->d_plan.as<uint8_t>() + r0 * kPlanBytes, cap,
+                                                c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
+                                                c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
+                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
+    k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0, big_count,
+                                              c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
+                                              c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
+                                              c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
+                                              c->d_rend.as<uint32_t>());
+}
+
+static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
+    if (!max_recs) return;
+    const uint64_t want = nblk(max_recs, 256);
+    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu * 8 ? want : (uint64_t)c->n_cu * 8);
+    k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+                                    c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
+                                    rng, c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>(),
+                                    c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_zrow.as<uint32_t>(),
+                                    c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
+                                    c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
+}
+
+static int ensure_records(Ctx *c, uint64_t nr) {
+    nr = nr ? nr : 1;
+    int rc;
+    if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_hdr.ensure(nr * 16)) ||
+        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_e.ensure((nr + 65) * 4)) ||
+        (rc = c->d_pre.ensure((nr + 65) * 4)) || (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
+        return rc;
+    return GCK_OK;
+}
+
+// Host bookkeeping from the per-file summaries (core/db.go:110-140): status,
+// files walked, final lastOffset, records in walk order; carries if asked.
+static uint64_t account_files(Ctx *c, const std::vector<uint32_t> &fterm, const std::vector<uint64_t> &ftpos,
+                              const std::vector<uint64_t> &ffirst, const std::vector<uint64_t> &fnrec,
+                              std::vector<uint32_t> *carry) {
+    const uint32_t nf = c->nfiles;
     c->status = GCK_OK;
     c->err_file = 0;
     c->err_off = 0;
@@ -1208,7 +1349,7 @@ static int ctx_run(Ctx *c) {
     uint64_t n_total = 0;
     uint32_t last = 0;  // keyDir.lastOffset at the start of each file
     for (uint32_t f = 0; f < nf; ++f) {
-        carry[f] = last;
+        if (carry) (*carry)[f] = last;
         const uint64_t valid = fterm[f] != T_NONE ? ftpos[f] : c->f_len[f];
         n_total = ffirst[f] + fnrec[f];
         last += (uint32_t)valid;
@@ -1222,71 +1363,231 @@ static int ctx_run(Ctx *c) {
         if (c->f_reset[f]) last = 0;  // resetOffset (core/db.go:117-119)
     }
     c->final_last_offset = last;
-    c->n_recs = n_total;
-    if (nf) GCK_HIP(hipMemcpyAsync(c->d_carry.p, carry.data(), nf * 4, hipMemcpyHostToDevice, s));
-    const uint64_t nr = n_total ? n_total : 1;
-    int rc;
-    if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_hdr.ensure(nr * 16)) ||
-        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_e.ensure((nr + 1) * 4)) || (rc = c->d_pre.ensure((nr + 1) * 4)) ||
-        (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
-        return rc;
-    if (n_total > 0xFFFFFFF0ull) return GCK_EINVAL;
+    return n_total;
+}
 
-    GCK_HIP(hipEventRecord(c->ev[PH_COMPACT], s));
-    if (n_total) {
-        k_compact<<<nblk(nc, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
+static int read_file_summaries(Ctx *c, hipStream_t s, std::vector<uint32_t> &fterm, std::vector<uint64_t> &ftpos,
+                               std::vector<uint64_t> &ffirst, std::vector<uint64_t> &fnrec) {
+    const uint32_t nf = c->nfiles;
+    fterm.assign(nf, 0);
+    ftpos.assign(nf, 0);
+    ffirst.assign(nf, 0);
+    fnrec.assign(nf, 0);
+    if (nf) {
+        GCK_HIP(hipMemcpyAsync(fterm.data(), c->d_fterm.p, nf * 4, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(ftpos.data(), c->d_ftpos.p, nf * 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(ffirst.data(), c->d_ffirstrec.p, nf * 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(fnrec.data(), c->d_fnrec.p, nf * 8, hipMemcpyDeviceToHost, s));
+    }
+    return GCK_OK;
+}
+
+// The synchronous pipeline: every phase over all files, one host round trip
+// after the boundary phases (exact record count, EOF verdicts, carries).
+// Used for single-file corpora and as the fallback of the pipelined run.
+static int ctx_run_sync(Ctx *c) {
+    const auto t0 = std::chrono::steady_clock::now();
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t nc = c->n_chunks, nf = c->nfiles;
+    uint32_t *cnt = c->d_counters.as<uint32_t>();
+    uint64_t *gbase = c->d_gbase.as<uint64_t>();
+    GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
+    GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
+    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
+    launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
+    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
+    const uint64_t big_cap = ~0ull >> 1;
+    launch_scan(c, s, 0, nc, 0, nf, gbase, big_cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
+
+    std::vector<uint32_t> fterm, carry(nf);
+    std::vector<uint64_t> ftpos, ffirst, fnrec;
+    if (read_file_summaries(c, s, fterm, ftpos, ffirst, fnrec)) return GCK_EDEVICE;
+    uint32_t hcnt[16] = {};
+    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    // rare: inconsistencies left after the device rounds (cascading mis-speculation)
+    for (uint32_t left = hcnt[CNT_VAL + kRounds]; left;) {
+        k_fixup<<<nblk(nc, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
                                               c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                              c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                              c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(),
-                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap,
-                                              nc, n_total, c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
-                                              c->d_rec_file.as<uint32_t>(), cnt);
+                                              c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
+                                              c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
+                                              c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
+                                              c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
+                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(),
+                                              c->opts.chunk_cap, 0u, nc, cnt + CNT_FIXUP);
+        GCK_HIP(hipMemsetAsync(cnt + CNT_HOSTVAL, 0, 4, s));
+        k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
+                                                 c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
+                                                 c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
+                                                 c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
+                                                 cnt + CNT_HOSTVAL, 0u, nc);
+        uint32_t v = 0;
+        GCK_HIP(hipMemcpyAsync(&v, cnt + CNT_HOSTVAL, 4, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        left = v;
+        if (!left) {
+            launch_scan(c, s, 0, nc, 0, nf, gbase, big_cap);
+            if (read_file_summaries(c, s, fterm, ftpos, ffirst, fnrec)) return GCK_EDEVICE;
+            GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
+            GCK_HIP(hipStreamSynchronize(s));
+        }
     }
-    GCK_HIP(hipEventRecord(c->ev[PH_ROWIDX], s));
-    if (n_total) {
-        k_row_index<<<nblk(n_total, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
-                                                      n_total, c->n_rows, c->d_row_first.as<uint32_t>());
-        k_row_plan<<<nblk(c->n_rows, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
-                                                       n_total, c->n_rows, c->d_row_first.as<uint32_t>(),
-                                                       c->d_plan.as<uint4>(), c->d_big.as<uint32_t>(), cnt + 5);
-    } else {
-        GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, (c->n_rows + 1) * 4, s));
-    }
+    c->n_fixups = hcnt[CNT_FIXUP];
+    const uint64_t n_total = account_files(c, fterm, ftpos, ffirst, fnrec, &carry);
+    c->n_recs = n_total;
+    if (n_total > 0xFFFFFFF0ull) return GCK_EINVAL;
+    int rc;
+    if ((rc = ensure_records(c, n_total))) return rc;
+    c->rec_cap = n_total;
+    const uint64_t rng_h[2] = {0, n_total};
+    if (nf) GCK_HIP(hipMemcpyAsync(c->d_carry.p, carry.data(), nf * 4, hipMemcpyHostToDevice, s));
+    GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
+
+    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
+    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (c->n_rows && n_total) {
-        const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
-        const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-        k_crc_rows<0, kDepth><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), n_total,
-                                         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
-                                         c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
-        k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>(), cnt + 5,
-                                                  c->d_row_first.as<uint32_t>(), n_total, c->d_rec_off.as<uint64_t>(),
-                                                  c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
-                                                  c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(),
-                                                  c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>());
-    }
+    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
-    if (n_total) {
-        k_finalize<<<nblk(n_total, 256), 256, 0, s>>>(
-            c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), c->d_rec_file.as<uint32_t>(),
-            c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(), n_total, c->d_e.as<uint32_t>(),
-            c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>(), c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
-            c->d_zrow.as<uint32_t>(),
-            c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(), c->d_out.as<gck_rec>(), cnt);
-    }
-    GCK_HIP(hipEventRecord(c->ev[PH_COUNT], s));
+    launch_finalize(c, s, gbase, n_total);
+    GCK_HIP(hipEventRecord(c->ev[PH_END], s));
     GCK_HIP(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
     GCK_HIP(hipGetLastError());
-    c->n_overflow = hcnt[2];
-    c->n_crc_fail = hcnt[3];
-    for (int p = 0; p < PH_COUNT; ++p) {
+    c->n_overflow = hcnt[CNT_STAGE];
+    c->n_crc_fail = hcnt[CNT_REJECT];
+    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
+    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
         c->ms_phase[p] = ms;
     }
+    float span = 0;
+    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
+    c->ms_phase[PH_PIPE] = span;
+    c->pipelined = false;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
+}
+
+// File groups of the pipelined run: consecutive files in walk order,
+// balanced by bytes, at most kMaxGroups.
+static void make_groups(Ctx *c) {
+    const uint32_t nf = c->nfiles;
+    c->g_file.clear();
+    const uint32_t G = nf < (uint32_t)kMaxGroups ? nf : (uint32_t)kMaxGroups;
+    c->g_file.push_back(0);
+    uint64_t acc = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+        acc += c->f_len[f];
+        const uint32_t g = (uint32_t)c->g_file.size();  // groups closed so far + 1
+        if (f + 1 < nf && g < G && acc * G >= c->data_bytes * g) c->g_file.push_back(f + 1);
+    }
+    c->g_file.push_back(nf);
+}
+
+// The pipelined run: file groups go through boundary discovery, record table
+// and row plan on stream s (in walk order, record bases and lastOffset
+// carried on the device), CRC rows on c->s_crc and finalize on c->s_fin, so
+// group g's CRC overlaps group g+1's boundary work and group g-1's finalize.
+// No host round trip until the end; anything unusual (validation not settled
+// after kRounds, record-table capacity, a startup error) reruns synchronously.
+static int ctx_run_pipe(Ctx *c) {
+    const auto t0 = std::chrono::steady_clock::now();
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t nf = c->nfiles, G = (uint32_t)c->g_file.size() - 1;
+    uint32_t *cnt = c->d_counters.as<uint32_t>();
+    uint64_t *gbase = c->d_gbase.as<uint64_t>();
+    uint32_t *gcarry = c->d_gcarry.as<uint32_t>();
+    uint32_t *gcnt = c->d_gcnt.as<uint32_t>();
+    const uint64_t cap = c->rec_cap;
+    GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
+    GCK_HIP(hipMemsetAsync(gbase, 0, (G + 1) * 8, s));
+    GCK_HIP(hipMemsetAsync(gcarry, 0, (G + 1) * 4, s));
+    GCK_HIP(hipMemsetAsync(gcnt, 0, G * 32, s));
+    GCK_HIP(hipEventRecord(c->ev_start, s));
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t f0 = c->g_file[g], f1 = c->g_file[g + 1];
+        const uint32_t c0 = c->f_first_chunk[f0], c1 = f1 < nf ? c->f_first_chunk[f1] : c->n_chunks;
+        const uint64_t r0 = c->f_base[f0] / kRow, r1 = f1 < nf ? c->f_base[f1] / kRow : c->n_rows;
+        launch_boundary(c, s, c0, c1, gcnt + g * 8 + G_VAL);
+        launch_scan(c, s, c0, c1, f0, f1, gbase + g, cap);
+        k_group_carry<<<1, 1, 0, s>>>(f1 - f0, c->d_flen.as<uint64_t>() + f0, c->d_freset.as<uint32_t>() + f0,
+                                      c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0,
+                                      c->d_carry.as<uint32_t>() + f0, gcarry + g, gcarry + g + 1);
+        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
+        GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
+        GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
+        GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
+        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
+        GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
+        GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
+        GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
+        launch_finalize(c, c->s_fin, gbase + g, (uint64_t)(c1 - c0) * c->opts.chunk_cap);
+        GCK_HIP(hipEventRecord(c->ev_fin1[g], c->s_fin));
+    }
+    std::vector<uint32_t> fterm, gc(G * 8);
+    std::vector<uint64_t> ftpos, ffirst, fnrec;
+    if (read_file_summaries(c, c->s_fin, fterm, ftpos, ffirst, fnrec)) return GCK_EDEVICE;
+    uint32_t hcnt[16] = {};
+    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, c->s_fin));
+    GCK_HIP(hipMemcpyAsync(gc.data(), gcnt, G * 32, hipMemcpyDeviceToHost, c->s_fin));
+    GCK_HIP(hipEventRecord(c->ev_end, c->s_fin));
+    GCK_HIP(hipStreamSynchronize(c->s_fin));
+    GCK_HIP(hipGetLastError());
+    bool settled = hcnt[CNT_CAP] == 0;
+    for (uint32_t g = 0; g < G; ++g) settled &= gc[g * 8 + G_VAL + kRounds] == 0;
+    const uint64_t n_total = account_files(c, fterm, ftpos, ffirst, fnrec, nullptr);
+    if (!settled || c->status != GCK_OK || n_total > 0xFFFFFFF0ull) {
+        ++c->n_sync_reruns;
+        return ctx_run_sync(c);
+    }
+    c->n_recs = n_total;
+    c->n_fixups = hcnt[CNT_FIXUP];
+    c->n_overflow = hcnt[CNT_STAGE];
+    c->n_crc_fail = hcnt[CNT_REJECT];
+    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        float a = 0, b = 0;
+        (void)hipEventElapsedTime(&a, c->ev_crc0[g], c->ev_crc1[g]);
+        (void)hipEventElapsedTime(&b, c->ev_fin0[g], c->ev_fin1[g]);
+        c->ms_phase[PH_CRC] += a;
+        c->ms_phase[PH_FINAL] += b;
+    }
+    float span = 0;
+    (void)hipEventElapsedTime(&span, c->ev_start, c->ev_end);
+    c->ms_phase[PH_PIPE] = span;
+    c->pipelined = true;
+    c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return GCK_OK;
+}
+
+static int ctx_run(Ctx *c) {
+    const bool pipe = c->nfiles >= 2 && !(c->opts.flags & GCK_OPT_SYNC);
+    if (!pipe) return ctx_run_sync(c);
+    GCK_HIP(hipSetDevice(c->device));
+    make_groups(c);
+    const uint32_t G = (uint32_t)c->g_file.size() - 1;
+    // record-table capacity: the stage bound (chunk_cap per chunk) or the last
+    // exact count, whichever is larger; beyond it the run reruns synchronously
+    const uint64_t want = std::max<uint64_t>((uint64_t)c->n_chunks * c->opts.chunk_cap, c->n_recs);
+    int rc;
+    if ((rc = ensure_records(c, want)) || (rc = c->d_gbase.ensure((G + 1) * 8)) ||
+        (rc = c->d_gcarry.ensure((G + 1) * 4)) || (rc = c->d_gcnt.ensure(G * 32)))
+        return rc;
+    c->rec_cap = want;
+    while (c->ev_bnd.size() < G) {
+        hipEvent_t e[5];
+        for (auto &x : e) GCK_HIP(hipEventCreate(&x));
+        c->ev_bnd.push_back(e[0]);
+        c->ev_crc0.push_back(e[1]);
+        c->ev_crc1.push_back(e[2]);
+        c->ev_fin0.push_back(e[3]);
+        c->ev_fin1.push_back(e[4]);
+    }
+    return ctx_run_pipe(c);
 }
 
 }  // namespace gck
@@ -1371,14 +1672,15 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->n_fixups = c->n_fixups;
     out->n_overflow = c->n_overflow;
     out->ms_total = c->ms_total;
-    for (int p = 0; p < PH_COUNT && p < 12; ++p) out->ms_kernel[p] = c->ms_phase[p];
+    for (int p = 0; p < PH_NPHASE && p < 12; ++p) out->ms_kernel[p] = c->ms_phase[p];
+    out->pipelined = c->pipelined ? 1u : 0u;
+    out->n_sync_reruns = c->n_sync_reruns;
     return GCK_OK;
 }
 
 const char *gck_phase_name(int phase) {
-    static const char *names[] = {"spec_entry", "walk", "validate", "scan", "host_sync",
-                                  "compact",    "row_index", "crc_rows", "finalize"};
-    return phase >= 0 && phase < PH_COUNT ? names[phase] : "";
+    static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows", "finalize", "pipeline"};
+    return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
 int gck_ctx_device_recs(gck_ctx *ctx, const gck_rec **recs, uint64_t *n) {
@@ -1453,7 +1755,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
         k_crc_rows<M, kDepth><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
                                                     c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
-                                                    c->d_rend.as<uint32_t>());                                          \
+                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows);    \
         break;
         switch (mode) {
             GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6) GCK_VARIANT(7) GCK_VARIANT(8)

@@ -80,8 +80,12 @@ typedef struct gck_opts {
     uint32_t chunk_bytes;  /* boundary-speculation chunk (default 256 KiB, power of two)  */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
     uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
-    uint32_t flags;        /* reserved, 0                                                  */
+    uint32_t flags;        /* GCK_OPT_* (0: defaults)                                      */
 } gck_opts;
+
+/* gck_opts.flags: run every phase over all files with one host round trip
+ * (no file-group pipeline).  Results are identical either way. */
+#define GCK_OPT_SYNC 1u
 
 typedef struct gck_result {
     gck_rec *recs;              /* library-owned host array; free with gck_result_free  */
@@ -110,6 +114,8 @@ typedef struct gck_stats {
     uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
     double ms_total;        /* last gck_ctx_run wall time (host clock)                */
     double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
+    uint32_t pipelined;     /* 1: the last run was the file-group pipeline            */
+    uint32_t n_sync_reruns; /* pipelined runs that fell back to the synchronous path  */
 } gck_stats;
 
 int gck_ctx_create(const gck_opts *opts, gck_ctx **out);
