@@ -39,6 +39,8 @@ constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 #define GCK_DEPTH 2
 #endif
 constexpr int kDepth = GCK_DEPTH;  // rows in flight per k_crc_rows wavefront
+constexpr uint32_t kBatch = 6;     // rows per k_crc_rows work grab (multiple of kDepth + 1)
+constexpr uint32_t kCtrs = 8;      // k_crc_rows work counters (128 B apart)
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -466,10 +468,14 @@ __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uin
 // row_first[row] = first record whose value ends after the row's first byte,
 // for the rows [r0, ...) of the group; rows past the group's last record end
 // keep k_row_fill's value rng[1].  Grid-stride over the device range.
+// k_row_fill writes rows (r0, r1]: row r1 (the next group's first row) gets
+// rng[1] = the next group's first record, its final value, before the next
+// group starts, so the row entries a group reads never change under it.  Row 0
+// is 0 from the start of the run.
 __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64_t r1,
                            const uint64_t *__restrict__ rng) {
     const uint32_t v = (uint32_t)rng[1];
-    for (uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
+    for (uint64_t row = r0 + 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
          row += (uint64_t)gridDim.x * blockDim.x)
         row_first[row] = v;
 }
@@ -809,17 +815,40 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib,
                                                    uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
-                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch) {
+                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch,
+                                                   uint32_t *__restrict__ row_ctr) {
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
-    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
 
-    uint64_t row = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    if (row >= n_rows) return;
+    // Rows are handed out in batches of kBatch by kCtrs counters (batch b from
+    // counter b % kCtrs; a wave whose counter runs dry moves on to the next):
+    // a wavefront that starts late, e.g. behind the boundary kernels of the
+    // next file group on its CU, simply takes fewer batches.  Each grab is
+    // issued a batch before its result is needed.
+    const uint64_t n_batches = (n_rows + kBatch - 1) / kBatch;
+    uint32_t ck = (blockIdx.x * kWaves + (threadIdx.x >> 6)) % kCtrs, tried = 0;
+    auto grab_issue = [&]() -> uint32_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(row_ctr + ck * 32, 1u);
+        return v;
+    };
+    auto grab_resolve = [&](uint32_t v) -> uint64_t {  // first row of the batch, kNone when done
+        uint64_t b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v) * kCtrs + ck;
+        while (b >= n_batches && tried + 1 < kCtrs) {
+            ck = (ck + 1) % kCtrs;
+            ++tried;
+            b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)grab_issue()) * kCtrs + ck;
+        }
+        return b < n_batches ? b * kBatch : kNone;
+    };
+    uint64_t cur = grab_resolve(grab_issue());
+    if (cur == kNone) return;
+    uint64_t nxt = grab_resolve(grab_issue());
+    uint32_t pend = grab_issue();
     struct RowBuf {
         u32x4 x[4];
         uint32_t pv;
@@ -838,6 +867,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         b.pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
     };
     auto process = [&](uint64_t row, const RowBuf &b) {
+        const bool dead = row >= n_rows;  // past the end inside the last batch: scratch stores only
         const uint64_t rs = row * kRow;
         // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
         const uint64_t H = __ballot(b.pv & 0x80u);
@@ -864,18 +894,19 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const RowOut1 o = crc_row1<MODE>(lds, lane, lb0, lb1, nbase, rs, words, cc, ra + idx, t);
         // every lane stores: the cut lanes to their record's slot, the rest to
         // the scratch slot n_total (no branch around a store)
-        const uint64_t slot = (cc != 0 && !slow) ? (uint64_t)ra + idx : n_total;
+        const uint64_t slot = (cc != 0 && !slow && !dead) ? (uint64_t)ra + idx : n_total;
         out_e[slot] = o.e;
         out_pre[slot] = o.pre;
-        *(slow ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+        *(slow || dead ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
     };
-    // DEPTH rows in flight while one is processed; the loop is unrolled over
-    // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
-    // force a wait on loads still in flight).
+    // DEPTH rows in flight while one is processed; the batch loop is unrolled
+    // over the DEPTH+1 buffers (kBatch is a multiple of DEPTH+1) so each has
+    // fixed registers (a rotating copy would force a wait on loads in flight).
+    static_assert(kBatch % (DEPTH + 1) == 0 && kBatch > DEPTH, "batch vs depth");
     RowBuf buf[DEPTH + 1] = {};
 #pragma unroll
     for (int i = 0; i < DEPTH; ++i) {
-        issue(row + i * stride, buf[i]);
+        issue(cur + i, buf[i]);
         // the 3 stores of a processed row, to the scratch slots: the loop is
         // entered with the same vector-memory queue shape as its back edge, so
         // the compiler's waits at the loop head are as late as in the body
@@ -885,12 +916,16 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     }
     for (;;) {
 #pragma unroll
-        for (int i = 0; i <= DEPTH; ++i) {
-            issue(row + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
-            process(row, buf[i]);
-            row += stride;
-            if (row >= n_rows) return;
+        for (int i = 0; i < (int)kBatch; ++i) {
+            const int pf = i + DEPTH;
+            const uint64_t pf_row = pf < (int)kBatch ? cur + pf : (nxt != kNone ? nxt + (pf - kBatch) : n_rows - 1);
+            issue(pf_row, buf[pf % (DEPTH + 1)]);
+            process(cur + i, buf[i % (DEPTH + 1)]);
         }
+        cur = nxt;
+        if (cur == kNone) return;
+        nxt = grab_resolve(pend);
+        pend = grab_issue();
     }
 }
 
@@ -1109,7 +1144,8 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
-        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)))
+        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)) ||
+        (rc = c->d_rowctr.ensure((size_t)(kMaxGroups + 1) * kCtrs * 128)))
         return rc;
     GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
@@ -1128,7 +1164,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_rowctr};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1298,7 +1334,7 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
 // CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
 // k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
 static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
-                       const uint32_t *big_count) {
+                       const uint32_t *big_count, uint32_t *row_ctr) {
     if (r1 <= r0) return;
     const uint64_t nr = r1 - r0, want = (nr + kWaves - 1) / kWaves;
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
@@ -1306,7 +1342,8 @@ static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const ui
                                                 c->d_plan.as<uint8_t>() + r0 * kPlanBytes, cap,
                                                 c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
                                                 c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
-                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
+                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows,
+                                                row_ctr);
     k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0, big_count,
                                               c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
                                               c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
@@ -1394,6 +1431,8 @@ static int ctx_run_sync(Ctx *c) {
     uint64_t *gbase = c->d_gbase.as<uint64_t>();
     GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
     GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
+    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
+    GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, kCtrs * 128, s));
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
     launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
@@ -1448,7 +1487,7 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
     launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
+    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG, c->d_rowctr.as<uint32_t>());
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1507,6 +1546,8 @@ static int ctx_run_pipe(Ctx *c) {
     GCK_HIP(hipMemsetAsync(gbase, 0, (G + 1) * 8, s));
     GCK_HIP(hipMemsetAsync(gcarry, 0, (G + 1) * 4, s));
     GCK_HIP(hipMemsetAsync(gcnt, 0, G * 32, s));
+    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
+    GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, (size_t)G * kCtrs * 128, s));
     GCK_HIP(hipEventRecord(c->ev_start, s));
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t f0 = c->g_file[g], f1 = c->g_file[g + 1];
@@ -1521,7 +1562,8 @@ static int ctx_run_pipe(Ctx *c) {
         GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
         GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
         GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
-        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
+        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG,
+                   c->d_rowctr.as<uint32_t>() + (size_t)g * kCtrs * 32);
         GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
         GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
         GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
@@ -1750,12 +1792,14 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     GCK_HIP(hipEventCreate(&b));
     GCK_HIP(hipEventRecord(a, c->stream));
     for (int i = 0; i < iters; ++i) {
+        GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, kCtrs * 128, c->stream));
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
         k_crc_rows<M, kDepth><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
                                                     c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
-                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows);    \
+                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows,     \
+                                                    c->d_rowctr.as<uint32_t>());                                        \
         break;
         switch (mode) {
             GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6) GCK_VARIANT(7) GCK_VARIANT(8)

@@ -52,7 +52,8 @@ def main():
     stats = {}
     for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
         stats[short(r["Name"])] = float(r["AverageNs"])
-    crc = summary.get("k_crc_rows<0>", {})
+    crc_key = next((k for k in summary if k.startswith("k_crc_rows<")), None)
+    crc = summary.get(crc_key, {})
     sr = summary.get("k_stream_read", {})
     out = {
         "config": cfg,
@@ -61,8 +62,9 @@ def main():
         "crc_rows_hbm_bytes_per_launch": crc.get("FETCH_SIZE", 0) * 2048 or None,
         "crc_rows_write_bytes_per_launch": crc.get("WRITE_SIZE", 0) * 1024 or None,
         "stream_read_hbm_bytes_per_launch": sr.get("FETCH_SIZE", 0) * 2048 or None,
-        "crc_rows_avg_ns_rocprof": stats.get("k_crc_rows<0>"),
-        "algorithmic_bytes_per_launch": bench["config"]["bytes_per_gpu"] if bench else None,
+        "crc_rows_avg_ns_rocprof": next((v for k, v in stats.items() if k.startswith("k_crc_rows<")), None),
+        "algorithmic_bytes_per_launch": (bench["config"]["bytes_per_gpu"] / bench["roofline"].get("launches_per_step", 1))
+        if bench else None,
     }
     json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
