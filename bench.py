@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--chunk-kib", type=int, default=0)
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--sync", action="store_true", help="no file-group pipeline (diagnostic)")
+    ap.add_argument("--pipeline", action="store_true", help="file-group pipeline (GCK_OPT_PIPELINE)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -117,7 +117,7 @@ def main():
 
     cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10, sync=args.sync)
+    ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10, pipeline=args.pipeline)
     info = ctx.encode(**cfg)
     setup_s = time.perf_counter() - t_setup
 

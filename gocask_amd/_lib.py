@@ -25,7 +25,7 @@ GCK_ECRC_FAILED = 7
 GCK_EINVALID_KEY = 8
 GCK_ENOT_DIR = 9
 
-GCK_OPT_SYNC = 1  # gck_opts.flags: no file-group pipeline
+GCK_OPT_PIPELINE = 2  # gck_opts.flags: file-group pipeline
 
 F_TOMBSTONE = 1
 F_CRC_OK = 2

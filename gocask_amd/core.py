@@ -79,13 +79,13 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = _lib.GCK_OPT_SYNC if sync else 0
+    o.flags = _lib.GCK_OPT_PIPELINE if pipeline else 0
     return o
 
 
@@ -223,14 +223,14 @@ def _result(res: GckResult):
                       files_walked=res.files_walked)
 
 
-def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, sync)),
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, pipeline)),
                       ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
@@ -256,10 +256,10 @@ def keydir(files, recs):
 class ReplayContext:
     """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
 
-    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, sync=False):
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
-        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, sync)),
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, pipeline)),
                                      ctypes.byref(self._h)))
 
     def load(self, files, reset_after=None):

@@ -81,7 +81,6 @@ struct Ctx {
     DBuf d_rec_base, d_bsum, d_scratch_off, d_scratch_hdr, d_counters;
     DBuf d_freset;                   // per file: 1 = lastOffset resets after it
     DBuf d_gbase, d_gcarry, d_gcnt;  // per file group: record base, lastOffset in, counters
-    DBuf d_rowctr;                   // per file group: k_crc_rows work counters
 
     // records
     uint64_t n_recs = 0;

@@ -39,8 +39,6 @@ constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 #define GCK_DEPTH 2
 #endif
 constexpr int kDepth = GCK_DEPTH;  // rows in flight per k_crc_rows wavefront
-constexpr uint32_t kBatch = 6;     // rows per k_crc_rows work grab (multiple of kDepth + 1)
-constexpr uint32_t kCtrs = 8;      // k_crc_rows work counters (128 B apart)
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -528,37 +526,44 @@ __device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ 
 //              H[45] = slow: some slab holds 2+ record ends (records < 64 B);
 //                      such rows are listed for k_crc_rows_big
 // Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
-// plan carries no ids or counts.
-__global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                           const uint64_t *__restrict__ rng, uint64_t r0, uint64_t nr,
-                           const uint32_t *__restrict__ row_first, uint4 *__restrict__ plan,
-                           uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+// plan carries no ids or counts.  Built in two passes: k_row_plan writes each
+// row's header bits (row-parallel), k_row_cuts ORs in the cut of every record
+// (record-parallel) and flags slow rows.
+__global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint64_t *__restrict__ rng, uint64_t r0,
+                           uint64_t nr, const uint32_t *__restrict__ row_first, uint4 *__restrict__ plan) {
     const uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (row >= r0 + nr) return;
     const uint32_t ra = row_first[row], rb = row_first[row + 1];
-    const uint64_t rs = row * kRow;
+    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, row * kRow) << 32);
     uint32_t w[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = 0;
-    bool slow = false;
-    int32_t prev = -1;
-    for (uint32_t r = ra; r < rb; ++r) {
-        const uint32_t end = (uint32_t)(value_end(rec_off, rec_hdr, r) - rs);  // 1..kRow
-        const int32_t slab = (int32_t)((end - 1) >> 6);
-        slow |= slab == prev;
-        prev = slab;
-        const uint32_t cc = end - (uint32_t)slab * kSlab;
-        // w[] is indexed by a loop-variant value: keep it in registers by selects
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] |= (slab >> 2) == i ? cc << (8 * (slab & 3)) : 0u;
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t nib = (uint32_t)(H >> (4 * i)) & 15u;  // header bits of bytes 4i .. 4i+3
+        w[i] = ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
     }
-    if (slow) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
-    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, rs) << 32) |
-                       ((uint64_t)slow << 45);
-#pragma unroll
-    for (int k = 0; k < 64; ++k) w[k >> 2] |= (uint32_t)((H >> k) & 1u) << (8 * (k & 3) + 7);
 #pragma unroll
     for (int i = 0; i < 4; ++i) plan[row * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+}
+
+constexpr uint32_t kSlowWord = 45 / 4, kSlowBit = 1u << (8 * (45 % 4) + 7);  // header bit 45
+
+__global__ void k_row_cuts(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
+                           const uint64_t *__restrict__ rng, uint32_t *__restrict__ plan32,
+                           uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+    const uint64_t rb = rng[0], re = rng[1];
+    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t ve = value_end(rec_off, rec_hdr, r);
+        const uint64_t row = (ve - 1) / kRow;
+        const uint32_t end = (uint32_t)(ve - row * kRow);  // 1..kRow
+        const uint32_t slab = (end - 1) >> 6, cc = end - slab * kSlab;
+        atomicOr(plan32 + row * 16 + (slab >> 2), cc << (8 * (slab & 3)));
+        // the previous record (same file group) ends in the same slab: slow row
+        if (r > rb && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6) {
+            const uint32_t old = atomicOr(plan32 + row * 16 + kSlowWord, kSlowBit);
+            if (!(old & kSlowBit)) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
+        }
+    }
 }
 
 // LDS image of the slicing-by-4 tables: two 64 KiB regions; in region r,
@@ -815,40 +820,17 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib,
                                                    uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
-                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch,
-                                                   uint32_t *__restrict__ row_ctr) {
+                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch) {
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
+    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
 
-    // Rows are handed out in batches of kBatch by kCtrs counters (batch b from
-    // counter b % kCtrs; a wave whose counter runs dry moves on to the next):
-    // a wavefront that starts late, e.g. behind the boundary kernels of the
-    // next file group on its CU, simply takes fewer batches.  Each grab is
-    // issued a batch before its result is needed.
-    const uint64_t n_batches = (n_rows + kBatch - 1) / kBatch;
-    uint32_t ck = (blockIdx.x * kWaves + (threadIdx.x >> 6)) % kCtrs, tried = 0;
-    auto grab_issue = [&]() -> uint32_t {
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(row_ctr + ck * 32, 1u);
-        return v;
-    };
-    auto grab_resolve = [&](uint32_t v) -> uint64_t {  // first row of the batch, kNone when done
-        uint64_t b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v) * kCtrs + ck;
-        while (b >= n_batches && tried + 1 < kCtrs) {
-            ck = (ck + 1) % kCtrs;
-            ++tried;
-            b = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)grab_issue()) * kCtrs + ck;
-        }
-        return b < n_batches ? b * kBatch : kNone;
-    };
-    uint64_t cur = grab_resolve(grab_issue());
-    if (cur == kNone) return;
-    uint64_t nxt = grab_resolve(grab_issue());
-    uint32_t pend = grab_issue();
+    uint64_t row = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    if (row >= n_rows) return;
     struct RowBuf {
         u32x4 x[4];
         uint32_t pv;
@@ -867,7 +849,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         b.pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
     };
     auto process = [&](uint64_t row, const RowBuf &b) {
-        const bool dead = row >= n_rows;  // past the end inside the last batch: scratch stores only
         const uint64_t rs = row * kRow;
         // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
         const uint64_t H = __ballot(b.pv & 0x80u);
@@ -894,19 +875,18 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const RowOut1 o = crc_row1<MODE>(lds, lane, lb0, lb1, nbase, rs, words, cc, ra + idx, t);
         // every lane stores: the cut lanes to their record's slot, the rest to
         // the scratch slot n_total (no branch around a store)
-        const uint64_t slot = (cc != 0 && !slow && !dead) ? (uint64_t)ra + idx : n_total;
+        const uint64_t slot = (cc != 0 && !slow) ? (uint64_t)ra + idx : n_total;
         out_e[slot] = o.e;
         out_pre[slot] = o.pre;
-        *(slow || dead ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+        *(slow ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
     };
-    // DEPTH rows in flight while one is processed; the batch loop is unrolled
-    // over the DEPTH+1 buffers (kBatch is a multiple of DEPTH+1) so each has
-    // fixed registers (a rotating copy would force a wait on loads in flight).
-    static_assert(kBatch % (DEPTH + 1) == 0 && kBatch > DEPTH, "batch vs depth");
+    // DEPTH rows in flight while one is processed; the loop is unrolled over
+    // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
+    // force a wait on loads still in flight).
     RowBuf buf[DEPTH + 1] = {};
 #pragma unroll
     for (int i = 0; i < DEPTH; ++i) {
-        issue(cur + i, buf[i]);
+        issue(row + i * stride, buf[i]);
         // the 3 stores of a processed row, to the scratch slots: the loop is
         // entered with the same vector-memory queue shape as its back edge, so
         // the compiler's waits at the loop head are as late as in the body
@@ -916,16 +896,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     }
     for (;;) {
 #pragma unroll
-        for (int i = 0; i < (int)kBatch; ++i) {
-            const int pf = i + DEPTH;
-            const uint64_t pf_row = pf < (int)kBatch ? cur + pf : (nxt != kNone ? nxt + (pf - kBatch) : n_rows - 1);
-            issue(pf_row, buf[pf % (DEPTH + 1)]);
-            process(cur + i, buf[i % (DEPTH + 1)]);
+        for (int i = 0; i <= DEPTH; ++i) {
+            issue(row + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
+            process(row, buf[i]);
+            row += stride;
+            if (row >= n_rows) return;
         }
-        cur = nxt;
-        if (cur == kNone) return;
-        nxt = grab_resolve(pend);
-        pend = grab_issue();
     }
 }
 
@@ -992,6 +968,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
 //   crc = F(0, value) ^ crc32(0^V)  (table for V < 2^17).
 // ValuePos = lastOffset + 16 + KeySize mod 2^32 (core/keydir.go:25), with
 // lastOffset = carry + offset within the file.
+__device__ __forceinline__ uint32_t z4096(const uint32_t *Tz, uint32_t a) {
+    return Tz[a & 0xFF] ^ Tz[256 + ((a >> 8) & 0xFF)] ^ Tz[512 + ((a >> 16) & 0xFF)] ^ Tz[768 + (a >> 24)];
+}
+
 __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint4 *__restrict__ rec_hdr,
@@ -1005,9 +985,13 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
                                                   const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
-    // no LDS: the 5 KiB of tables stay in L1/L2, and the kernel can share CUs
-    // with k_crc_rows (which holds all of the LDS) in the pipelined run
-    const uint32_t *Tz = zrow, *T0 = g_slice;
+    __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
+    __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
+        Tz[i] = zrow[i];
+        T[i] = g_slice[i];
+    }
+    __syncthreads();
     const uint64_t rb = rng[0], re = rng[1];
     for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
          r += (uint64_t)gridDim.x * blockDim.x) {
@@ -1018,20 +1002,33 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         const uint64_t vs = start + 16 + h.z, ve = vs + V;
         const uint64_t w0 = (start + 3) & ~3ull;
         const uint64_t fr = w0 / kRow, lr = (ve - 1) / kRow;
+        // Horner over the rows the chain crosses; the row values are loaded 8
+        // at a time so their latency overlaps
         uint32_t acc = 0;
-        for (uint64_t row = fr; row <= lr; ++row) {
-            acc = Tz[acc & 0xFF] ^ Tz[256 + ((acc >> 8) & 0xFF)] ^ Tz[512 + ((acc >> 16) & 0xFF)] ^ Tz[768 + (acc >> 24)];
-            acc ^= row < lr ? rend[row] : pre[r];
+        for (uint64_t row = fr; row < lr; row += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = row + j < lr ? rend[row + j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (row + j < lr) acc = z4096(Tz, acc) ^ v[j];
         }
+        acc = z4096(Tz, acc) ^ pre[r];
         const uint64_t row_end = (lr + 1) * kRow;
         const uint32_t chain = e[r] ^ (acc ? multmodp(xinv[row_end - ve], acc) : 0u);
-        // F(0, prefix): header bytes [w0 - start, 16) then the key
+        // F(0, prefix): the bytes [w0, vs) = header tail + key, read as aligned
+        // words from the arena (slicing-by-4), the last partial word bytewise
+        const uint32_t L = (uint32_t)(vs - w0);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
         uint32_t p = 0;
-        const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
-        for (uint32_t i = (uint32_t)(w0 - start); i < 16; ++i)
-            p = T0[(p ^ (hw[i >> 2] >> (8 * (i & 3)))) & 0xFF] ^ (p >> 8);
-        const uint8_t *key = arena + start + 16;
-        for (uint32_t i = 0; i < h.z; ++i) p = T0[(p ^ key[i]) & 0xFF] ^ (p >> 8);
+        for (uint32_t i = 0; i < L / 4; ++i) {
+            const uint32_t x = p ^ wp[i];
+            p = T[768 + (x & 0xFF)] ^ T[512 + ((x >> 8) & 0xFF)] ^ T[256 + ((x >> 16) & 0xFF)] ^ T[x >> 24];
+        }
+        if (L & 3) {
+            uint32_t y = wp[L / 4];
+            for (uint32_t i = 0; i < (L & 3); ++i, y >>= 8) p = T[(p ^ y) & 0xFF] ^ (p >> 8);
+        }
         const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
         const uint32_t raw0 = chain ^ (p ? multmodp(xv, p) : 0u);
         const uint32_t z = V < (1u << 17) ? zl[V] : multmodp(multmodp(xa[V >> 16], xb[V & 0xFFFF]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
@@ -1144,8 +1141,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
-        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)) ||
-        (rc = c->d_rowctr.ensure((size_t)(kMaxGroups + 1) * kCtrs * 128)))
+        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)))
         return rc;
     GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
@@ -1164,7 +1160,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_rowctr};
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1326,15 +1322,16 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
                                      c->d_row_first.as<uint32_t>());
     if (r1 > r0)
-        k_row_plan<<<nblk(r1 - r0, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
-                                                      r1 - r0, c->d_row_first.as<uint32_t>(), c->d_plan.as<uint4>(),
-                                                      c->d_big.as<uint32_t>() + r0, big_count);
+        k_row_plan<<<nblk(r1 - r0, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), rng, r0, r1 - r0,
+                                                      c->d_row_first.as<uint32_t>(), c->d_plan.as<uint4>());
+    k_row_cuts<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng,
+                                    c->d_plan.as<uint32_t>(), c->d_big.as<uint32_t>() + r0, big_count);
 }
 
 // CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
 // k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
 static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
-                       const uint32_t *big_count, uint32_t *row_ctr) {
+                       const uint32_t *big_count) {
     if (r1 <= r0) return;
     const uint64_t nr = r1 - r0, want = (nr + kWaves - 1) / kWaves;
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
@@ -1342,8 +1339,7 @@ static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const ui
                                                 c->d_plan.as<uint8_t>() + r0 * kPlanBytes, cap,
                                                 c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
                                                 c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
-                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows,
-                                                row_ctr);
+                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
     k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0, big_count,
                                               c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
                                               c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
@@ -1432,7 +1428,6 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
     GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
     GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
-    GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, kCtrs * 128, s));
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
     launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
@@ -1487,7 +1482,7 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
     launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG, c->d_rowctr.as<uint32_t>());
+    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1547,7 +1542,6 @@ static int ctx_run_pipe(Ctx *c) {
     GCK_HIP(hipMemsetAsync(gcarry, 0, (G + 1) * 4, s));
     GCK_HIP(hipMemsetAsync(gcnt, 0, G * 32, s));
     GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
-    GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, (size_t)G * kCtrs * 128, s));
     GCK_HIP(hipEventRecord(c->ev_start, s));
     for (uint32_t g = 0; g < G; ++g) {
         const uint32_t f0 = c->g_file[g], f1 = c->g_file[g + 1];
@@ -1562,8 +1556,7 @@ static int ctx_run_pipe(Ctx *c) {
         GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
         GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
         GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
-        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG,
-                   c->d_rowctr.as<uint32_t>() + (size_t)g * kCtrs * 32);
+        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
         GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
         GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
         GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
@@ -1607,7 +1600,7 @@ static int ctx_run_pipe(Ctx *c) {
 }
 
 static int ctx_run(Ctx *c) {
-    const bool pipe = c->nfiles >= 2 && !(c->opts.flags & GCK_OPT_SYNC);
+    const bool pipe = c->nfiles >= 2 && (c->opts.flags & GCK_OPT_PIPELINE);
     if (!pipe) return ctx_run_sync(c);
     GCK_HIP(hipSetDevice(c->device));
     make_groups(c);
@@ -1792,14 +1785,12 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     GCK_HIP(hipEventCreate(&b));
     GCK_HIP(hipEventRecord(a, c->stream));
     for (int i = 0; i < iters; ++i) {
-        GCK_HIP(hipMemsetAsync(c->d_rowctr.p, 0, kCtrs * 128, c->stream));
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
         k_crc_rows<M, kDepth><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
                                                     c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
-                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows,     \
-                                                    c->d_rowctr.as<uint32_t>());                                        \
+                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows);    \
         break;
         switch (mode) {
             GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6) GCK_VARIANT(7) GCK_VARIANT(8)

@@ -83,9 +83,11 @@ typedef struct gck_opts {
     uint32_t flags;        /* GCK_OPT_* (0: defaults)                                      */
 } gck_opts;
 
-/* gck_opts.flags: run every phase over all files with one host round trip
- * (no file-group pipeline).  Results are identical either way. */
-#define GCK_OPT_SYNC 1u
+/* gck_opts.flags: GCK_OPT_PIPELINE runs file groups as a pipeline (boundary
+ * discovery of group g+1 beside the CRC of group g, no host round trip until
+ * the end); the default runs every phase over all files with one host round
+ * trip.  Results are identical either way. */
+#define GCK_OPT_PIPELINE 2u
 
 typedef struct gck_result {
     gck_rec *recs;              /* library-owned host array; free with gck_result_free  */

@@ -167,14 +167,14 @@ CORPORA = [
 ]
 
 
-@pytest.mark.parametrize("sync", [False, True])
+@pytest.mark.parametrize("pipeline", [False, True])
 @pytest.mark.parametrize("chunk,cap", [(4096, 2), (1 << 15, 256), (1 << 18, 256)])
 @pytest.mark.parametrize("ci", range(len(CORPORA)))
-def test_random_corpora(g, orc, ci, chunk, cap, sync):
+def test_random_corpora(g, orc, ci, chunk, cap, pipeline):
     files, names = orc.gen_corpus(**CORPORA[ci])
     wf, reset = walk_sorted(files, names)
     want, wst = orc.replay(wf, reset)
-    got, gst = g.replay(wf, reset, chunk_bytes=chunk, chunk_cap=cap, sync=sync)
+    got, gst = g.replay(wf, reset, chunk_bytes=chunk, chunk_cap=cap, pipeline=pipeline)
     assert_same(got, gst, want, wst)
     assert np.array_equal(got["flags"] & 2 == 0, want["crc_calc"] != want["crc"])
 
@@ -188,7 +188,7 @@ def test_pipeline_vs_oracle_multi_file(g, orc):
     files, names = orc.gen_corpus(**kw)
     wf, reset = walk_sorted(files, names)
     want, wst = orc.replay(wf, reset)
-    with g.ReplayContext() as ctx:
+    with g.ReplayContext(pipeline=True) as ctx:
         ctx.load(wf, reset)
         ctx.run()
         got, gst = ctx.fetch()
@@ -202,15 +202,15 @@ def test_pipeline_equals_sync_c3_shape(g):
     kw = dict(seed=3, val_fixed=0, key_min=8, key_max=24, key_universe=600000, tomb_permille=10,
               flip_permille=10, max_file_size=256 << 20, n_files=16)
     out = {}
-    for sync in (False, True):
-        with g.ReplayContext(sync=sync) as ctx:
+    for pipe in (False, True):
+        with g.ReplayContext(pipeline=pipe) as ctx:
             ctx.encode(**kw)
             ctx.run()
             ctx.run()  # second run: capacity from the first
-            out[sync] = ctx.fetch()
+            out[pipe] = ctx.fetch()
             st = ctx.stats()
-            assert st["pipelined"] == (not sync) and st["n_sync_reruns"] == 0
-    (a, ast), (b, bst) = out[False], out[True]
+            assert st["pipelined"] == pipe and st["n_sync_reruns"] == 0
+    (a, ast), (b, bst) = out[True], out[False]
     assert_same(a, ast, b, bst)
 
 
@@ -221,7 +221,7 @@ def test_pipeline_falls_back_when_capacity_exceeded(g, orc):
     files = [b"".join(recs[:2000]), b"".join(recs[2000:])]
     reset = [True, False]
     want, wst = orc.replay(files, reset)
-    with g.ReplayContext(chunk_bytes=4096, chunk_cap=16) as ctx:
+    with g.ReplayContext(chunk_bytes=4096, chunk_cap=16, pipeline=True) as ctx:
         ctx.load(files, reset)
         ctx.run()
         got, gst = ctx.fetch()
