@@ -49,7 +49,7 @@ assert REC_DTYPE.itemsize == 40
 EXPORTED = [
     "gck_replay", "gck_result_free", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
     "gck_ctx_fetch", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
-    "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_crc_variant", "gck_encode_corpus", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_db_open",
+    "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_stream_pattern", "gck_diag_crc_variant", "gck_encode_corpus", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
     "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count",
     "gck_version", "gck_last_error",
@@ -145,6 +145,8 @@ def load():
         "gck_ctx_stream": (vp, [vp]),
         "gck_ctx_read_file": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint64, vp, ctypes.c_uint64]),
         "gck_diag_stream_read": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]),
+        "gck_diag_stream_pattern": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double),
+                                                   P(ctypes.c_double)]),
         "gck_diag_crc_variant": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double)]),
         "gck_encode_corpus": (ctypes.c_int, [vp, P(GckCorpusCfg), P(ctypes.c_uint32), P(ctypes.c_uint64), vp,
                                              ctypes.c_uint32]),

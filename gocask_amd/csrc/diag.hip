@@ -22,9 +22,68 @@ __global__ __launch_bounds__(256) void k_stream_read(const uint4 *__restrict__ p
     if (acc == 0x9E3779B9u) sink[0] = acc;  // practically never: keeps the loads live
 }
 
+// Row-streaming probes with k_crc_rows' geometry (1024-thread workgroups, one
+// per CU, a wavefront per 4 KiB row, two rows in flight): SLAB = lane l reads
+// its 64 contiguous bytes as 4 x 16 B (lane stride 64 B, the k_crc_rows
+// layout); otherwise lane l reads 16 B at 16 l + 1024 j (each instruction
+// reads 1 KiB contiguous).
+template <bool SLAB>
+__global__ __launch_bounds__(1024) void k_stream_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
+                                                      uint32_t *sink) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * 16;
+    uint32_t acc = 0;
+    for (uint64_t row = blockIdx.x * 16 + (threadIdx.x >> 6); row < n_rows; row += 2 * stride) {
+        const uint64_t row2 = min(row + stride, n_rows - 1);
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t off = SLAB ? lane * 64 + 16 * j : lane * 16 + 1024 * j;
+            v[j] = *reinterpret_cast<const uint4 *>(arena + row * 4096 + off);
+            v[4 + j] = *reinterpret_cast<const uint4 *>(arena + row2 * 4096 + off);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 }  // namespace gck
 
 using namespace gck;
+
+// pattern 0: k_stream_read; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>.
+extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs) {
+    if (!ctx || iters <= 0 || pattern < 0 || pattern > 2) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    if (!c->n_rows) return GCK_EINVAL;
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    auto launch = [&]() {
+        if (pattern == 0)
+            k_stream_read<<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
+        else if (pattern == 1)
+            k_stream_rows<true><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
+        else
+            k_stream_rows<false><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
+    };
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    launch();  // warm-up
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) launch();
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    const double per = ms / iters;
+    if (ms_per_iter) *ms_per_iter = per;
+    if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
+    return GCK_OK;
+}
 
 extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs) {
     if (!ctx || iters <= 0) return GCK_EINVAL;

@@ -150,19 +150,23 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     if (cs == 0) {
         found = 0;
     } else {
-        for (uint64_t b0 = cs; b0 < ce && found == kNone; b0 += 4096) {
-            const uint64_t p0 = b0 + 64ull * lane;
-            // bytes [p0, p0+80): the 64 positions plus their header bytes (arena
-            // is 16 B aligned here and padded past every file)
-            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + p0);
+        // windows are double-buffered (A/B, unrolled so neither is copied):
+        // the next window's loads are in flight while this one is checked
+        auto load = [&](uint64_t b0, uint4 (&v)[5]) {
+            // bytes [p0, p0+80): the 64 positions plus their header bytes (the
+            // arena is 16 B aligned here and padded 4 windows past every file)
+            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + b0 + 64ull * lane);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) v[k] = src[k];
+        };
+        auto scan = [&](uint64_t b0, const uint4 (&v)[5]) {
             uint32_t w[20];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
-                const uint4 v = src[k];
-                w[4 * k] = v.x;
-                w[4 * k + 1] = v.y;
-                w[4 * k + 2] = v.z;
-                w[4 * k + 3] = v.w;
+                w[4 * k] = v[k].x;
+                w[4 * k + 1] = v[k].y;
+                w[4 * k + 2] = v[k].z;
+                w[4 * k + 3] = v[k].w;
             }
             uint32_t zf[20];
 #pragma unroll
@@ -191,6 +195,16 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 }
                 lanes &= lanes - 1;
             }
+        };
+        uint4 A[5], B[5];
+        load(cs, A);
+        for (uint64_t b0 = cs;; b0 += 8192) {
+            load(b0 + 4096, B);
+            scan(b0, A);
+            if (found != kNone || b0 + 4096 >= ce) break;
+            load(b0 + 8192, A);
+            scan(b0 + 4096, B);
+            if (found != kNone || b0 + 8192 >= ce) break;
         }
         if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, mk)) found += 1;
     }
@@ -1209,8 +1223,10 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     const uint64_t nc = c->n_chunks, nf = nfiles ? nfiles : 1;
     const uint64_t cap = c->opts.chunk_cap;
     int rc;
-    const bool fresh = c->arena.cap < pos + 2 * kRow;
-    if ((rc = c->arena.ensure(pos + 2 * kRow))) return rc;
+    // slack past the last file: k_spec_entry reads up to two 4 KiB windows
+    // (+80 B) beyond a chunk end
+    const bool fresh = c->arena.cap < pos + 4 * kRow;
+    if ((rc = c->arena.ensure(pos + 4 * kRow))) return rc;
     if (fresh) GCK_HIP(hipMemset(c->arena.p, 0, c->arena.cap));
     if ((rc = c->d_fbase.ensure(nf * 8)) || (rc = c->d_flen.ensure(nf * 8)) || (rc = c->d_ffirst.ensure(nf * 4)) ||
         (rc = c->d_fnch.ensure(nf * 4)) || (rc = c->d_fbad.ensure(nf * 4)) || (rc = c->d_fterm.ensure(nf * 4)) ||

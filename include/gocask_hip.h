@@ -137,6 +137,9 @@ void *gck_ctx_stream(gck_ctx *ctx);
 /* Measurement helper (not on the replay path): time a plain streaming read of
  * the resident arena, the practical HBM read ceiling k_crc_rows is compared to. */
 int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs);
+/* Diagnostic read probes over the arena: 0 = gck_diag_stream_read's kernel,
+ * 1 = k_crc_rows' slab layout (lane stride 64 B), 2 = same geometry coalesced. */
+int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs);
 /* Measurement helper: time ablated variants of the CRC kernel on the last run's
  * state (mode bits 1 = no record intervals, 2 = no LDS table chain, 4 = no
  * tail shift / segmented scan).  Clobbers the last run's outputs. */

@@ -15,4 +15,8 @@ for mode in [0, 2, 4, 5, 6, 7, 8]:
     g._lib.check(ctx._L.gck_diag_crc_variant(ctx._h, mode, 5, ctypes.byref(ms)))
     out[f"mode{mode}_ms"] = round(ms.value, 3)
     out[f"mode{mode}_gbs"] = round(st["bytes"] / ms.value / 1e6, 1)
+gbs = ctypes.c_double()
+for pat in range(3):
+    g._lib.check(ctx._L.gck_diag_stream_pattern(ctx._h, pat, 5, ctypes.byref(ms), ctypes.byref(gbs)))
+    out[f"stream_pattern{pat}_ms"] = round(ms.value, 3)
 print(json.dumps(out))
