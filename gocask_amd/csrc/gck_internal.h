@@ -89,6 +89,8 @@ struct Ctx {
     // rows
     uint64_t n_rows = 0;
     DBuf d_row_first, d_rend, d_plan, d_big;
+    DBuf d_slow;           // per row: generation of the run that listed it as slow
+    uint32_t run_gen = 0;  // gck_ctx_run counter
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;

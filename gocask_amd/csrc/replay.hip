@@ -537,12 +537,11 @@ __device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ 
 //   bit  7     bit k of the row header H, recovered with one ballot:
 //              H[0..31] = ra, the first record whose end lies past the row start
 //              H[32..44] = tail start (row_tail_start)
-//              H[45] = slow: some slab holds 2+ record ends (records < 64 B);
-//                      such rows are listed for k_crc_rows_big
 // Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
 // plan carries no ids or counts.  Built in two passes: k_row_plan writes each
 // row's header bits (row-parallel), k_row_cuts ORs in the cut of every record
-// (record-parallel) and flags slow rows.
+// (record-parallel) and lists the rows where a slab holds 2+ record ends
+// (records under 64 B) for k_crc_rows_big.
 __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint64_t *__restrict__ rng, uint64_t r0,
                            uint64_t nr, const uint32_t *__restrict__ row_first, uint4 *__restrict__ plan) {
     const uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -559,24 +558,27 @@ __global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint64_t 
     for (int i = 0; i < 4; ++i) plan[row * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
 }
 
-constexpr uint32_t kSlowWord = 45 / 4, kSlowBit = 1u << (8 * (45 % 4) + 7);  // header bit 45
-
+// Record-parallel: OR each record's cut into the byte of its end slab (a
+// plain read-modify-write: in rows where every slab holds at most one record
+// end, each byte has one writer).  A record ending in the same slab as the one
+// before makes its row slow: listed once per run (slow_gen[row] == gen) for
+// k_crc_rows_big, which recomputes everything k_crc_rows wrote for that row.
 __global__ void k_row_cuts(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                           const uint64_t *__restrict__ rng, uint32_t *__restrict__ plan32,
-                           uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+                           const uint64_t *__restrict__ rng, uint8_t *__restrict__ plan,
+                           uint32_t *__restrict__ slow_gen, uint32_t gen, uint32_t *__restrict__ big_rows,
+                           uint32_t *big_count) {
     const uint64_t rb = rng[0], re = rng[1];
     for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
          r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t ve = value_end(rec_off, rec_hdr, r);
         const uint64_t row = (ve - 1) / kRow;
         const uint32_t end = (uint32_t)(ve - row * kRow);  // 1..kRow
-        const uint32_t slab = (end - 1) >> 6, cc = end - slab * kSlab;
-        atomicOr(plan32 + row * 16 + (slab >> 2), cc << (8 * (slab & 3)));
-        // the previous record (same file group) ends in the same slab: slow row
-        if (r > rb && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6) {
-            const uint32_t old = atomicOr(plan32 + row * 16 + kSlowWord, kSlowBit);
-            if (!(old & kSlowBit)) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
-        }
+        const uint32_t slab = (end - 1) >> 6;
+        uint8_t *pb = plan + row * kPlanBytes + slab;
+        *pb = (uint8_t)(*pb | (end - slab * kSlab));
+        if (r > rb && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6 &&
+            atomicExch(slow_gen + row, gen) != gen)
+            big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
     }
 }
 
@@ -868,7 +870,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const uint64_t H = __ballot(b.pv & 0x80u);
         const uint32_t ra = (uint32_t)H, hh = (uint32_t)(H >> 32);
         const uint32_t tail_start = hh & 0x1FFFu;
-        const bool slow = (hh >> 13) & 1u;  // wave-uniform: k_crc_rows_big owns the row
         const int32_t cc = (MODE & 1) ? 0 : (int32_t)(b.pv & 0x7Fu);
         const uint64_t C = __ballot(cc != 0);
         const uint32_t n_ends = (uint32_t)__popcll(C);
@@ -889,10 +890,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const RowOut1 o = crc_row1<MODE>(lds, lane, lb0, lb1, nbase, rs, words, cc, ra + idx, t);
         // every lane stores: the cut lanes to their record's slot, the rest to
         // the scratch slot n_total (no branch around a store)
-        const uint64_t slot = (cc != 0 && !slow) ? (uint64_t)ra + idx : n_total;
+        // (a row where a slab holds 2+ record ends gets cuts OR'ed together
+        // here; k_crc_rows_big then rewrites all of this row's outputs)
+        const uint64_t slot = cc != 0 ? (uint64_t)ra + idx : n_total;
         out_e[slot] = o.e;
         out_pre[slot] = o.pre;
-        *(slow ? rend_scratch : out_rend + row) = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
+        out_rend[row] = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
     };
     // DEPTH rows in flight while one is processed; the loop is unrolled over
     // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
@@ -1174,7 +1177,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_slow};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1228,6 +1231,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     const bool fresh = c->arena.cap < pos + 4 * kRow;
     if ((rc = c->arena.ensure(pos + 4 * kRow))) return rc;
     if (fresh) GCK_HIP(hipMemset(c->arena.p, 0, c->arena.cap));
+    const bool slow_fresh = c->d_slow.cap < (c->n_rows + 1) * 4;
     if ((rc = c->d_fbase.ensure(nf * 8)) || (rc = c->d_flen.ensure(nf * 8)) || (rc = c->d_ffirst.ensure(nf * 4)) ||
         (rc = c->d_fnch.ensure(nf * 4)) || (rc = c->d_fbad.ensure(nf * 4)) || (rc = c->d_fterm.ensure(nf * 4)) ||
         (rc = c->d_ftpos.ensure(nf * 8)) || (rc = c->d_fnrec.ensure(nf * 8)) ||
@@ -1239,8 +1243,10 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)))
+        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_slow.ensure((c->n_rows + 1) * 4)))
         return rc;
+    if (slow_fresh) GCK_HIP(hipMemset(c->d_slow.p, 0, c->d_slow.cap));  // generation 0: never listed
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
         GCK_HIP(hipMemcpy(c->d_flen.p, c->f_len.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -1341,7 +1347,8 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
         k_row_plan<<<nblk(r1 - r0, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), rng, r0, r1 - r0,
                                                       c->d_row_first.as<uint32_t>(), c->d_plan.as<uint4>());
     k_row_cuts<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng,
-                                    c->d_plan.as<uint32_t>(), c->d_big.as<uint32_t>() + r0, big_count);
+                                    c->d_plan.as<uint8_t>(), c->d_slow.as<uint32_t>(), c->run_gen,
+                                    c->d_big.as<uint32_t>() + r0, big_count);
 }
 
 // CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
@@ -1373,6 +1380,15 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_zrow.as<uint32_t>(),
                                     c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
+}
+
+// A fresh generation for the slow-row list of each run attempt.
+static int next_gen(Ctx *c) {
+    if (++c->run_gen == 0) {  // wrapped: start over
+        GCK_HIP(hipMemset(c->d_slow.p, 0, c->d_slow.cap));
+        c->run_gen = 1;
+    }
+    return GCK_OK;
 }
 
 static int ensure_records(Ctx *c, uint64_t nr) {
@@ -1437,6 +1453,7 @@ static int read_file_summaries(Ctx *c, hipStream_t s, std::vector<uint32_t> &fte
 static int ctx_run_sync(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
+    if (next_gen(c)) return GCK_EDEVICE;
     hipStream_t s = c->stream;
     const uint32_t nc = c->n_chunks, nf = c->nfiles;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
@@ -1546,6 +1563,7 @@ static void make_groups(Ctx *c) {
 static int ctx_run_pipe(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
+    if (next_gen(c)) return GCK_EDEVICE;
     hipStream_t s = c->stream;
     const uint32_t nf = c->nfiles, G = (uint32_t)c->g_file.size() - 1;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
