@@ -36,9 +36,13 @@ enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 #ifndef GCK_DEPTH
-#define GCK_DEPTH 2
+#define GCK_DEPTH 1
 #endif
-constexpr int kDepth = GCK_DEPTH;  // rows in flight per k_crc_rows wavefront
+constexpr int kDepth = GCK_DEPTH;  // steps in flight per k_crc_rows wavefront
+#ifndef GCK_NR
+#define GCK_NR 2
+#endif
+constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes at once
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -800,6 +804,67 @@ __device__ __forceinline__ RowOut1 crc_row1(const uint32_t *lds, uint32_t lane, 
     return o;
 }
 
+// NR rows of one wavefront at once (k_crc_rows): the NR CRC chains of a lane
+// are independent, so their LDS lookups interleave and each wave keeps NR
+// table reads in flight per step of the chain (ILP against LDS latency).  Per
+// row exactly crc_row1's arithmetic.
+template <int MODE, int NR>
+__device__ __forceinline__ void crc_rowsN(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1,
+                                          uint32_t nbase, const uint64_t (&rs)[NR], uint32_t (&words)[NR][16],
+                                          const int32_t (&cc)[NR], const uint32_t (&my_id)[NR],
+                                          const uint32_t (&t)[NR], RowOut1 (&o)[NR]) {
+    int32_t cj[NR];
+    uint32_t crc[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        cj[i] = cc[i] ? (cc[i] - 1) >> 2 : 99;
+        crc[i] = 0;
+        o[i] = RowOut1{};
+        if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded rows
+#pragma unroll
+            for (int j = 0; j < 16; ++j) words[i][j] = (uint32_t)(rs[i] >> 4) * 2654435761u + lane * 97u + j;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t nc[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+            nc[i] = (MODE & 2) ? __builtin_amdgcn_alignbit(crc[i] ^ words[i][j], crc[i] ^ words[i][j], 5) + 0x9E3779B9u
+                               : slice4(lds, lb0, lb1, crc[i] ^ words[i][j]);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            if (j == cj[i]) {
+                const int nb = cc[i] - 4 * j;
+                if (nb < 4) {
+                    uint32_t x = crc[i], y = words[i][j];
+                    for (int b = 0; b < nb; ++b) {
+                        x = byte1(lds, lb1, x, y);
+                        y >>= 8;
+                    }
+                    nc[i] = x;
+                }
+                o[i].e = nc[i];
+                nc[i] = 0;
+            }
+            crc[i] = nc[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const uint32_t z = t[i] != kNone32 ? crc[i] : 0u;
+        o[i].rend = crc[i] ^ t[i];
+        if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
+            asm volatile("" ::"v"(crc[i]), "v"(z));
+        } else {
+            uint32_t runv, runprev, tprev;
+            wave_runs(lds, lane, nbase, z, t[i], runv, runprev, tprev);
+            o[i].rend = t[i] != kNone32 ? runv : 0u;
+            o[i].pre = (cc[i] && lane > 0 && tprev == my_id[i]) ? runprev : 0u;
+        }
+    }
+}
+
 // Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
@@ -830,7 +895,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint3
 // load would make every LDS wait (lgkmcnt(0)) wait for HBM too.  Control flow
 // around the stores is uniform and their number fixed, so the compiler's vmcnt
 // waits land rows after the loads they wait for.
-template <int MODE, int DEPTH>
+template <int MODE, int DEPTH, int NR>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
                                                    const uint8_t *__restrict__ plan, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
@@ -843,81 +908,103 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
+    // a step is NR consecutive rows; steps are strided over the wavefronts
+    const uint64_t n_steps = (n_rows + NR - 1) / NR;
     const uint64_t stride = (uint64_t)gridDim.x * kWaves;
 
-    uint64_t row = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    if (row >= n_rows) return;
+    uint64_t step = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
+    if (step >= n_steps) return;
     struct RowBuf {
         u32x4 x[4];
         uint32_t pv;
     };
-    auto issue = [&](uint64_t r, RowBuf &b) {
+    auto issue = [&](uint64_t st, RowBuf (&bs)[NR]) {
         if constexpr ((MODE & 8) != 0) return;
-        // buffer loads: the row base lives in a scalar resource, the lane
-        // offset in one VGPR that never changes (no per-load VGPR address)
-        r = min(r, n_rows - 1);
-        const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
-        const __amdgpu_buffer_rsrc_t rplan = make_rsrc(plan + r * kPlanBytes, kPlanBytes);
-        b.x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel, 0, 0);
-        b.x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 16, 0, 0);
-        b.x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 32, 0, 0);
-        b.x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 48, 0, 0);
-        b.pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
-    };
-    auto process = [&](uint64_t row, const RowBuf &b) {
-        const uint64_t rs = row * kRow;
-        // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
-        const uint64_t H = __ballot(b.pv & 0x80u);
-        const uint32_t ra = (uint32_t)H, hh = (uint32_t)(H >> 32);
-        const uint32_t tail_start = hh & 0x1FFFu;
-        const int32_t cc = (MODE & 1) ? 0 : (int32_t)(b.pv & 0x7Fu);
-        const uint64_t C = __ballot(cc != 0);
-        const uint32_t n_ends = (uint32_t)__popcll(C);
-        const uint32_t idx = __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-        const uint32_t n_le = idx + (cc != 0);  // record ends at or before the slab end
-        // the record open at the slab end: the next one after the ends counted;
-        // it exists if it ends inside the row, or it is the row's tail record and
-        // starts before the slab end (not padding after a file's last record)
-        const uint32_t t = (n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + n_le : kNone32;
-        uint32_t words[16];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            words[4 * k] = b.x[k].x;
-            words[4 * k + 1] = b.x[k].y;
-            words[4 * k + 2] = b.x[k].z;
-            words[4 * k + 3] = b.x[k].w;
+        for (int i = 0; i < NR; ++i) {
+            // buffer loads: the row base lives in a scalar resource, the lane
+            // offset in one VGPR that never changes (no per-load VGPR address)
+            const uint64_t r = min(st * NR + i, n_rows - 1);
+            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
+            const __amdgpu_buffer_rsrc_t rplan = make_rsrc(plan + r * kPlanBytes, kPlanBytes);
+            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel, 0, 0);
+            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 16, 0, 0);
+            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 32, 0, 0);
+            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 48, 0, 0);
+            bs[i].pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
         }
-        const RowOut1 o = crc_row1<MODE>(lds, lane, lb0, lb1, nbase, rs, words, cc, ra + idx, t);
-        // every lane stores: the cut lanes to their record's slot, the rest to
-        // the scratch slot n_total (no branch around a store)
-        // (a row where a slab holds 2+ record ends gets cuts OR'ed together
-        // here; k_crc_rows_big then rewrites all of this row's outputs)
-        const uint64_t slot = cc != 0 ? (uint64_t)ra + idx : n_total;
-        out_e[slot] = o.e;
-        out_pre[slot] = o.pre;
-        out_rend[row] = (uint32_t)__builtin_amdgcn_readlane((int)o.rend, 63);
     };
-    // DEPTH rows in flight while one is processed; the loop is unrolled over
-    // the DEPTH+1 buffers so each has fixed registers (a rotating copy would
-    // force a wait on loads still in flight).
-    RowBuf buf[DEPTH + 1] = {};
+    auto process = [&](uint64_t st, const RowBuf (&bs)[NR]) {
+        uint64_t rs[NR], row[NR];
+        int32_t cc[NR];
+        uint32_t ra[NR], idx[NR], my_id[NR], t[NR];
+        uint32_t words[NR][16];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            row[i] = st * NR + i;
+            rs[i] = row[i] * kRow;
+            // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
+            const uint64_t H = __ballot(bs[i].pv & 0x80u);
+            ra[i] = (uint32_t)H;
+            const uint32_t tail_start = (uint32_t)(H >> 32) & 0x1FFFu;
+            cc[i] = (MODE & 1) ? 0 : (int32_t)(bs[i].pv & 0x7Fu);
+            const uint64_t C = __ballot(cc[i] != 0);
+            const uint32_t n_ends = (uint32_t)__popcll(C);
+            idx[i] = __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
+            const uint32_t n_le = idx[i] + (cc[i] != 0);  // record ends at or before the slab end
+            // the record open at the slab end: the next one after the ends
+            // counted; it exists if it ends inside the row, or it is the row's
+            // tail record and starts before the slab end (not padding after a
+            // file's last record)
+            t[i] = (n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra[i] + n_le : kNone32;
+            my_id[i] = ra[i] + idx[i];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                words[i][4 * k] = bs[i].x[k].x;
+                words[i][4 * k + 1] = bs[i].x[k].y;
+                words[i][4 * k + 2] = bs[i].x[k].z;
+                words[i][4 * k + 3] = bs[i].x[k].w;
+            }
+        }
+        RowOut1 o[NR];
+        crc_rowsN<MODE, NR>(lds, lane, lb0, lb1, nbase, rs, words, cc, my_id, t, o);
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            // every lane stores: the cut lanes to their record's slot, the rest
+            // (and rows past the end) to the scratch slots (no branch around a
+            // store).  A row where a slab holds 2+ record ends gets cuts OR'ed
+            // together here; k_crc_rows_big then rewrites all its outputs.
+            const bool dead = row[i] >= n_rows;
+            const uint64_t slot = (cc[i] != 0 && !dead) ? (uint64_t)ra[i] + idx[i] : n_total;
+            out_e[slot] = o[i].e;
+            out_pre[slot] = o[i].pre;
+            *(dead ? rend_scratch : out_rend + row[i]) = (uint32_t)__builtin_amdgcn_readlane((int)o[i].rend, 63);
+        }
+    };
+    // DEPTH steps in flight while one is processed; the loop is unrolled over
+    // the DEPTH+1 buffer sets so each has fixed registers (a rotating copy
+    // would force a wait on loads still in flight).
+    RowBuf buf[DEPTH + 1][NR] = {};
 #pragma unroll
     for (int i = 0; i < DEPTH; ++i) {
-        issue(row + i * stride, buf[i]);
-        // the 3 stores of a processed row, to the scratch slots: the loop is
+        issue(step + i * stride, buf[i]);
+        // the stores of a processed step, to the scratch slots: the loop is
         // entered with the same vector-memory queue shape as its back edge, so
         // the compiler's waits at the loop head are as late as in the body
-        out_e[n_total] = 0;
-        out_pre[n_total] = 0;
-        *rend_scratch = 0;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) {
+            out_e[n_total] = 0;
+            out_pre[n_total] = 0;
+            *rend_scratch = 0;
+        }
     }
     for (;;) {
 #pragma unroll
         for (int i = 0; i <= DEPTH; ++i) {
-            issue(row + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
-            process(row, buf[i]);
-            row += stride;
-            if (row >= n_rows) return;
+            issue(step + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
+            process(step, buf[i]);
+            step += stride;
+            if (step >= n_steps) return;
         }
     }
 }
@@ -1356,9 +1443,9 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
 static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
                        const uint32_t *big_count) {
     if (r1 <= r0) return;
-    const uint64_t nr = r1 - r0, want = (nr + kWaves - 1) / kWaves;
+    const uint64_t nr = r1 - r0, want = (nr + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-    k_crc_rows<0, kDepth><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>() + r0 * kRow, nr,
+    k_crc_rows<0, kDepth, kRowsPerStep><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>() + r0 * kRow, nr,
                                                 c->d_plan.as<uint8_t>() + r0 * kPlanBytes, cap,
                                                 c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
                                                 c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
@@ -1812,7 +1899,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     Ctx *c = &ctx->c;
     if (!c->n_rows || !c->n_recs) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
-    const uint64_t want = (c->n_rows + kWaves - 1) / kWaves;
+    const uint64_t want = (c->n_rows + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
@@ -1821,7 +1908,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
     for (int i = 0; i < iters; ++i) {
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
-        k_crc_rows<M, kDepth><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
+        k_crc_rows<M, kDepth, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
                                                     c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
                                                     c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
                                                     c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows);    \
