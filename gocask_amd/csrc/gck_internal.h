@@ -50,7 +50,8 @@ enum Phase {
     PH_SCAN,          // record slots per chunk, per-file summary
     PH_HOST,          // D2H summary + host bookkeeping (synchronous path)
     PH_RECORDS,       // k_compact, k_row_fill / k_row_index, k_row_plan
-    PH_CRC,           // k_crc_rows (+ k_crc_rows_big): the HBM-bound kernel
+    PH_CRC,           // k_crc_rows: the HBM-bound kernel
+    PH_CRCBIG,        // k_crc_rows_big: rows where a slab holds 2+ record ends
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
     PH_PIPE = PH_END, // (time) device span of the whole run
@@ -89,8 +90,6 @@ struct Ctx {
     // rows
     uint64_t n_rows = 0;
     DBuf d_row_first, d_rend, d_plan, d_big;
-    DBuf d_slow;           // per row: generation of the run that listed it as slow
-    uint32_t run_gen = 0;  // gck_ctx_run counter
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;

@@ -46,6 +46,13 @@ constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes a
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
+}
+
 __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t sh) {
     return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
@@ -145,7 +152,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                                                     uint64_t *__restrict__ ch_entry, uint32_t n_chunks,
                                                     uint32_t max_key) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
     if (c >= n_chunks) return;
     const uint32_t f = ch_file[c];
     const uint64_t cs = ch_start[c], ce = ch_end[c], base = fbase[f], len = flen[f];
@@ -154,16 +161,19 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     if (cs == 0) {
         found = 0;
     } else {
-        // windows are double-buffered (A/B, unrolled so neither is copied):
-        // the next window's loads are in flight while this one is checked
-        auto load = [&](uint64_t b0, uint4 (&v)[5]) {
+        // The scan loop only computes candidate masks (no dependent loads in
+        // it, so the next windows' loads stay in flight: windows A/B/C rotate,
+        // unrolled so none is copied); a window with candidates leaves the
+        // loop for the chain tests and the scan resumes after it if none holds.
+        auto load = [&](uint64_t b0, u32x4 (&v)[5]) {
             // bytes [p0, p0+80): the 64 positions plus their header bytes (the
-            // arena is 16 B aligned here and padded 4 windows past every file)
-            const uint4 *src = reinterpret_cast<const uint4 *>(arena + base + b0 + 64ull * lane);
+            // arena is padded 3 windows past every file).  Buffer loads: the
+            // compiler keeps them where they are issued (ahead of their use).
+            const __amdgpu_buffer_rsrc_t rw = make_rsrc(arena + base + b0, 4096 + 80);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) v[k] = src[k];
+            for (int k = 0; k < 5; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, lane * 64 + 16 * k, 0, 0);
         };
-        auto scan = [&](uint64_t b0, const uint4 (&v)[5]) {
+        auto cands = [&](const u32x4 (&v)[5]) -> uint64_t {  // bit t: bytes p0+t+10, p0+t+11 both zero
             uint32_t w[20];
 #pragma unroll
             for (int k = 0; k < 5; ++k) {
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
             uint32_t zf[20];
 #pragma unroll
             for (int k = 2; k < 20; ++k) zf[k] = zero_bytes(w[k]);
-            uint64_t cm = 0;  // bit t: bytes p0+t+10, p0+t+11 both zero
+            uint64_t cm = 0;
 #pragma unroll
             for (int k = 2; k <= 18; ++k) {
                 const uint32_t pr = zf[k] & ((zf[k] >> 8) | (zf[k + 1] << 24));
@@ -183,6 +193,31 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 const int t0 = 4 * k - 10;
                 cm |= t0 >= 0 ? (uint64_t)nib << t0 : (uint64_t)(nib >> -t0);
             }
+            return cm;
+        };
+        uint64_t from = cs;
+        while (found == kNone && from < ce) {
+            uint64_t wb = kNone, cm = 0;
+            {
+                u32x4 A[5], B[5], C[5];
+                load(from, A);
+                load(from + 4096, B);
+                for (uint64_t b0 = from;; b0 += 3 * 4096) {
+                    load(b0 + 2 * 4096, C);
+                    cm = cands(A);
+                    if (__ballot(cm != 0)) { wb = b0; break; }
+                    if (b0 + 4096 >= ce) break;
+                    load(b0 + 3 * 4096, A);
+                    cm = cands(B);
+                    if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
+                    if (b0 + 2 * 4096 >= ce) break;
+                    load(b0 + 4 * 4096, B);
+                    cm = cands(C);
+                    if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
+                    if (b0 + 3 * 4096 >= ce) break;
+                }
+            }
+            if (wb == kNone) break;
             uint64_t lanes = __ballot(cm != 0);
             while (lanes && found == kNone) {
                 const int l = __ffsll((long long)lanes) - 1;
@@ -190,7 +225,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cm, l);
                 while (lm) {
                     const int t = __ffsll((long long)lm) - 1;
-                    const uint64_t q = b0 + 64ull * l + t;
+                    const uint64_t q = wb + 64ull * l + t;
                     if (q < ce && chain_ok(arena, base, len, q, mk)) {
                         found = q;
                         break;
@@ -199,16 +234,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 }
                 lanes &= lanes - 1;
             }
-        };
-        uint4 A[5], B[5];
-        load(cs, A);
-        for (uint64_t b0 = cs;; b0 += 8192) {
-            load(b0 + 4096, B);
-            scan(b0, A);
-            if (found != kNone || b0 + 4096 >= ce) break;
-            load(b0 + 8192, A);
-            scan(b0 + 4096, B);
-            if (found != kNone || b0 + 8192 >= ce) break;
+            from = wb + 4096;
         }
         if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, mk)) found += 1;
     }
@@ -542,48 +568,58 @@ __device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ 
 //              H[0..31] = ra, the first record whose end lies past the row start
 //              H[32..44] = tail start (row_tail_start)
 // Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
-// plan carries no ids or counts.  Built in two passes: k_row_plan writes each
-// row's header bits (row-parallel), k_row_cuts ORs in the cut of every record
-// (record-parallel) and lists the rows where a slab holds 2+ record ends
-// (records under 64 B) for k_crc_rows_big.
-__global__ void k_row_plan(const uint64_t *__restrict__ rec_off, const uint64_t *__restrict__ rng, uint64_t r0,
-                           uint64_t nr, const uint32_t *__restrict__ row_first, uint4 *__restrict__ plan) {
-    const uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (row >= r0 + nr) return;
-    const uint32_t ra = row_first[row], rb = row_first[row + 1];
-    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, row * kRow) << 32);
+// plan carries no ids or counts.  Rows where a slab holds 2+ record ends
+// (records under 64 B) are listed for k_crc_rows_big, which rewrites all of
+// k_crc_rows' outputs for them.
+//
+// One wavefront per 64 rows (lane = row): the records ending in those rows
+// are a contiguous range, read 64 at a time (coalesced); each lane ORs its
+// record's cut into an LDS image of the 64 plan rows, then every lane writes
+// its row (64 B, header bits added): 4 KiB contiguous per wavefront.
+constexpr int kPlanWaves = 4;
+
+__global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__restrict__ rec_off,
+                                                              const uint4 *__restrict__ rec_hdr,
+                                                              const uint64_t *__restrict__ rng, uint64_t r0,
+                                                              uint64_t nr, const uint32_t *__restrict__ row_first,
+                                                              uint4 *__restrict__ plan,
+                                                              uint32_t *__restrict__ big_rows, uint32_t *big_count) {
+    __shared__ uint32_t cut_lds[kPlanWaves][64 * 16];
+    __shared__ uint32_t slow_lds[kPlanWaves][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t R0 = r0 + ((uint64_t)blockIdx.x * kPlanWaves + wv) * 64, r1 = r0 + nr;
+    if (R0 >= r1) return;
+    uint32_t *cw = cut_lds[wv];
+    for (uint32_t i = lane; i < 64 * 16; i += 64) cw[i] = 0;
+    slow_lds[wv][lane] = 0;
+    const uint64_t Re = min(R0 + 64, r1);  // rows [R0, Re)
+    const uint64_t R = R0 + lane;
+    const bool live = R < Re;
+    const uint32_t ra = row_first[min(R, r1)], rb = row_first[min(R + 1, r1)];
+    const uint64_t lo = row_first[R0], hi = row_first[Re];  // records ending in rows [R0, Re)
+    for (uint64_t b = lo; b < hi; b += 64) {
+        const uint64_t r = b + lane;
+        if (r < hi) {
+            const uint64_t ve = value_end(rec_off, rec_hdr, r);
+            const uint32_t rl = (uint32_t)((ve - 1) / kRow - R0);  // 0..63
+            const uint32_t end = (uint32_t)(ve - (R0 + rl) * kRow), slab = (end - 1) >> 6;
+            atomicOr(cw + rl * 16 + (slab >> 2), (end - slab * kSlab) << (8 * (slab & 3)));
+            // the record before ends in the same slab (never for the range's
+            // first record: it ends in an earlier row)
+            if (r > lo && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6) slow_lds[wv][rl] = 1;
+        }
+    }
+    if (!live) return;
+    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, R * kRow) << 32);
     uint32_t w[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const uint32_t nib = (uint32_t)(H >> (4 * i)) & 15u;  // header bits of bytes 4i .. 4i+3
-        w[i] = ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
+        w[i] = cw[lane * 16 + i] | ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) plan[row * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-}
-
-// Record-parallel: OR each record's cut into the byte of its end slab (a
-// plain read-modify-write: in rows where every slab holds at most one record
-// end, each byte has one writer).  A record ending in the same slab as the one
-// before makes its row slow: listed once per run (slow_gen[row] == gen) for
-// k_crc_rows_big, which recomputes everything k_crc_rows wrote for that row.
-__global__ void k_row_cuts(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
-                           const uint64_t *__restrict__ rng, uint8_t *__restrict__ plan,
-                           uint32_t *__restrict__ slow_gen, uint32_t gen, uint32_t *__restrict__ big_rows,
-                           uint32_t *big_count) {
-    const uint64_t rb = rng[0], re = rng[1];
-    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ve = value_end(rec_off, rec_hdr, r);
-        const uint64_t row = (ve - 1) / kRow;
-        const uint32_t end = (uint32_t)(ve - row * kRow);  // 1..kRow
-        const uint32_t slab = (end - 1) >> 6;
-        uint8_t *pb = plan + row * kPlanBytes + slab;
-        *pb = (uint8_t)(*pb | (end - slab * kSlab));
-        if (r > rb && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6 &&
-            atomicExch(slow_gen + row, gen) != gen)
-            big_rows[atomicAdd(big_count, 1u)] = (uint32_t)row;
-    }
+    for (int i = 0; i < 4; ++i) plan[R * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
+    if (slow_lds[wv][lane]) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)R;
 }
 
 // LDS image of the slicing-by-4 tables: two 64 KiB regions; in region r,
@@ -611,7 +647,6 @@ __device__ __forceinline__ uint32_t byte1(const uint32_t *lds, uint32_t lb1, uin
     return lds_at(lds, tbl_addr<0>(crc ^ b, lb1) + 128) ^ (crc >> 8);
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -865,10 +900,6 @@ __device__ __forceinline__ void crc_rowsN(const uint32_t *lds, uint32_t lane, ui
     }
 }
 
-// Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, (int)bytes, 0x00020000);
-}
 
 // The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns bytes
 // [64k, 64k+64).  Every byte enters a CRC register, no masking: records tile
@@ -1264,7 +1295,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_slow};
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1313,12 +1344,11 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     const uint64_t nc = c->n_chunks, nf = nfiles ? nfiles : 1;
     const uint64_t cap = c->opts.chunk_cap;
     int rc;
-    // slack past the last file: k_spec_entry reads up to two 4 KiB windows
+    // slack past the last file: k_spec_entry reads up to three 4 KiB windows
     // (+80 B) beyond a chunk end
-    const bool fresh = c->arena.cap < pos + 4 * kRow;
-    if ((rc = c->arena.ensure(pos + 4 * kRow))) return rc;
+    const bool fresh = c->arena.cap < pos + 5 * kRow;
+    if ((rc = c->arena.ensure(pos + 5 * kRow))) return rc;
     if (fresh) GCK_HIP(hipMemset(c->arena.p, 0, c->arena.cap));
-    const bool slow_fresh = c->d_slow.cap < (c->n_rows + 1) * 4;
     if ((rc = c->d_fbase.ensure(nf * 8)) || (rc = c->d_flen.ensure(nf * 8)) || (rc = c->d_ffirst.ensure(nf * 4)) ||
         (rc = c->d_fnch.ensure(nf * 4)) || (rc = c->d_fbad.ensure(nf * 4)) || (rc = c->d_fterm.ensure(nf * 4)) ||
         (rc = c->d_ftpos.ensure(nf * 8)) || (rc = c->d_fnrec.ensure(nf * 8)) ||
@@ -1330,10 +1360,8 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_slow.ensure((c->n_rows + 1) * 4)))
+        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)))
         return rc;
-    if (slow_fresh) GCK_HIP(hipMemset(c->d_slow.p, 0, c->d_slow.cap));  // generation 0: never listed
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
         GCK_HIP(hipMemcpy(c->d_flen.p, c->f_len.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -1431,17 +1459,15 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
                                      c->d_row_first.as<uint32_t>());
     if (r1 > r0)
-        k_row_plan<<<nblk(r1 - r0, 256), 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), rng, r0, r1 - r0,
-                                                      c->d_row_first.as<uint32_t>(), c->d_plan.as<uint4>());
-    k_row_cuts<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng,
-                                    c->d_plan.as<uint8_t>(), c->d_slow.as<uint32_t>(), c->run_gen,
-                                    c->d_big.as<uint32_t>() + r0, big_count);
+        k_row_plan<<<nblk(r1 - r0, 64 * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
+            c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0, r1 - r0, c->d_row_first.as<uint32_t>(),
+            c->d_plan.as<uint4>(), c->d_big.as<uint32_t>() + r0, big_count);
 }
 
 // CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
 // k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
 static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
-                       const uint32_t *big_count) {
+                       const uint32_t *big_count, hipEvent_t between = nullptr) {
     if (r1 <= r0) return;
     const uint64_t nr = r1 - r0, want = (nr + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
@@ -1450,6 +1476,7 @@ static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const ui
                                                 c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
                                                 c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
                                                 c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
+    if (between) (void)hipEventRecord(between, s);
     k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0, big_count,
                                               c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
                                               c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
@@ -1467,15 +1494,6 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_zrow.as<uint32_t>(),
                                     c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
-}
-
-// A fresh generation for the slow-row list of each run attempt.
-static int next_gen(Ctx *c) {
-    if (++c->run_gen == 0) {  // wrapped: start over
-        GCK_HIP(hipMemset(c->d_slow.p, 0, c->d_slow.cap));
-        c->run_gen = 1;
-    }
-    return GCK_OK;
 }
 
 static int ensure_records(Ctx *c, uint64_t nr) {
@@ -1540,7 +1558,6 @@ static int read_file_summaries(Ctx *c, hipStream_t s, std::vector<uint32_t> &fte
 static int ctx_run_sync(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
-    if (next_gen(c)) return GCK_EDEVICE;
     hipStream_t s = c->stream;
     const uint32_t nc = c->n_chunks, nf = c->nfiles;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
@@ -1602,7 +1619,8 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
     launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
+    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG, c->ev[PH_CRCBIG]);
+    else GCK_HIP(hipEventRecord(c->ev[PH_CRCBIG], s));
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1650,7 +1668,6 @@ static void make_groups(Ctx *c) {
 static int ctx_run_pipe(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
-    if (next_gen(c)) return GCK_EDEVICE;
     hipStream_t s = c->stream;
     const uint32_t nf = c->nfiles, G = (uint32_t)c->g_file.size() - 1;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
@@ -1835,7 +1852,8 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
 }
 
 const char *gck_phase_name(int phase) {
-    static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows", "finalize", "pipeline"};
+    static const char *names[] = {"boundary", "scan",     "host_sync", "records",
+                                  "crc_rows", "crc_big", "finalize",  "pipeline"};
     return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
