@@ -89,7 +89,7 @@ struct Ctx {
     DBuf d_rec_off, d_rec_hdr, d_rec_file, d_e, d_pre, d_out;
     // rows
     uint64_t n_rows = 0;
-    DBuf d_row_first, d_rend, d_plan, d_big;
+    DBuf d_row_first, d_rend, d_plan, d_big, d_bigcnt;
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;

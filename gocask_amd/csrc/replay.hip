@@ -553,20 +553,11 @@ __global__ void k_group_carry(uint32_t nf, const uint64_t *__restrict__ flen, co
 
 constexpr int kPlanBytes = 64;  // per row: one byte per 64 B slab (= per k_crc_rows lane)
 
-// Tail start of row `row`: row-relative start of record rb (the record open at
-// the row end), clamped to [0, kRow]; kRow if there is none.
-__device__ __forceinline__ uint32_t row_tail_start(const uint64_t *__restrict__ rec_off, uint64_t n_total,
-                                                   uint32_t rb, uint64_t rs) {
-    if (rb >= n_total) return kRow;
-    const int64_t st = (int64_t)rec_off[rb] - (int64_t)rs;
-    return (uint32_t)max(min(st, (int64_t)kRow), (int64_t)0);
-}
 
 // Per-row plan for k_crc_rows, 64 bytes, byte k for lane k (slab k):
 //   bits 0..6  cut: offset (1..64) inside slab k where a record ends, 0 = none
 //   bit  7     bit k of the row header H, recovered with one ballot:
 //              H[0..31] = ra, the first record whose end lies past the row start
-//              H[32..44] = tail start (row_tail_start)
 // Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
 // plan carries no ids or counts.  Rows where a slab holds 2+ record ends
 // (records under 64 B) are listed for k_crc_rows_big, which rewrites all of
@@ -583,19 +574,20 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__
                                                               const uint64_t *__restrict__ rng, uint64_t r0,
                                                               uint64_t nr, const uint32_t *__restrict__ row_first,
                                                               uint4 *__restrict__ plan,
-                                                              uint32_t *__restrict__ big_rows, uint32_t *big_count) {
-    __shared__ uint32_t cut_lds[kPlanWaves][64 * 16];
+                                                              uint32_t *__restrict__ big_rows,
+                                                              uint32_t *__restrict__ big_cnt, uint32_t *big_any) {
+    __shared__ uint32_t cut_lds[kPlanWaves][64 * 17];  // row stride 17 words: conflict-free row reads
     __shared__ uint32_t slow_lds[kPlanWaves][64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t R0 = r0 + ((uint64_t)blockIdx.x * kPlanWaves + wv) * 64, r1 = r0 + nr;
     if (R0 >= r1) return;
     uint32_t *cw = cut_lds[wv];
-    for (uint32_t i = lane; i < 64 * 16; i += 64) cw[i] = 0;
+    for (uint32_t i = lane; i < 64 * 17; i += 64) cw[i] = 0;
     slow_lds[wv][lane] = 0;
     const uint64_t Re = min(R0 + 64, r1);  // rows [R0, Re)
     const uint64_t R = R0 + lane;
     const bool live = R < Re;
-    const uint32_t ra = row_first[min(R, r1)], rb = row_first[min(R + 1, r1)];
+    const uint32_t ra = live ? row_first[R] : 0u;
     const uint64_t lo = row_first[R0], hi = row_first[Re];  // records ending in rows [R0, Re)
     for (uint64_t b = lo; b < hi; b += 64) {
         const uint64_t r = b + lane;
@@ -603,23 +595,38 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__
             const uint64_t ve = value_end(rec_off, rec_hdr, r);
             const uint32_t rl = (uint32_t)((ve - 1) / kRow - R0);  // 0..63
             const uint32_t end = (uint32_t)(ve - (R0 + rl) * kRow), slab = (end - 1) >> 6;
-            atomicOr(cw + rl * 16 + (slab >> 2), (end - slab * kSlab) << (8 * (slab & 3)));
+            atomicOr(cw + rl * 17 + (slab >> 2), (end - slab * kSlab) << (8 * (slab & 3)));
             // the record before ends in the same slab (never for the range's
             // first record: it ends in an earlier row)
             if (r > lo && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6) slow_lds[wv][rl] = 1;
         }
     }
-    if (!live) return;
-    const uint64_t H = (uint64_t)ra | ((uint64_t)row_tail_start(rec_off, rng[1], rb, R * kRow) << 32);
-    uint32_t w[16];
+    // header bits (ra) into the LDS image, then write the 64 rows out with
+    // each store instruction covering 1 KiB contiguous (a lane-per-row store
+    // would scatter 16 B pieces at a 64 B stride: partial-line writes)
+    const uint64_t H = ra;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t nib = (uint32_t)(H >> (4 * i)) & 15u;  // header bits of bytes 4i .. 4i+3
-        w[i] = cw[lane * 16 + i] | ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
+    for (int i = 0; i < 8; ++i) {  // header bits live in bytes 0..31 (ra is 32 bits)
+        const uint32_t nib = (uint32_t)(H >> (4 * i)) & 15u;
+        cw[lane * 17 + i] |= ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
     }
+    uint4 *blk = plan + R0 * 4;  // the wavefront's rows as 16 B units
 #pragma unroll
-    for (int i = 0; i < 4; ++i) plan[R * 4 + i] = make_uint4(w[4 * i], w[4 * i + 1], w[4 * i + 2], w[4 * i + 3]);
-    if (slow_lds[wv][lane]) big_rows[atomicAdd(big_count, 1u)] = (uint32_t)R;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t u = lane + 64 * k, rl = u >> 2, q = (u & 3) * 4;  // 16 B unit u: row rl, words q..q+3
+        if (R0 + rl < Re)
+            blk[u] = make_uint4(cw[rl * 17 + q], cw[rl * 17 + q + 1], cw[rl * 17 + q + 2], cw[rl * 17 + q + 3]);
+    }
+    // slow rows: compacted into this wavefront's 64 list slots, count per
+    // wavefront (no atomics: a global counter here serialises at one address)
+    const bool slow = live && slow_lds[wv][lane];
+    const uint64_t sm = __ballot(slow);
+    const uint32_t w = (uint32_t)((R0 - r0) >> 6);
+    if (slow) big_rows[(uint64_t)w * 64 + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] = (uint32_t)R;
+    if (lane == 0) {
+        big_cnt[w] = (uint32_t)__popcll(sm);
+        if (sm) *big_any = 1u;
+    }
 }
 
 // LDS image of the slicing-by-4 tables: two 64 KiB regions; in region r,
@@ -977,17 +984,17 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
             const uint64_t H = __ballot(bs[i].pv & 0x80u);
             ra[i] = (uint32_t)H;
-            const uint32_t tail_start = (uint32_t)(H >> 32) & 0x1FFFu;
+
             cc[i] = (MODE & 1) ? 0 : (int32_t)(bs[i].pv & 0x7Fu);
             const uint64_t C = __ballot(cc[i] != 0);
-            const uint32_t n_ends = (uint32_t)__popcll(C);
             idx[i] = __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
             const uint32_t n_le = idx[i] + (cc[i] != 0);  // record ends at or before the slab end
             // the record open at the slab end: the next one after the ends
-            // counted; it exists if it ends inside the row, or it is the row's
-            // tail record and starts before the slab end (not padding after a
-            // file's last record)
-            t[i] = (n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra[i] + n_le : kNone32;
+            // counted.  (Past a file's last record the slab is padding and
+            // "record" t is the next file's first one or none: the padding only
+            // reaches this row's rend, which no record reads, since records
+            // never cross files and files start on row boundaries.)
+            t[i] = ra[i] + n_le;
             my_id[i] = ra[i] + idx[i];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1046,7 +1053,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict__ arena,
                                                        const uint32_t *__restrict__ big_rows,
-                                                       const uint32_t *__restrict__ big_count,
+                                                       const uint32_t *__restrict__ big_cnt,
+                                                       const uint32_t *__restrict__ big_any, uint32_t n_lists,
                                                        const uint32_t *__restrict__ row_first,
                                                        const uint64_t *__restrict__ rng,
                                                        const uint64_t *__restrict__ rec_off,
@@ -1055,8 +1063,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
                                                        const uint32_t *__restrict__ g_nib,
                                                        uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
                                                        uint32_t *__restrict__ out_rend) {
-    const uint32_t nbig = *big_count;
-    if (blockIdx.x * kWaves >= nbig) return;
+    if (*big_any == 0) return;
     const uint64_t n_total = rng[1];
     __shared__ uint32_t lds[40960];
     fill_crc_lds(lds, g_slice, g_nib);
@@ -1064,10 +1071,17 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const int32_t s_rel = (int32_t)lane * kSlab;
-    for (uint32_t bi = blockIdx.x * kWaves + (threadIdx.x >> 6); bi < nbig; bi += gridDim.x * kWaves) {
-        const uint64_t row = big_rows[bi], rs = row * kRow;
+    // list w holds big_cnt[w] rows at big_rows[64 w ..] (k_row_plan)
+    uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6)), i = 0;
+    for (;;) {
+        while (w < n_lists && i >= big_cnt[w]) {
+            w += gridDim.x * kWaves;
+            i = 0;
+        }
+        if (w >= n_lists) break;
+        const uint64_t row = big_rows[(uint64_t)w * 64 + i++], rs = row * kRow;
         const uint32_t ra = row_first[row], rb = row_first[row + 1], n_ends = rb - ra;
-        const uint32_t tail_start = row_tail_start(rec_off, n_total, rb, rs);
+
         RowCuts rc;
         for (uint32_t j0 = 0; j0 < n_ends; j0 += 64) {
             const uint32_t cnt = min(64u, n_ends - j0);
@@ -1075,7 +1089,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict
             const int32_t e_ = (int32_t)(value_end(rec_off, rec_hdr, r) - rs);
             for (uint32_t j = 0; j < cnt; ++j) rc.take((uint32_t)__builtin_amdgcn_readlane(e_, j), j0 + j, ra, lane, s_rel);
         }
-        const uint32_t t = (rc.n_le < n_ends || (int32_t)tail_start < s_rel + kSlab) ? ra + rc.n_le : kNone32;
+        const uint32_t t = ra + rc.n_le;  // see k_crc_rows
         const uint4 *src = reinterpret_cast<const uint4 *>(arena + rs + s_rel);
         uint32_t words[16];
 #pragma unroll
@@ -1127,16 +1141,46 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         T[i] = g_slice[i];
     }
     __syncthreads();
-    const uint64_t rb = rng[0], re = rng[1];
-    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t start = rec_off[r];
-        const uint4 h = rec_hdr[r];
-        const uint32_t f = rec_file[r];
+    const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
+    // software-pipelined over the grid-stride loop: the next record's table
+    // entries are in flight while this one is finished
+    struct RecIn {
+        uint64_t start;
+        uint4 h;
+        uint32_t f, e, pre;
+    };
+    auto fetch = [&](uint64_t r) {
+        RecIn x;
+        x.start = rec_off[r];
+        x.h = rec_hdr[r];
+        x.f = rec_file[r];
+        x.e = e[r];
+        x.pre = pre[r];
+        return x;
+    };
+    uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
+    RecIn cur{};
+    if (r < re) cur = fetch(r);
+    for (; r < re; r += G) {
+        const RecIn nxt = fetch(min(r + G, re - 1));
+        const uint64_t start = cur.start;
+        const uint4 h = cur.h;
+        const uint32_t f = cur.f;
         const uint32_t V = h.w;
         const uint64_t vs = start + 16 + h.z, ve = vs + V;
         const uint64_t w0 = (start + 3) & ~3ull;
         const uint64_t fr = w0 / kRow, lr = (ve - 1) / kRow;
+        const uint64_t row_end = (lr + 1) * kRow;
+        // independent loads first: the tables for the shifts, the prefix words
+        const uint32_t xinv_d = xinv[row_end - ve];
+        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
+        const uint32_t zv = V < (1u << 17) ? zl[V] : 0u;
+        const uint32_t L = (uint32_t)(vs - w0);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
+        uint32_t pw[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) pw[i] = wp[i];  // header tail + keys up to 24 B (the arena is padded)
         // Horner over the rows the chain crosses; the row values are loaded 8
         // at a time so their latency overlaps
         uint32_t acc = 0;
@@ -1148,25 +1192,21 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
             for (int j = 0; j < 8; ++j)
                 if (row + j < lr) acc = z4096(Tz, acc) ^ v[j];
         }
-        acc = z4096(Tz, acc) ^ pre[r];
-        const uint64_t row_end = (lr + 1) * kRow;
-        const uint32_t chain = e[r] ^ (acc ? multmodp(xinv[row_end - ve], acc) : 0u);
-        // F(0, prefix): the bytes [w0, vs) = header tail + key, read as aligned
-        // words from the arena (slicing-by-4), the last partial word bytewise
-        const uint32_t L = (uint32_t)(vs - w0);
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
+        acc = z4096(Tz, acc) ^ cur.pre;
+        const uint32_t chain = cur.e ^ (acc ? multmodp(xinv_d, acc) : 0u);
+        // F(0, prefix): the bytes [w0, vs) = header tail + key as aligned words
+        // (slicing-by-4), the last partial word bytewise
         uint32_t p = 0;
         for (uint32_t i = 0; i < L / 4; ++i) {
-            const uint32_t x = p ^ wp[i];
+            const uint32_t x = p ^ (i < 10 ? pw[i] : wp[i]);
             p = T[768 + (x & 0xFF)] ^ T[512 + ((x >> 8) & 0xFF)] ^ T[256 + ((x >> 16) & 0xFF)] ^ T[x >> 24];
         }
         if (L & 3) {
-            uint32_t y = wp[L / 4];
+            uint32_t y = L / 4 < 10 ? pw[L / 4] : wp[L / 4];
             for (uint32_t i = 0; i < (L & 3); ++i, y >>= 8) p = T[(p ^ y) & 0xFF] ^ (p >> 8);
         }
-        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
         const uint32_t raw0 = chain ^ (p ? multmodp(xv, p) : 0u);
-        const uint32_t z = V < (1u << 17) ? zl[V] : multmodp(multmodp(xa[V >> 16], xb[V & 0xFFFF]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        const uint32_t z = V < (1u << 17) ? zv : multmodp(multmodp(xa[V >> 16], xb[V & 0xFFFF]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         const uint32_t calc = raw0 ^ z;
         const uint64_t fo = start - fbase[f];
         const bool tomb = h.z == 0;
@@ -1181,10 +1221,18 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == h.x ? GCK_F_CRC_OK : 0u);
         o.crc_calc = calc;
         out[r] = o;
-        const uint64_t m = __ballot(calc != h.x);  // one atomic per wavefront with rejects
-        if (m && (threadIdx.x & 63) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))
-            atomicAdd(&counters[3], (uint32_t)__popcll(m));
+        n_rej += calc != h.x;
+        cur = nxt;
     }
+    // one global atomic per block (per-record or per-wavefront atomics on one
+    // address serialise: C5 has ~100k rejects)
+    __shared__ uint32_t blk_rej;
+    if (threadIdx.x == 0) blk_rej = 0;
+    __syncthreads();
+    const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(n_rej), 63);
+    if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&blk_rej, wsum);
+    __syncthreads();
+    if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[3], blk_rej);
 }
 
 // ------------------------------------------------------------- host side ---
@@ -1295,7 +1343,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt};
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_bigcnt};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1360,7 +1408,8 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)))
+        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_bigcnt.ensure((c->n_rows / 64 + kMaxGroups + 2) * 4)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -1442,8 +1491,12 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
 }
 
 // Record table of chunks [c0, c1), row index and row plan of rows [r0, r1).
+// Slow-row lists of rows [r0, r1): list slots d_big + r0, per-64-row counts at
+// d_bigcnt + (r0 / 64 + g) (disjoint per file group g), any-flag big_any.
+static uint32_t *big_counts(Ctx *c, uint64_t r0, uint32_t g) { return c->d_bigcnt.as<uint32_t>() + r0 / 64 + g; }
+
 static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
-                           const uint64_t *rng, uint64_t cap, uint32_t *big_count) {
+                           const uint64_t *rng, uint64_t cap, uint32_t g, uint32_t *big_any) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
     if (n)
         k_compact<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
@@ -1461,13 +1514,13 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     if (r1 > r0)
         k_row_plan<<<nblk(r1 - r0, 64 * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
             c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0, r1 - r0, c->d_row_first.as<uint32_t>(),
-            c->d_plan.as<uint4>(), c->d_big.as<uint32_t>() + r0, big_count);
+            c->d_plan.as<uint4>(), c->d_big.as<uint32_t>() + r0, big_counts(c, r0, g), big_any);
 }
 
 // CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
 // k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
 static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
-                       const uint32_t *big_count, hipEvent_t between = nullptr) {
+                       uint32_t g, const uint32_t *big_any, hipEvent_t between = nullptr) {
     if (r1 <= r0) return;
     const uint64_t nr = r1 - r0, want = (nr + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
@@ -1477,7 +1530,8 @@ static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const ui
                                                 c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
                                                 c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
     if (between) (void)hipEventRecord(between, s);
-    k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0, big_count,
+    k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0,
+                                              big_counts(c, r0, g), big_any, (uint32_t)((nr + 63) / 64),
                                               c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
                                               c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
                                               c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
@@ -1617,9 +1671,9 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
 
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG);
+    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, 0, cnt + CNT_BIG);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, cnt + CNT_BIG, c->ev[PH_CRCBIG]);
+    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, 0, cnt + CNT_BIG, c->ev[PH_CRCBIG]);
     else GCK_HIP(hipEventRecord(c->ev[PH_CRCBIG], s));
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
@@ -1690,11 +1744,11 @@ static int ctx_run_pipe(Ctx *c) {
         k_group_carry<<<1, 1, 0, s>>>(f1 - f0, c->d_flen.as<uint64_t>() + f0, c->d_freset.as<uint32_t>() + f0,
                                       c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0,
                                       c->d_carry.as<uint32_t>() + f0, gcarry + g, gcarry + g + 1);
-        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
+        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, g, gcnt + g * 8 + G_BIG);
         GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
         GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
         GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
-        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, gcnt + g * 8 + G_BIG);
+        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, g, gcnt + g * 8 + G_BIG);
         GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
         GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
         GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
