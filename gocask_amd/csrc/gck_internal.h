@@ -51,7 +51,6 @@ enum Phase {
     PH_HOST,          // D2H summary + host bookkeeping (synchronous path)
     PH_RECORDS,       // k_compact, k_row_fill / k_row_index, k_row_plan
     PH_CRC,           // k_crc_rows: the HBM-bound kernel
-    PH_CRCBIG,        // k_crc_rows_big: rows where a slab holds 2+ record ends
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
     PH_PIPE = PH_END, // (time) device span of the whole run
@@ -86,13 +85,13 @@ struct Ctx {
     // records
     uint64_t n_recs = 0;
     uint64_t rec_cap = 0;  // record-table capacity of the current run
-    DBuf d_rec_off, d_rec_hdr, d_rec_file, d_e, d_pre, d_out;
+    DBuf d_rec_off, d_rec_hdr, d_rec_file, d_ep, d_out;
     // rows
     uint64_t n_rows = 0;
-    DBuf d_row_first, d_rend, d_plan, d_big, d_bigcnt;
+    DBuf d_row_first, d_rend, d_plan, d_queue;
 
     // constant tables
-    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;
+    DBuf d_slice, d_nib, d_xinv, d_xfw, d_xa, d_xb, d_zrow, d_zl;
 
     // results of the last run
     int32_t status = 0;

@@ -35,10 +35,6 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
-#ifndef GCK_DEPTH
-#define GCK_DEPTH 1
-#endif
-constexpr int kDepth = GCK_DEPTH;  // steps in flight per k_crc_rows wavefront
 #ifndef GCK_NR
 #define GCK_NR 2
 #endif
@@ -551,82 +547,54 @@ __global__ void k_group_carry(uint32_t nf, const uint64_t *__restrict__ flen, co
     *carry_out = last;
 }
 
-constexpr int kPlanBytes = 64;  // per row: one byte per 64 B slab (= per k_crc_rows lane)
+constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
+constexpr int kBlockRows = 64;   // rows per plan block = per k_crc_rows work item
+constexpr int kPlanLaneBytes = 32;  // plan bytes per lane per block (64 rows x 4 bits)
+constexpr int kPlanRowBytes = kPlanLaneBytes * 64 / kBlockRows;  // = 32: plan bytes per row
+constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
 
-
-// Per-row plan for k_crc_rows, 64 bytes, byte k for lane k (slab k):
-//   bits 0..6  cut: offset (1..64) inside slab k where a record ends, 0 = none
-//   bit  7     bit k of the row header H, recovered with one ballot:
-//              H[0..31] = ra, the first record whose end lies past the row start
-// Record ids of the cuts follow from ra and the cut ballot (mbcnt), so the
-// plan carries no ids or counts.  Rows where a slab holds 2+ record ends
-// (records under 64 B) are listed for k_crc_rows_big, which rewrites all of
-// k_crc_rows' outputs for them.
+// Row plan for k_crc_rows, lane-major per block of 64 rows so that a
+// wavefront loads the plan of a whole block with two 16 B loads per lane:
+//   block q, lane k (slab k): 32 B = 8 dwords; dword d, nibble n belongs to
+//   row 64q + 8d + n; its bit b is set iff a record's last byte lies in block b
+//   of slab k, i.e. in row bytes [64k + 16b, 64k + 16b + 16).  A 16 B block
+//   holds at most one record end: records are at least 16 B (a bare header).
+// The first record whose end lies past a row's start is row_first[row]
+// (k_row_index); record ids of the ends follow from it and a count over the
+// lanes, so the plan carries no ids.
 //
-// One wavefront per 64 rows (lane = row): the records ending in those rows
-// are a contiguous range, read 64 at a time (coalesced); each lane ORs its
-// record's cut into an LDS image of the 64 plan rows, then every lane writes
-// its row (64 B, header bits added): 4 KiB contiguous per wavefront.
+// One wavefront per block: the records ending in its rows are a contiguous
+// range, read 64 at a time (coalesced); each lane ORs its record's bit into
+// an LDS image of the block, then each lane writes its 32 B (2 KiB contiguous
+// per wavefront).
 constexpr int kPlanWaves = 4;
 
 __global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__restrict__ rec_off,
                                                               const uint4 *__restrict__ rec_hdr,
-                                                              const uint64_t *__restrict__ rng, uint64_t r0,
-                                                              uint64_t nr, const uint32_t *__restrict__ row_first,
-                                                              uint4 *__restrict__ plan,
-                                                              uint32_t *__restrict__ big_rows,
-                                                              uint32_t *__restrict__ big_cnt, uint32_t *big_any) {
-    __shared__ uint32_t cut_lds[kPlanWaves][64 * 17];  // row stride 17 words: conflict-free row reads
-    __shared__ uint32_t slow_lds[kPlanWaves][64];
+                                                              uint64_t r0, uint64_t nr,
+                                                              const uint32_t *__restrict__ row_first,
+                                                              uint4 *__restrict__ plan) {
+    __shared__ uint32_t cut_lds[kPlanWaves][64 * 9];  // lane stride 9 dwords: conflict-free row reads
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t R0 = r0 + ((uint64_t)blockIdx.x * kPlanWaves + wv) * 64, r1 = r0 + nr;
+    const uint64_t R0 = r0 + ((uint64_t)blockIdx.x * kPlanWaves + wv) * kBlockRows, r1 = r0 + nr;
     if (R0 >= r1) return;
     uint32_t *cw = cut_lds[wv];
-    for (uint32_t i = lane; i < 64 * 17; i += 64) cw[i] = 0;
-    slow_lds[wv][lane] = 0;
-    const uint64_t Re = min(R0 + 64, r1);  // rows [R0, Re)
-    const uint64_t R = R0 + lane;
-    const bool live = R < Re;
-    const uint32_t ra = live ? row_first[R] : 0u;
+    for (uint32_t i = lane; i < 64 * 9; i += 64) cw[i] = 0;
+    const uint64_t Re = min(R0 + kBlockRows, r1);           // rows [R0, Re)
     const uint64_t lo = row_first[R0], hi = row_first[Re];  // records ending in rows [R0, Re)
     for (uint64_t b = lo; b < hi; b += 64) {
         const uint64_t r = b + lane;
         if (r < hi) {
-            const uint64_t ve = value_end(rec_off, rec_hdr, r);
-            const uint32_t rl = (uint32_t)((ve - 1) / kRow - R0);  // 0..63
-            const uint32_t end = (uint32_t)(ve - (R0 + rl) * kRow), slab = (end - 1) >> 6;
-            atomicOr(cw + rl * 17 + (slab >> 2), (end - slab * kSlab) << (8 * (slab & 3)));
-            // the record before ends in the same slab (never for the range's
-            // first record: it ends in an earlier row)
-            if (r > lo && (value_end(rec_off, rec_hdr, r - 1) - 1) >> 6 == (ve - 1) >> 6) slow_lds[wv][rl] = 1;
+            const uint64_t last = value_end(rec_off, rec_hdr, r) - 1;  // the record's last byte
+            const uint32_t rl = (uint32_t)(last / kRow - R0);          // 0..63
+            const uint32_t o = (uint32_t)(last % kRow), slab = o / kSlab, blk = (o % kSlab) / kBlock;
+            atomicOr(cw + slab * 9 + rl / 8, (1u << blk) << (4 * (rl % 8)));
         }
     }
-    // header bits (ra) into the LDS image, then write the 64 rows out with
-    // each store instruction covering 1 KiB contiguous (a lane-per-row store
-    // would scatter 16 B pieces at a 64 B stride: partial-line writes)
-    const uint64_t H = ra;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {  // header bits live in bytes 0..31 (ra is 32 bits)
-        const uint32_t nib = (uint32_t)(H >> (4 * i)) & 15u;
-        cw[lane * 17 + i] |= ((nib & 1u) << 7) | ((nib & 2u) << 14) | ((nib & 4u) << 21) | ((nib & 8u) << 28);
-    }
-    uint4 *blk = plan + R0 * 4;  // the wavefront's rows as 16 B units
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t u = lane + 64 * k, rl = u >> 2, q = (u & 3) * 4;  // 16 B unit u: row rl, words q..q+3
-        if (R0 + rl < Re)
-            blk[u] = make_uint4(cw[rl * 17 + q], cw[rl * 17 + q + 1], cw[rl * 17 + q + 2], cw[rl * 17 + q + 3]);
-    }
-    // slow rows: compacted into this wavefront's 64 list slots, count per
-    // wavefront (no atomics: a global counter here serialises at one address)
-    const bool slow = live && slow_lds[wv][lane];
-    const uint64_t sm = __ballot(slow);
-    const uint32_t w = (uint32_t)((R0 - r0) >> 6);
-    if (slow) big_rows[(uint64_t)w * 64 + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u))] = (uint32_t)R;
-    if (lane == 0) {
-        big_cnt[w] = (uint32_t)__popcll(sm);
-        if (sm) *big_any = 1u;
-    }
+    // the launch's plan counts blocks from its first row r0
+    uint4 *dst = plan + ((R0 - r0) / kBlockRows) * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
+    dst[0] = make_uint4(cw[lane * 9], cw[lane * 9 + 1], cw[lane * 9 + 2], cw[lane * 9 + 3]);
+    dst[1] = make_uint4(cw[lane * 9 + 4], cw[lane * 9 + 5], cw[lane * 9 + 6], cw[lane * 9 + 7]);
 }
 
 // LDS image of the slicing-by-4 tables: two 64 KiB regions; in region r,
@@ -644,23 +612,25 @@ template <int K>
 __device__ __forceinline__ uint32_t tbl_addr(uint32_t c, uint32_t lb) {
     return __builtin_amdgcn_perm(c, lb, 0x0C020000u | ((4u + K) << 8));
 }
-// crc' = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3] for c = crc ^ word.
-__device__ __forceinline__ uint32_t slice4(const uint32_t *lds, uint32_t lb0, uint32_t lb1, uint32_t c) {
-    return lds_at(lds, tbl_addr<0>(c, lb0)) ^ lds_at(lds, tbl_addr<1>(c, lb0) + 128) ^
-           lds_at(lds, tbl_addr<2>(c, lb1)) ^ lds_at(lds, tbl_addr<3>(c, lb1) + 128);
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
-// One byte through T0: crc' = T0[(crc ^ b) & 0xFF] ^ crc >> 8.
-__device__ __forceinline__ uint32_t byte1(const uint32_t *lds, uint32_t lb1, uint32_t crc, uint32_t b) {
-    return lds_at(lds, tbl_addr<0>(crc ^ b, lb1) + 128) ^ (crc >> 8);
+// One slicing-by-4 step on a = crc ^ word, with the next word x folded in:
+// T3[a0] ^ T2[a1] ^ T1[a2] ^ T0[a3] ^ x.  4 v_perm + 4 ds_read + 2 v_bitop3.
+__device__ __forceinline__ uint32_t slice4x(const uint32_t *lds, uint32_t lb0, uint32_t lb1, uint32_t a,
+                                            uint32_t x) {
+    return xor3(xor3(lds_at(lds, tbl_addr<0>(a, lb0)), lds_at(lds, tbl_addr<1>(a, lb0) + 128),
+                     lds_at(lds, tbl_addr<2>(a, lb1))),
+                lds_at(lds, tbl_addr<3>(a, lb1) + 128), x);
 }
-
 
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xF, false);
 }
 
-// LDS image of the CRC tables (identical in every k_crc_rows* workgroup).
+// LDS image of the CRC tables (identical in every k_crc_rows workgroup).
 __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__restrict__ g_slice,
                                              const uint32_t *__restrict__ g_nib) {
     for (uint32_t i = threadIdx.x; i < 32768; i += blockDim.x)
@@ -672,453 +642,280 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
     __syncthreads();
 }
 
-// Per-lane state of one row (see k_crc_rows).
-struct RowCuts {
-    int ncut = 0;
-    int32_t c0 = 99, c1 = 99, c2 = 99, c3 = 99;  // record end offsets inside the slab (1..64); named
-    uint32_t id0 = 0, id1 = 0, id2 = 0, id3 = 0;  // registers, never an indexed array (no scratch)
-    uint32_t n_le = 0;                             // record ends at or before the slab end
-    int32_t my_end = 0;                            // row-relative end of record ra + lane
-    __device__ __forceinline__ void take(uint32_t end, uint32_t j, uint32_t ra, uint32_t lane, int32_t s_rel) {
-        const int32_t cc = (int32_t)end - s_rel;
-        if (cc > 0 && cc <= kSlab) {
-            const uint32_t id = ra + j;
-            c0 = ncut == 0 ? cc : c0;
-            c1 = ncut == 1 ? cc : c1;
-            c2 = ncut == 2 ? cc : c2;
-            c3 = ncut == 3 ? cc : c3;
-            id0 = ncut == 0 ? id : id0;
-            id1 = ncut == 1 ? id : id1;
-            id2 = ncut == 2 ? id : id2;
-            id3 = ncut == 3 ? id : id3;
-            ++ncut;
-        }
-        n_le += (int32_t)end <= s_rel + kSlab ? 1u : 0u;
-        my_end = lane == j ? (int32_t)end : my_end;
-    }
-};
-
-struct RowOut {
-    uint32_t e[4] = {0, 0, 0, 0};  // register at each record end in the slab
-    uint32_t pre_first = 0;         // run just before the first record end of the slab
-    uint32_t rend = 0;              // (lane 63) run open at the row end
-};
-
-// Z_{64(63-lane)}(z) (the open register referenced to the row end, 8 nibble
-// lookups in the lane's LDS table), then a segmented inclusive XOR over the
-// wave: lanes whose open register belongs to the same record t form a run.
-// runv = run value up to this lane, runprev = the previous lane's, tprev = its t.
-__device__ __forceinline__ void wave_runs(const uint32_t *lds, uint32_t lane, uint32_t nbase, uint32_t z,
-                                          uint32_t t, uint32_t &runv, uint32_t &runprev, uint32_t &tprev) {
-    // Z_{64(63-lane)}(z): reference the open register to the row end
-    uint32_t cz = 0;
-#pragma unroll
-    for (int qn = 0; qn < 8; ++qn) cz ^= lds[nbase + qn * 512 + (((z >> (4 * qn)) & 15u) << 5)];
-    // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
-    uint32_t P = cz;
-    P ^= dpp<0x111, 0xF>(P);  // row_shr:1
-    P ^= dpp<0x112, 0xF>(P);  // row_shr:2
-    P ^= dpp<0x114, 0xF>(P);  // row_shr:4
-    P ^= dpp<0x118, 0xF>(P);  // row_shr:8
-    P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
-    P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
-    tprev = (uint32_t)__builtin_amdgcn_update_dpp((int)kNone32, (int)t, 0x138, 0xF, 0xF, false);
-    const bool start = lane == 0 || t != tprev;
-    const uint64_t B = __ballot(start);
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    const int rsl = 63 - __clzll((long long)(B & upto));
-    const uint32_t Pp = __shfl(P, rsl > 0 ? rsl - 1 : 0);
-    runv = P ^ (rsl > 0 ? Pp : 0u);
-    runprev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)runv, 0x138, 0xF, 0xF, false);
-}
-
-// The per-row work of k_crc_rows: every byte of the slab enters the CRC
-// register; it is closed at each record end (exactly: the last partial word
-// byte-wise), the open register at the slab end is shifted to the row end and
-// a segmented XOR over the wave joins each record's lanes.
-template <int MODE>
-__device__ __forceinline__ RowOut crc_row(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1, uint32_t nbase,
-                                          int32_t s_rel, uint64_t rs, uint32_t (&words)[16], const RowCuts &rc,
-                                          uint32_t t) {
-    RowOut o;
-    int q = 0;
-    int32_t cc = rc.c0, n1 = rc.c1, n2 = rc.c2, n3 = rc.c3;  // pending cuts, shifted down at each cut
-    int32_t cj = (cc - 1) >> 2;  // word holding the record's last byte (99 -> never)
-    uint32_t crc = 0;
-    if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded row
-#pragma unroll
-        for (int j = 0; j < 16; ++j) words[j] = (uint32_t)(rs >> 4) * 2654435761u + lane * 97u + j;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t x = words[j];
-        uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
-                                 : slice4(lds, lb0, lb1, crc ^ x);
-        if (j == cj) {
-            const int nb = cc - 4 * j;
-            if (nb < 4) {
-                nc = crc;
-                uint32_t y = x;
-                for (int b = 0; b < nb; ++b) {
-                    nc = byte1(lds, lb1, nc, y);
-                    y >>= 8;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) o.e[k] = q == k ? nc : o.e[k];
-            nc = 0;
-            ++q;
-            cc = n1;
-            n1 = n2;
-            n2 = n3;
-            n3 = 99;
-            cj = (cc - 1) >> 2;
-        }
-        crc = nc;
-    }
-    const uint32_t z = t != kNone32 ? crc : 0u;
-    o.rend = crc ^ t;
-    if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
-        asm volatile("" ::"v"(crc), "v"(z));
-    } else {
-        uint32_t runv, runprev, tprev;
-        wave_runs(lds, lane, nbase, z, t, runv, runprev, tprev);
-        o.rend = t != kNone32 ? runv : 0u;
-        // the first record closing in this slab continues the run of the lane before
-        o.pre_first = (rc.ncut > 0 && lane > 0 && tprev == rc.id0) ? runprev : 0u;
-    }
-    return o;
-}
-
-struct RowOut1 {
-    uint32_t e = 0;    // register at the record end in the slab
-    uint32_t pre = 0;  // run of the lanes before, for the record ending in the slab
-    uint32_t rend = 0; // run open at the slab end, referenced to the row end (lane 63: the row's)
-};
-
-// The per-row work of k_crc_rows for rows with at most one record end per
-// slab: every byte of the slab enters the CRC register; it is closed at the
-// record end cc (the last partial word byte-wise), the open register at the
-// slab end is shifted to the row end and a segmented XOR over the wave joins
-// each record's lanes.
-template <int MODE>
-__device__ __forceinline__ RowOut1 crc_row1(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1,
-                                            uint32_t nbase, uint64_t rs, uint32_t (&words)[16], int32_t cc,
-                                            uint32_t my_id, uint32_t t) {
-    RowOut1 o;
-    const int32_t cj = cc ? (cc - 1) >> 2 : 99;  // word holding the record's last byte
-    uint32_t crc = 0;
-    if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded row
-#pragma unroll
-        for (int j = 0; j < 16; ++j) words[j] = (uint32_t)(rs >> 4) * 2654435761u + lane * 97u + j;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t x = words[j];
-        uint32_t nc = (MODE & 2) ? __builtin_amdgcn_alignbit(crc ^ x, crc ^ x, 5) + 0x9E3779B9u
-                                 : slice4(lds, lb0, lb1, crc ^ x);
-        if (j == cj) {
-            const int nb = cc - 4 * j;
-            if (nb < 4) {
-                nc = crc;
-                uint32_t y = x;
-                for (int b = 0; b < nb; ++b) {
-                    nc = byte1(lds, lb1, nc, y);
-                    y >>= 8;
-                }
-            }
-            o.e = nc;
-            nc = 0;
-        }
-        crc = nc;
-    }
-    const uint32_t z = t != kNone32 ? crc : 0u;
-    o.rend = crc ^ t;
-    if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
-        asm volatile("" ::"v"(crc), "v"(z));
-    } else {
-        uint32_t runv, runprev, tprev;
-        wave_runs(lds, lane, nbase, z, t, runv, runprev, tprev);
-        o.rend = t != kNone32 ? runv : 0u;
-        // the record closing in this slab continues the run of the lane before
-        o.pre = (cc && lane > 0 && tprev == my_id) ? runprev : 0u;
-    }
-    return o;
-}
-
-// NR rows of one wavefront at once (k_crc_rows): the NR CRC chains of a lane
-// are independent, so their LDS lookups interleave and each wave keeps NR
-// table reads in flight per step of the chain (ILP against LDS latency).  Per
-// row exactly crc_row1's arithmetic.
+// The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns slab k =
+// bytes [64k, 64k+64).  Branch-free: every lane runs one CRC register from 0
+// over its 16 words (slicing-by-4, LDS tables) and keeps the register at each
+// 16 B block start (c1, c2, c3 after words 3, 7, 11; c0 = 0) and at the slab
+// end, G = F(0, slab).  Record boundaries never enter the arithmetic:
+//   - G is referenced to the row end, Z_{64(63-k)}(G) (8 nibble lookups in the
+//     lane's LDS table), and an inclusive prefix XOR over the wave (DPP) gives
+//     rrow = F(0, row) (lane 63) and, per lane, pre = the exclusive prefix =
+//     the slabs before k referenced to the row end;
+//   - per record end (plan: block b of slab k) the lane stores (c_b, pre) at
+//     the record's slot; k_finalize continues c_b over the <= 16 bytes of the
+//     block up to the record end and stitches rows (see there).
+// Outputs: out_ep (c, pre) per record, out_rend per row (rrow).
+//
+// Work: blocks of 64 consecutive rows from an atomic queue (late-starting or
+// slow wavefronts simply take fewer blocks), NR rows per step.  Per block a
+// lane loads its 32 plan bytes and row_first of one row (3 loads, issued a
+// block ahead) and the block's 64 rrow values leave in one coalesced store,
+// so per row the vector-memory queue holds only the 4 x 16 B row loads and
+// one 8 B (c, pre) store.  Rows are local to the launch: arena, plan,
+// row_first and out_rend point at its first row; n_total is the record-slot
+// scratch base (64 slots per wavefront), rend_scratch 64 row slots.
+//
+// Memory pipeline: the row data are buffer loads (row base in a scalar
+// resource, lane offset in a fixed VGPR) issued one step ahead.  No scalar
+// loads in the loop: an outstanding SMEM load would make every LDS wait
+// (lgkmcnt(0)) wait for HBM too.  Every lane stores on every path (lanes
+// without a record end to their scratch slot), so the compiler's vmcnt waits
+// count the same stores on every path and stay a step behind the loads.
+//
+// MODE (ablation, gck_diag_crc_variant): 2 = no LDS table chain, 4 = no row
+// shift / wave scan, 8 = synthetic bytes instead of loads, 16 = no (c, pre)
+// stores.
 template <int MODE, int NR>
-__device__ __forceinline__ void crc_rowsN(const uint32_t *lds, uint32_t lane, uint32_t lb0, uint32_t lb1,
-                                          uint32_t nbase, const uint64_t (&rs)[NR], uint32_t (&words)[NR][16],
-                                          const int32_t (&cc)[NR], const uint32_t (&my_id)[NR],
-                                          const uint32_t (&t)[NR], RowOut1 (&o)[NR]) {
-    int32_t cj[NR];
-    uint32_t crc[NR];
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        cj[i] = cc[i] ? (cc[i] - 1) >> 2 : 99;
-        crc[i] = 0;
-        o[i] = RowOut1{};
-        if constexpr ((MODE & 8) != 0) {  // ablation: synthetic bytes instead of the loaded rows
-#pragma unroll
-            for (int j = 0; j < 16; ++j) words[i][j] = (uint32_t)(rs[i] >> 4) * 2654435761u + lane * 97u + j;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        uint32_t nc[NR];
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-            nc[i] = (MODE & 2) ? __builtin_amdgcn_alignbit(crc[i] ^ words[i][j], crc[i] ^ words[i][j], 5) + 0x9E3779B9u
-                               : slice4(lds, lb0, lb1, crc[i] ^ words[i][j]);
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            if (j == cj[i]) {
-                const int nb = cc[i] - 4 * j;
-                if (nb < 4) {
-                    uint32_t x = crc[i], y = words[i][j];
-                    for (int b = 0; b < nb; ++b) {
-                        x = byte1(lds, lb1, x, y);
-                        y >>= 8;
-                    }
-                    nc[i] = x;
-                }
-                o[i].e = nc[i];
-                nc[i] = 0;
-            }
-            crc[i] = nc[i];
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const uint32_t z = t[i] != kNone32 ? crc[i] : 0u;
-        o[i].rend = crc[i] ^ t[i];
-        if constexpr ((MODE & 4) != 0) {  // ablation: no tail shift / segmented scan
-            asm volatile("" ::"v"(crc[i]), "v"(z));
-        } else {
-            uint32_t runv, runprev, tprev;
-            wave_runs(lds, lane, nbase, z, t[i], runv, runprev, tprev);
-            o[i].rend = t[i] != kNone32 ? runv : 0u;
-            o[i].pre = (cc[i] && lane > 0 && tprev == my_id[i]) ? runprev : 0u;
-        }
-    }
-}
-
-
-// The HBM-bound kernel.  A wavefront owns a 4 KiB row; lane k owns bytes
-// [64k, 64k+64).  Every byte enters a CRC register, no masking: records tile
-// the file, so lane k's register simply runs over whole records and is closed
-// exactly at every record end and restarted at the next word.  The chain of
-// record r therefore covers [align4(start_r), end_r) = header/key prefix ||
-// value; k_finalize removes the prefix by linearity.  An open register at the
-// slab end belongs to the record containing that position; it is referenced to
-// the row end with the per-lane constant shift Z_{64(63-k)} (8 nibble lookups)
-// and a segmented XOR over the wave (DPP prefix scan) joins each record's
-// lanes.  Outputs: per record e (the register at its end) and pre (the run of
-// the lanes before its closing slab), stored by the lane whose slab holds the
-// record end (slot ra + mbcnt of the cut ballot); per row the run open at the
-// row end.  A slab holds at most one record end here; rows where one holds
-// more (records under 64 B) are flagged by k_row_plan and done by
-// k_crc_rows_big (their stores here go to the scratch slots).
-//
-// Rows are local to the launch: arena, plan and out_rend point at its first
-// row; n_total is the e/pre scratch slot, rend_scratch the rend one.
-//
-// Memory pipeline: the row data (4 x 16 B per lane) and the row plan byte are
-// buffer loads (row base in a scalar resource, lane offset in a fixed VGPR)
-// issued DEPTH rows ahead.  No scalar loads in the loop: an outstanding SMEM
-// load would make every LDS wait (lgkmcnt(0)) wait for HBM too.  Control flow
-// around the stores is uniform and their number fixed, so the compiler's vmcnt
-// waits land rows after the loads they wait for.
-template <int MODE, int DEPTH, int NR>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint8_t *__restrict__ plan, uint64_t n_total,
+                                                   const uint4 *__restrict__ plan,
+                                                   const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
-                                                   const uint32_t *__restrict__ g_nib,
-                                                   uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
-                                                   uint32_t *__restrict__ out_rend, uint32_t *__restrict__ rend_scratch) {
+                                                   const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
+                                                   uint32_t *__restrict__ out_rend,
+                                                   uint32_t *__restrict__ rend_scratch,
+                                                   uint32_t *__restrict__ queue) {
+    static_assert(kBlockRows % (4 * NR) == 0, "a block is whole quads of steps");
+    constexpr int kSteps = kBlockRows / NR;  // steps per block
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
-    const int32_t s_rel = (int32_t)lane * kSlab;
-    // a step is NR consecutive rows; steps are strided over the wavefronts
-    const uint64_t n_steps = (n_rows + NR - 1) / NR;
-    const uint64_t stride = (uint64_t)gridDim.x * kWaves;
+    const uint32_t s_rel = lane * kSlab;
+    const uint64_t n_blocks = (n_rows + kBlockRows - 1) / kBlockRows;
+    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    const uint64_t scratch = n_total + (uint64_t)(wid & 255) * 64 + lane;  // this lane's scratch slot
 
-    uint64_t step = __builtin_amdgcn_readfirstlane((uint32_t)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    if (step >= n_steps) return;
+    auto grab = [&]() -> uint32_t {  // next block index from the queue
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(queue, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    struct Plan {
+        uint4 a, b;  // the lane's 64 row nibbles
+        uint32_t ra; // row_first of row lane
+    };
+    auto load_plan = [&](uint64_t q, Plan &p) {
+        const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
+        const uint4 *src = plan + qc * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
+        p.a = src[0];
+        p.b = src[1];
+        p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
+    };
     struct RowBuf {
         u32x4 x[4];
-        uint32_t pv;
     };
-    auto issue = [&](uint64_t st, RowBuf (&bs)[NR]) {
+    auto issue = [&](uint64_t row0, RowBuf (&bs)[NR]) {
         if constexpr ((MODE & 8) != 0) return;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            // buffer loads: the row base lives in a scalar resource, the lane
-            // offset in one VGPR that never changes (no per-load VGPR address)
-            const uint64_t r = min(st * NR + i, n_rows - 1);
+            const uint64_t r = min(row0 + i, n_rows - 1);
             const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
-            const __amdgpu_buffer_rsrc_t rplan = make_rsrc(plan + r * kPlanBytes, kPlanBytes);
-            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel, 0, 0);
-            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 16, 0, 0);
-            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 32, 0, 0);
-            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, (uint32_t)s_rel + 48, 0, 0);
-            bs[i].pv = __builtin_amdgcn_raw_buffer_load_b8(rplan, lane, 0, 0);
+            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel, 0, 0);
+            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 16, 0, 0);
+            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 32, 0, 0);
+            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 48, 0, 0);
         }
     };
-    auto process = [&](uint64_t st, const RowBuf (&bs)[NR]) {
-        uint64_t rs[NR], row[NR];
-        int32_t cc[NR];
-        uint32_t ra[NR], idx[NR], my_id[NR], t[NR];
-        uint32_t words[NR][16];
+    // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
+    // nib holds their plan nibbles from bit 0 up
+    auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t ra_reg, const RowBuf (&bs)[NR],
+                       uint32_t &rend_buf) {
+        uint32_t w[NR][16];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            row[i] = st * NR + i;
-            rs[i] = row[i] * kRow;
-            // row header from bit 7 of the 64 plan bytes, the cut of this slab from bits 0..6
-            const uint64_t H = __ballot(bs[i].pv & 0x80u);
-            ra[i] = (uint32_t)H;
-
-            cc[i] = (MODE & 1) ? 0 : (int32_t)(bs[i].pv & 0x7Fu);
-            const uint64_t C = __ballot(cc[i] != 0);
-            idx[i] = __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-            const uint32_t n_le = idx[i] + (cc[i] != 0);  // record ends at or before the slab end
-            // the record open at the slab end: the next one after the ends
-            // counted.  (Past a file's last record the slab is padding and
-            // "record" t is the next file's first one or none: the padding only
-            // reaches this row's rend, which no record reads, since records
-            // never cross files and files start on row boundaries.)
-            t[i] = ra[i] + n_le;
-            my_id[i] = ra[i] + idx[i];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                words[i][4 * k] = bs[i].x[k].x;
-                words[i][4 * k + 1] = bs[i].x[k].y;
-                words[i][4 * k + 2] = bs[i].x[k].z;
-                words[i][4 * k + 3] = bs[i].x[k].w;
+                w[i][4 * k] = bs[i].x[k].x;
+                w[i][4 * k + 1] = bs[i].x[k].y;
+                w[i][4 * k + 2] = bs[i].x[k].z;
+                w[i][4 * k + 3] = bs[i].x[k].w;
+            }
+            if constexpr ((MODE & 8) != 0) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) w[i][j] = (uint32_t)(row0 + i) * 2654435761u + lane * 97u + j;
             }
         }
-        RowOut1 o[NR];
-        crc_rowsN<MODE, NR>(lds, lane, lb0, lb1, nbase, rs, words, cc, my_id, t, o);
+        // NR independent chains interleaved: NR table reads in flight per step
+        uint32_t a[NR], c1[NR], c2[NR], c3[NR], G[NR];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) a[i] = w[i][0];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const uint32_t nx = j < 15 ? w[i][j < 15 ? j + 1 : 15] : 0u;
+                if constexpr ((MODE & 2) != 0) {
+                    a[i] = (__builtin_amdgcn_alignbit(a[i], a[i], 5) + 0x9E3779B9u) ^ nx;
+                    if (j == 3) c1[i] = a[i];
+                    if (j == 7) c2[i] = a[i];
+                    if (j == 11) c3[i] = a[i];
+                    if (j == 15) G[i] = a[i];
+                } else if (j == 15) {
+                    G[i] = slice4x(lds, lb0, lb1, a[i], 0u);
+                } else if ((j & 3) == 3) {
+                    const uint32_t c = slice4x(lds, lb0, lb1, a[i], 0u);
+                    if (j == 3) c1[i] = c;
+                    if (j == 7) c2[i] = c;
+                    if (j == 11) c3[i] = c;
+                    a[i] = c ^ nx;
+                } else {
+                    a[i] = slice4x(lds, lb0, lb1, a[i], nx);
+                }
+            }
+        }
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            // every lane stores: the cut lanes to their record's slot, the rest
-            // (and rows past the end) to the scratch slots (no branch around a
-            // store).  A row where a slab holds 2+ record ends gets cuts OR'ed
-            // together here; k_crc_rows_big then rewrites all its outputs.
-            const bool dead = row[i] >= n_rows;
-            const uint64_t slot = (cc[i] != 0 && !dead) ? (uint64_t)ra[i] + idx[i] : n_total;
-            out_e[slot] = o[i].e;
-            out_pre[slot] = o[i].pre;
-            *(dead ? rend_scratch : out_rend + row[i]) = (uint32_t)__builtin_amdgcn_readlane((int)o[i].rend, 63);
+            const uint64_t row = row0 + i;
+            const uint32_t j = j0 + i;
+            // Z_{64(63-lane)}(G): the slab referenced to the row end
+            uint32_t pre = 0, rrow = G[i];
+            if constexpr ((MODE & 4) == 0) {
+                uint32_t t[8];
+#pragma unroll
+                for (int qn = 0; qn < 8; ++qn) t[qn] = lds[nbase + qn * 512 + (((G[i] >> (4 * qn)) & 15u) << 5)];
+                // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
+                uint32_t P = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+                P ^= dpp<0x111, 0xF>(P);  // row_shr:1
+                P ^= dpp<0x112, 0xF>(P);  // row_shr:2
+                P ^= dpp<0x114, 0xF>(P);  // row_shr:4
+                P ^= dpp<0x118, 0xF>(P);  // row_shr:8
+                P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
+                P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
+                pre = dpp<0x138, 0xF>(P);  // wave_shr:1 -> exclusive (lane 0: 0)
+                rrow = P;
+            }
+            // blocks of this slab holding a record end (0 past the last row)
+            const uint32_t m = row < n_rows ? (nib >> (4 * i)) & 15u : 0u;
+            const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
+            // the register at the start of block b (selects, no branches)
+            auto cap = [&](uint32_t b) {
+                uint32_t v = b == 3 ? c3[i] : c2[i];
+                v = b == 1 ? c1[i] : v;
+                return b == 0 ? 0u : v;
+            };
+            if constexpr ((MODE & 16) != 0) {
+                asm volatile("" ::"v"(m), "v"(pre), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
+            } else if (__ballot(m & (m - 1)) == 0) {
+                // common case: at most one record end per slab, its slot is
+                // ra + (cut lanes before)
+                const uint64_t C = __ballot(m != 0);
+                const uint32_t idx =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
+                out_ep[m ? (uint64_t)ra + idx : scratch] = make_uint2(cap((uint32_t)__builtin_ctz(m | 16u)), pre);
+            } else {
+                // a slab with 2..4 record ends (records under 64 B): ids by
+                // an exclusive count over the lanes, four stores per lane
+                const uint32_t n = __builtin_popcount(m);
+                const uint32_t ex = wave_incl_sum(n) - n;
+                uint32_t mm = m;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    out_ep[q < n ? (uint64_t)ra + ex + q : scratch] =
+                        make_uint2(cap((uint32_t)__builtin_ctz(mm | 16u)), pre);
+                    mm &= mm - 1;
+                }
+            }
+            rend_buf = lane == j ? (uint32_t)__builtin_amdgcn_readlane((int)rrow, 63) : rend_buf;
         }
     };
-    // DEPTH steps in flight while one is processed; the loop is unrolled over
-    // the DEPTH+1 buffer sets so each has fixed registers (a rotating copy
-    // would force a wait on loads still in flight).
-    RowBuf buf[DEPTH + 1][NR] = {};
-#pragma unroll
-    for (int i = 0; i < DEPTH; ++i) {
-        issue(step + i * stride, buf[i]);
-        // the stores of a processed step, to the scratch slots: the loop is
-        // entered with the same vector-memory queue shape as its back edge, so
-        // the compiler's waits at the loop head are as late as in the body
-#pragma unroll
-        for (int k = 0; k < NR; ++k) {
-            out_e[n_total] = 0;
-            out_pre[n_total] = 0;
-            *rend_scratch = 0;
-        }
-    }
+
+    // prologue: this wave's first two blocks, the first plan
+    uint64_t q = grab();
+    if (q >= n_blocks) return;
+    uint64_t qn = grab();
+    Plan pc, pn;
+    load_plan(q, pc);
+    RowBuf buf[2][NR];
+    issue(q * kBlockRows, buf[0]);
     for (;;) {
+        // block q: plan pc is resident; fetch the next block's plan and claim
+        // the one after it (both land during this block)
+        load_plan(qn, pn);
+        const uint64_t qnn = grab();
+        const uint64_t row_b = q * kBlockRows;
+        uint32_t rend_buf = 0;
+        const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
+        // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
+        // lane; the two row buffers alternate, so each has fixed registers
+        for (int qd = 0; qd < kSteps / 4; ++qd) {
+            // this quad's nibbles (a uniform select: qd is a loop counter)
+            uint32_t nib = nibs[0];
 #pragma unroll
-        for (int i = 0; i <= DEPTH; ++i) {
-            issue(step + DEPTH * stride, buf[(i + DEPTH) % (DEPTH + 1)]);
-            process(step, buf[i]);
-            step += stride;
-            if (step >= n_steps) return;
+            for (int d = 1; d < 8; ++d)
+                if (qd * NR / 2 == d) nib = nibs[d];
+            if constexpr (NR == 1) nib >>= 16 * (qd & 1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int st = qd * 4 + u;
+                // the next step's rows: this block, or the next block's first
+                const uint64_t nrow = st + 1 < kSteps ? row_b + (uint64_t)(st + 1) * NR : qn * kBlockRows;
+                issue(nrow, buf[(u + 1) & 1]);
+                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u & 1],
+                        rend_buf);
+            }
         }
+        // the block's 64 rrow values, one coalesced store (rows past the end
+        // to the scratch slots)
+        *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
+        if (qn >= n_blocks) return;
+        q = qn;
+        qn = qnn;
+        pc = pn;
     }
 }
 
-// Rows where a slab holds 2+ record ends (records shorter than 64 B): one
-// wavefront per listed row, record ends read from the record table, direct
-// stores; up to 4 ends per slab (a record is at least 16 B).
-template <int MODE>
-__global__ __launch_bounds__(1024) void k_crc_rows_big(const uint8_t *__restrict__ arena,
-                                                       const uint32_t *__restrict__ big_rows,
-                                                       const uint32_t *__restrict__ big_cnt,
-                                                       const uint32_t *__restrict__ big_any, uint32_t n_lists,
-                                                       const uint32_t *__restrict__ row_first,
-                                                       const uint64_t *__restrict__ rng,
-                                                       const uint64_t *__restrict__ rec_off,
-                                                       const uint4 *__restrict__ rec_hdr,
-                                                       const uint32_t *__restrict__ g_slice,
-                                                       const uint32_t *__restrict__ g_nib,
-                                                       uint32_t *__restrict__ out_e, uint32_t *__restrict__ out_pre,
-                                                       uint32_t *__restrict__ out_rend) {
-    if (*big_any == 0) return;
-    const uint64_t n_total = rng[1];
-    __shared__ uint32_t lds[40960];
-    fill_crc_lds(lds, g_slice, g_nib);
-    const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
-    const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
-    const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
-    const int32_t s_rel = (int32_t)lane * kSlab;
-    // list w holds big_cnt[w] rows at big_rows[64 w ..] (k_row_plan)
-    uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6)), i = 0;
-    for (;;) {
-        while (w < n_lists && i >= big_cnt[w]) {
-            w += gridDim.x * kWaves;
-            i = 0;
-        }
-        if (w >= n_lists) break;
-        const uint64_t row = big_rows[(uint64_t)w * 64 + i++], rs = row * kRow;
-        const uint32_t ra = row_first[row], rb = row_first[row + 1], n_ends = rb - ra;
-
-        RowCuts rc;
-        for (uint32_t j0 = 0; j0 < n_ends; j0 += 64) {
-            const uint32_t cnt = min(64u, n_ends - j0);
-            const uint64_t r = min((uint64_t)ra + j0 + min(lane, cnt - 1), n_total - 1);
-            const int32_t e_ = (int32_t)(value_end(rec_off, rec_hdr, r) - rs);
-            for (uint32_t j = 0; j < cnt; ++j) rc.take((uint32_t)__builtin_amdgcn_readlane(e_, j), j0 + j, ra, lane, s_rel);
-        }
-        const uint32_t t = ra + rc.n_le;  // see k_crc_rows
-        const uint4 *src = reinterpret_cast<const uint4 *>(arena + rs + s_rel);
-        uint32_t words[16];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const uint4 v = src[k];
-            words[4 * k] = v.x;
-            words[4 * k + 1] = v.y;
-            words[4 * k + 2] = v.z;
-            words[4 * k + 3] = v.w;
-        }
-        const RowOut o = crc_row<MODE>(lds, lane, lb0, lb1, nbase, s_rel, rs, words, rc, t);
-        if (rc.ncut > 0) out_e[rc.id0] = o.e[0], out_pre[rc.id0] = o.pre_first;
-        if (rc.ncut > 1) out_e[rc.id1] = o.e[1], out_pre[rc.id1] = 0u;
-        if (rc.ncut > 2) out_e[rc.id2] = o.e[2], out_pre[rc.id2] = 0u;
-        if (rc.ncut > 3) out_e[rc.id3] = o.e[3], out_pre[rc.id3] = 0u;
-        if (lane == 63) out_rend[row] = o.rend;
-    }
-}
-
-// Per record (core/db.go:311 applied to every record):
-//   chain = F(0, [align4(start), end)) = e ^ Z_-(row_end-end)(stitched runs),
-//           runs stitched over rows by Horner with Z_4096 (LDS byte tables);
-//   F(0, value) = chain ^ Z_V(F(0, prefix)), prefix = header bytes from
-//           align4(start) plus the key (bytes the chain saw before the value);
-//   crc = F(0, value) ^ crc32(0^V)  (table for V < 2^17).
+// ---------------------------------------------------------------- finalize ---
+// Per record r = [rs, ve) (core/db.go:311 applied to every record).  Notation
+// as in gck_math.h; for a position p inside row R (row end E_R):
+//   A(p) = Z_{E_R - p}(F(0, [R*4096, p)))   the row's bytes before p, referenced to E_R.
+// k_crc_rows gives, for the record end ve in block [bs, bs+16) of slab k:
+//   c = F(0, [slab start, bs)),  pre = A(slab start),  so
+//   A(ve) = pre ^ Z_{E - ve}(ft),  ft = F(c, [bs, ve))  (<= 16 bytes, here);
+// and per row rrow = F(0, row).  Then, with fr / lr the rows of rs / ve - 1:
+//   acc = A(ve) ^ A(rs)                                  (fr == lr)
+//   acc = Horner_{Z_4096}(rrow[fr] ^ A(rs), rrow[fr+1..lr-1], A(ve))   (else)
+//   F(0, [rs, ve)) = Z_{-(E - ve)}(acc) = ft ^ Z_{-(E - ve)}(acc ^ Z_{E-ve}(ft))
+// (A(rs) = 0 when rs starts a row).  The header + key prefix is removed by
+// linearity: F(0, value) = F(0, [rs, ve)) ^ Z_V(F(0, [rs, vs))), and
+//   crc = F(0, value) ^ crc32(0^V).
+// ft of record r-1 uses the 16 B block just before rs, which record r's lane
+// reads next to its own header anyway: lane k computes it and hands it to
+// lane k-1 (DPP); a lane whose successor is not its neighbour (wave end, file
+// end, range end) reads its own end block.
 // ValuePos = lastOffset + 16 + KeySize mod 2^32 (core/keydir.go:25), with
 // lastOffset = carry + offset within the file.
 __device__ __forceinline__ uint32_t z4096(const uint32_t *Tz, uint32_t a) {
     return Tz[a & 0xFF] ^ Tz[256 + ((a >> 8) & 0xFF)] ^ Tz[512 + ((a >> 16) & 0xFF)] ^ Tz[768 + (a >> 24)];
+}
+// crc' = T3[b0] ^ T2[b1] ^ T1[b2] ^ T0[b3] for a = crc ^ word (T[k*256+b] = Tk[b])
+__device__ __forceinline__ uint32_t slice4t(const uint32_t *T, uint32_t a) {
+    return xor3(T[768 + (a & 0xFF)], T[512 + ((a >> 8) & 0xFF)], T[256 + ((a >> 16) & 0xFF)]) ^ T[a >> 24];
+}
+// F(c, the first nb (1..3) bytes of word y): (c >> 8nb) ^ slice4 of (c ^ y)
+// moved up by 4 - nb bytes (the moved-out bytes index T[0] = 0).
+__device__ __forceinline__ uint32_t partial_word(const uint32_t *T, uint32_t c, uint32_t y, uint32_t nb) {
+    return (c >> (8 * nb)) ^ slice4t(T, (c ^ y) << (32 - 8 * nb));
+}
+// F(c, bytes [0, L)) of the 16 B block v, L in [0, 16].
+__device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, const uint4 &v, uint32_t L) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (4u * i + 4 <= L) c = slice4t(T, c ^ w[i]);
+    const uint32_t nb = L & 3u, j = L >> 2;
+    if (nb) c = partial_word(T, c, j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3], nb);
+    return c;
 }
 
 __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ arena,
@@ -1127,10 +924,10 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
                                                   const uint32_t *__restrict__ rec_file,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint32_t *__restrict__ carry, const uint64_t *__restrict__ rng,
-                                                  const uint32_t *__restrict__ e, const uint32_t *__restrict__ pre,
-                                                  const uint32_t *__restrict__ rend,
+                                                  const uint2 *__restrict__ ep, const uint32_t *__restrict__ rend,
                                                   const uint32_t *__restrict__ g_slice,
-                                                  const uint32_t *__restrict__ xinv, const uint32_t *__restrict__ zrow,
+                                                  const uint32_t *__restrict__ xinv, const uint32_t *__restrict__ xfw,
+                                                  const uint32_t *__restrict__ zrow,
                                                   const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
@@ -1141,88 +938,98 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         T[i] = g_slice[i];
     }
     __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
-    // software-pipelined over the grid-stride loop: the next record's table
-    // entries are in flight while this one is finished
-    struct RecIn {
-        uint64_t start;
-        uint4 h;
-        uint32_t f, e, pre;
-    };
-    auto fetch = [&](uint64_t r) {
-        RecIn x;
-        x.start = rec_off[r];
-        x.h = rec_hdr[r];
-        x.f = rec_file[r];
-        x.e = e[r];
-        x.pre = pre[r];
-        return x;
-    };
-    uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
-    RecIn cur{};
-    if (r < re) cur = fetch(r);
-    for (; r < re; r += G) {
-        const RecIn nxt = fetch(min(r + G, re - 1));
-        const uint64_t start = cur.start;
-        const uint4 h = cur.h;
-        const uint32_t f = cur.f;
+    // wave-uniform loop: the 64 lanes hold 64 consecutive records
+    for (uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < re; base += G) {
+        const uint64_t r_ = base + lane;
+        const bool valid = r_ < re;
+        const uint64_t r = valid ? r_ : re - 1;
+        const uint64_t rs = rec_off[r];
+        const uint4 h = rec_hdr[r];
+        const uint32_t f = rec_file[r];
         const uint32_t V = h.w;
-        const uint64_t vs = start + 16 + h.z, ve = vs + V;
-        const uint64_t w0 = (start + 3) & ~3ull;
-        const uint64_t fr = w0 / kRow, lr = (ve - 1) / kRow;
-        const uint64_t row_end = (lr + 1) * kRow;
-        // independent loads first: the tables for the shifts, the prefix words
-        const uint32_t xinv_d = xinv[row_end - ve];
-        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
-        const uint32_t zv = V < (1u << 17) ? zl[V] : 0u;
-        const uint32_t L = (uint32_t)(vs - w0);
+        const uint64_t vs = rs + 16 + h.z, ve = vs + V;
+        // ft of the previous record (same file: its end is rs), from the 16 B
+        // block holding byte rs - 1
+        const bool prev_same = rs != fbase[f];
+        const uint64_t bsp = prev_same ? (rs - 1) & ~15ull : rs;
+        const uint4 vp = *reinterpret_cast<const uint4 *>(arena + bsp);
+        const uint2 ep_prev = prev_same ? ep[r - 1] : make_uint2(0u, 0u);
+        const uint32_t e_prev = ep_prev.x, pre_prev = ep_prev.y;
+        const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
+        // A(rs) (0 when rs starts a row)
+        const uint32_t dp = (uint32_t)(((rs + kRow - 1) & ~(uint64_t)(kRow - 1)) - rs);
+        const uint32_t a_rs = (prev_same && dp) ? pre_prev ^ (ft_prev ? multmodp(xfw[dp], ft_prev) : 0u) : 0u;
+        // ft of this record: from lane + 1 if that lane holds record r + 1 of the same file
+        const uint64_t nb_same = __ballot(valid && prev_same);
+        const uint32_t ft_next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ft_prev, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const bool have = lane < 63 && ((nb_same >> (lane + 1)) & 1);
+        const uint2 ep_own = ep[r];
+        uint32_t ft = ft_next;
+        if (!have) {
+            const uint64_t bse = (ve - 1) & ~15ull;
+            ft = crc_block(T, ep_own.x, *reinterpret_cast<const uint4 *>(arena + bse), (uint32_t)(ve - bse));
+        }
+        const uint32_t e_pre = ep_own.y;
+        // Horner over the rows the record crosses
+        const uint64_t fr = rs / kRow, lr = (ve - 1) / kRow;
+        const uint32_t d = (uint32_t)((lr + 1) * kRow - ve);
+        // acc = the record's bytes of its rows, referenced to the end row's
+        // end, without the last block's ft (added back unshifted below)
+        uint32_t acc = e_pre;
+        if (fr == lr) {
+            acc ^= a_rs;
+        } else {
+            uint32_t h_acc = rend[fr] ^ a_rs;
+            for (uint64_t row = fr + 1; row < lr; row += 8) {
+                uint32_t v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = row + j < lr ? rend[row + j] : 0u;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (row + j < lr) h_acc = z4096(Tz, h_acc) ^ v[j];
+            }
+            acc ^= z4096(Tz, h_acc);
+        }
+        // F(0, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
+        const uint32_t chain = ft ^ (acc ? multmodp(xinv[d], acc) : 0u);
+        // F(0, prefix): header + key bytes [rs, vs) as aligned words from
+        // rs & ~3, the bytes before rs masked to zero (F ignores leading zeros)
+        const uint64_t w0 = rs & ~3ull;
+        const uint32_t lead = (uint32_t)(rs & 3), L = (uint32_t)(vs - w0);
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
-        uint32_t pw[10];
+        uint32_t pw[11];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) pw[i] = wp[i];  // header tail + keys up to 24 B (the arena is padded)
-        // Horner over the rows the chain crosses; the row values are loaded 8
-        // at a time so their latency overlaps
-        uint32_t acc = 0;
-        for (uint64_t row = fr; row < lr; row += 8) {
-            uint32_t v[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = row + j < lr ? rend[row + j] : 0u;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (row + j < lr) acc = z4096(Tz, acc) ^ v[j];
-        }
-        acc = z4096(Tz, acc) ^ cur.pre;
-        const uint32_t chain = cur.e ^ (acc ? multmodp(xinv_d, acc) : 0u);
-        // F(0, prefix): the bytes [w0, vs) = header tail + key as aligned words
-        // (slicing-by-4), the last partial word bytewise
+        for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
+        pw[0] &= ~0u << (8 * lead);
         uint32_t p = 0;
-        for (uint32_t i = 0; i < L / 4; ++i) {
-            const uint32_t x = p ^ (i < 10 ? pw[i] : wp[i]);
-            p = T[768 + (x & 0xFF)] ^ T[512 + ((x >> 8) & 0xFF)] ^ T[256 + ((x >> 16) & 0xFF)] ^ T[x >> 24];
-        }
+        for (uint32_t i = 0; i < L / 4; ++i) p = slice4t(T, p ^ (i < 11 ? pw[i] : wp[i]));
         if (L & 3) {
-            uint32_t y = L / 4 < 10 ? pw[L / 4] : wp[L / 4];
-            for (uint32_t i = 0; i < (L & 3); ++i, y >>= 8) p = T[(p ^ y) & 0xFF] ^ (p >> 8);
+            const uint32_t y = L / 4 < 11 ? pw[L / 4] : wp[L / 4];
+            p = partial_word(T, p, y, L & 3);  // L >= 16: never the masked word
         }
+        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
         const uint32_t raw0 = chain ^ (p ? multmodp(xv, p) : 0u);
-        const uint32_t z = V < (1u << 17) ? zv : multmodp(multmodp(xa[V >> 16], xb[V & 0xFFFF]), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        const uint32_t z = V < (1u << 17) ? zl[V] : multmodp(xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         const uint32_t calc = raw0 ^ z;
-        const uint64_t fo = start - fbase[f];
-        const bool tomb = h.z == 0;
-        gck_rec o;
-        o.rec_off = fo;
-        o.file = f;
-        o.key_len = tomb ? h.w : h.z;
-        o.value_pos = carry[f] + (uint32_t)fo + 16u + h.z;
-        o.value_size = h.w;
-        o.crc = h.x;
-        o.ts = h.y;
-        o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == h.x ? GCK_F_CRC_OK : 0u);
-        o.crc_calc = calc;
-        out[r] = o;
-        n_rej += calc != h.x;
-        cur = nxt;
+        if (valid) {
+            const uint64_t fo = rs - fbase[f];
+            const bool tomb = h.z == 0;
+            gck_rec o;
+            o.rec_off = fo;
+            o.file = f;
+            o.key_len = tomb ? h.w : h.z;
+            o.value_pos = carry[f] + (uint32_t)fo + 16u + h.z;
+            o.value_size = h.w;
+            o.crc = h.x;
+            o.ts = h.y;
+            o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == h.x ? GCK_F_CRC_OK : 0u);
+            o.crc_calc = calc;
+            out[r] = o;
+            n_rej += calc != h.x;
+        }
     }
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
@@ -1237,7 +1044,7 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
 
 // ------------------------------------------------------------- host side ---
 static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib, std::vector<uint32_t> &xinv,
-                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
+                        std::vector<uint32_t> &xfw, std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
                         std::vector<uint32_t> &zl) {
     slice.assign(4 * 256, 0);
     for (uint32_t n = 0; n < 256; ++n) {
@@ -1259,6 +1066,9 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
     xinv.assign(kRow, 0);
     xinv[0] = kX0;
     for (int d = 1; d < kRow; ++d) xinv[d] = multmodp(xinv[d - 1], xinv8);
+    xfw.assign(kRow, 0);  // x^(8d): forward shifts inside a row
+    xfw[0] = kX0;
+    for (int d = 1; d < kRow; ++d) xfw[d] = multmodp(xfw[d - 1], kX0 >> 8);
     xa.assign(65536, 0);
     xb.assign(65536, 0);
     xa[0] = xb[0] = kX0;
@@ -1318,11 +1128,11 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipEventCreate(&c->ev_start));
     GCK_HIP(hipEventCreate(&c->ev_end));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
-    std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow, zl;
-    make_tables(slice, nib, xinv, xa, xb, zrow, zl);
+    std::vector<uint32_t> slice, nib, xinv, xfw, xa, xb, zrow, zl;
+    make_tables(slice, nib, xinv, xfw, xa, xb, zrow, zl);
     int rc;
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
-        (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
+        (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xfw.ensure(xfw.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
         (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)))
         return rc;
@@ -1331,6 +1141,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipMemcpy(c->d_slice.p, slice.data(), slice.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xinv.p, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
+    GCK_HIP(hipMemcpy(c->d_xfw.p, xfw.data(), xfw.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xa.p, xa.data(), xa.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xb.p, xb.data(), xb.size() * 4, hipMemcpyHostToDevice));
     return GCK_OK;
@@ -1341,9 +1152,9 @@ static void ctx_free(Ctx *c) {
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
-                   &c->d_rec_hdr, &c->d_rec_file, &c->d_e, &c->d_pre, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan, &c->d_big,
-                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_bigcnt};
+                   &c->d_rec_hdr, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
+                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
+                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_queue};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1408,8 +1219,9 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_rend.ensure((c->n_rows + 1) * 4)) || (rc = c->d_plan.ensure((c->n_rows + 1) * 64)) || (rc = c->d_big.ensure((c->n_rows + 1) * 4)) ||
-        (rc = c->d_bigcnt.ensure((c->n_rows / 64 + kMaxGroups + 2) * 4)))
+        (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
+        (rc = c->d_plan.ensure((c->n_rows + kBlockRows * (kMaxGroups + 1)) * kPlanRowBytes)) ||
+        (rc = c->d_queue.ensure((kMaxGroups + 1) * 4)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -1433,9 +1245,9 @@ static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + p
 // (re-walked by k_compact), 3 CRC rejects, 5 big rows (sync path), 6 record-
 // table capacity overflow (pipelined path), 8.. validation rounds (sync path),
 // 15 host validation loop.
-enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_BIG = 5, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
+enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
 // Per-group counter slots (d_gcnt, 8 x u32 per group).
-enum : int { G_BIG = 0, G_VAL = 1 };  // G_VAL + round: validation rounds, the last one must be 0
+enum : int { G_VAL = 1 };  // G_VAL + round: validation rounds, the last one must be 0
 constexpr int kRounds = 2;             // device validation/fixup rounds
 
 // Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
@@ -1491,12 +1303,15 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
 }
 
 // Record table of chunks [c0, c1), row index and row plan of rows [r0, r1).
-// Slow-row lists of rows [r0, r1): list slots d_big + r0, per-64-row counts at
-// d_bigcnt + (r0 / 64 + g) (disjoint per file group g), any-flag big_any.
-static uint32_t *big_counts(Ctx *c, uint64_t r0, uint32_t g) { return c->d_bigcnt.as<uint32_t>() + r0 / 64 + g; }
+// Plan of the file group g whose rows start at r0: the group's blocks are
+// counted from r0, and each group's region is padded by a block so that a
+// group's last partial block never overlaps the next group's plan.
+static uint4 *group_plan(Ctx *c, uint64_t r0, uint32_t g) {
+    return c->d_plan.as<uint4>() + (r0 + (uint64_t)kBlockRows * g) * kPlanRowBytes / 16;
+}
 
 static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
-                           const uint64_t *rng, uint64_t cap, uint32_t g, uint32_t *big_any) {
+                           const uint64_t *rng, uint64_t cap, uint32_t g) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
     if (n)
         k_compact<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
@@ -1512,30 +1327,24 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
                                      c->d_row_first.as<uint32_t>());
     if (r1 > r0)
-        k_row_plan<<<nblk(r1 - r0, 64 * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
-            c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0, r1 - r0, c->d_row_first.as<uint32_t>(),
-            c->d_plan.as<uint4>(), c->d_big.as<uint32_t>() + r0, big_counts(c, r0, g), big_any);
+        k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
+            c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
+            group_plan(c, r0, g));
 }
 
-// CRC partials of rows [r0, r1): k_crc_rows, then k_crc_rows_big on the rows
-// k_row_plan listed.  e/pre scratch slot: cap; rend scratch: row n_rows.
-static void launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, const uint64_t *rng, uint64_t cap,
-                       uint32_t g, const uint32_t *big_any, hipEvent_t between = nullptr) {
-    if (r1 <= r0) return;
-    const uint64_t nr = r1 - r0, want = (nr + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
-    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
-    k_crc_rows<0, kDepth, kRowsPerStep><<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>() + r0 * kRow, nr,
-                                                c->d_plan.as<uint8_t>() + r0 * kPlanBytes, cap,
-                                                c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),
-                                                c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
-                                                c->d_rend.as<uint32_t>() + r0, c->d_rend.as<uint32_t>() + c->n_rows);
-    if (between) (void)hipEventRecord(between, s);
-    k_crc_rows_big<0><<<c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_big.as<uint32_t>() + r0,
-                                              big_counts(c, r0, g), big_any, (uint32_t)((nr + 63) / 64),
-                                              c->d_row_first.as<uint32_t>(), rng, c->d_rec_off.as<uint64_t>(),
-                                              c->d_rec_hdr.as<uint4>(), c->d_slice.as<uint32_t>(),
-                                              c->d_nib.as<uint32_t>(), c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),
-                                              c->d_rend.as<uint32_t>());
+// CRC partials of rows [r0, r1) of file group g (k_crc_rows).  Record-slot
+// scratch: cap .. cap + kEpScratch; rend scratch: rows n_rows ...
+static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, uint32_t g) {
+    if (r1 <= r0) return GCK_OK;
+    const uint64_t nb = (r1 - r0 + kBlockRows - 1) / kBlockRows;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
+    uint32_t *queue = c->d_queue.as<uint32_t>() + g;
+    GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
+    k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, group_plan(c, r0, g), c->d_row_first.as<uint32_t>() + r0, cap,
+        c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
+        c->d_rend.as<uint32_t>() + c->n_rows, queue);
+    return GCK_OK;
 }
 
 static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
@@ -1544,8 +1353,9 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
     const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu * 8 ? want : (uint64_t)c->n_cu * 8);
     k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
-                                    rng, c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(), c->d_rend.as<uint32_t>(),
-                                    c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_zrow.as<uint32_t>(),
+                                    rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
+                                    c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_xfw.as<uint32_t>(),
+                                    c->d_zrow.as<uint32_t>(),
                                     c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
 }
@@ -1554,8 +1364,8 @@ static int ensure_records(Ctx *c, uint64_t nr) {
     nr = nr ? nr : 1;
     int rc;
     if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_hdr.ensure(nr * 16)) ||
-        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_e.ensure((nr + 65) * 4)) ||
-        (rc = c->d_pre.ensure((nr + 65) * 4)) || (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
+        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_ep.ensure((nr + kEpScratch) * 8)) ||
+        (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
         return rc;
     return GCK_OK;
 }
@@ -1671,10 +1481,9 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
 
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, 0, cnt + CNT_BIG);
+    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, 0);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total) launch_crc(c, s, 0, c->n_rows, gbase, n_total, 0, cnt + CNT_BIG, c->ev[PH_CRCBIG]);
-    else GCK_HIP(hipEventRecord(c->ev[PH_CRCBIG], s));
+    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, 0))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1744,11 +1553,11 @@ static int ctx_run_pipe(Ctx *c) {
         k_group_carry<<<1, 1, 0, s>>>(f1 - f0, c->d_flen.as<uint64_t>() + f0, c->d_freset.as<uint32_t>() + f0,
                                       c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0,
                                       c->d_carry.as<uint32_t>() + f0, gcarry + g, gcarry + g + 1);
-        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, g, gcnt + g * 8 + G_BIG);
+        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, g);
         GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
         GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
         GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
-        launch_crc(c, c->s_crc, r0, r1, gbase + g, cap, g, gcnt + g * 8 + G_BIG);
+        if (int rc = launch_crc(c, c->s_crc, r0, r1, cap, g)) return rc;
         GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
         GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
         GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
@@ -1906,8 +1715,7 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
 }
 
 const char *gck_phase_name(int phase) {
-    static const char *names[] = {"boundary", "scan",     "host_sync", "records",
-                                  "crc_rows", "crc_big", "finalize",  "pipeline"};
+    static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows", "finalize", "pipeline"};
     return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
@@ -1964,29 +1772,32 @@ const char *gck_last_error(void) { return gck::last_error(); }
 
 // Measurement helper: time ablated variants of k_crc_rows on the state left by
 // the last gck_ctx_run (outputs are clobbered; rerun before fetching).
-// mode bits: 1 = no record intervals, 2 = no LDS table chain, 4 = no tail
-// shift / segmented scan.
+// mode bits: 2 = no LDS table chain, 4 = no row shift / wave scan, 8 = no
+// loads (synthetic bytes).
 int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
-    if (!ctx || iters <= 0 || mode < 0 || mode > 15) return GCK_EINVAL;
+    if (!ctx || iters <= 0 || mode < 0 || mode > 127) return GCK_EINVAL;
     Ctx *c = &ctx->c;
     if (!c->n_rows || !c->n_recs) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
-    const uint64_t want = (c->n_rows + kWaves * kRowsPerStep - 1) / (kWaves * kRowsPerStep);
-    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu ? want : (uint64_t)c->n_cu);
+    const uint64_t nb = (c->n_rows + kBlockRows - 1) / kBlockRows;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
+    uint32_t *queue = c->d_queue.as<uint32_t>();
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
     GCK_HIP(hipEventRecord(a, c->stream));
     for (int i = 0; i < iters; ++i) {
+        GCK_HIP(hipMemsetAsync(queue, 0, 4, c->stream));
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
-        k_crc_rows<M, kDepth, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint8_t>(), \
-                                                    c->n_recs, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(),      \
-                                                    c->d_e.as<uint32_t>(), c->d_pre.as<uint32_t>(),                     \
-                                                    c->d_rend.as<uint32_t>(), c->d_rend.as<uint32_t>() + c->n_rows);    \
+        k_crc_rows<M, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(                                                  \
+            c->arena.as<uint8_t>(), c->n_rows, group_plan(c, 0, 0), c->d_row_first.as<uint32_t>(), c->n_recs,      \
+            c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),      \
+            c->d_rend.as<uint32_t>() + c->n_rows, queue);                                                           \
         break;
         switch (mode) {
-            GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(5) GCK_VARIANT(6) GCK_VARIANT(7) GCK_VARIANT(8)
+            GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(6) GCK_VARIANT(8) GCK_VARIANT(12)
+            GCK_VARIANT(16) GCK_VARIANT(22)
             default: return GCK_EINVAL;
         }
 #undef GCK_VARIANT

@@ -11,7 +11,7 @@ for _ in range(3):
 st = ctx.stats()
 out = {"cfg": cfg, "bytes": st["bytes"], "phase_ms": st["ms_phase"], "stream": ctx.stream_read_ceiling(5)}
 ms = ctypes.c_double()
-for mode in [0, 2, 4, 5, 6, 7, 8]:
+for mode in [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else "0,2,4,6,8,12".split(","))]:
     g._lib.check(ctx._L.gck_diag_crc_variant(ctx._h, mode, 5, ctypes.byref(ms)))
     out[f"mode{mode}_ms"] = round(ms.value, 3)
     out[f"mode{mode}_gbs"] = round(st["bytes"] / ms.value / 1e6, 1)
