@@ -95,7 +95,6 @@ def main():
     ap.add_argument("--chunk-kib", type=int, default=0)
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pipeline", action="store_true", help="file-group pipeline (GCK_OPT_PIPELINE)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
 
@@ -117,7 +116,7 @@ def main():
 
     cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10, pipeline=args.pipeline)
+    ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10)
     info = ctx.encode(**cfg)
     setup_s = time.perf_counter() - t_setup
 
@@ -150,7 +149,7 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         value = total_bytes * args.steps / elapsed / GiB
         crc_avg = sum(crc_ms) / len(crc_ms)
-        launches = min(info["n_files"], 16) if st["pipelined"] else 1
+        launches = 1
         achieved = my_bytes / (crc_avg * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
@@ -188,13 +187,12 @@ def main():
                 "crc_rows_ms": round(crc_avg, 4),
                 "launches_per_step": launches,
                 "algorithmic_bytes_per_launch": round(my_bytes / launches),
-                "note": "achieved = data-file bytes / HIP-event time of the k_crc_rows launches of a step "
-                        "(one launch per file group; bytes per launch = the group's files)",
+                "note": "achieved = data-file bytes / HIP-event time of the k_crc_rows launch of a step "
+                        "(one launch per step over all files)",
                 "stream_read_gbs": round(stream_gbs, 1),
                 "frac_of_stream_read": round(achieved / stream_gbs, 4),
             },
             "phase_ms": {k: round(v / args.steps, 4) for k, v in phases_sum.items()},
-            "pipelined": st["pipelined"],
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config, int(args.cpu_sample_gib * GiB))

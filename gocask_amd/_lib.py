@@ -25,7 +25,6 @@ GCK_ECRC_FAILED = 7
 GCK_EINVALID_KEY = 8
 GCK_ENOT_DIR = 9
 
-GCK_OPT_PIPELINE = 2  # gck_opts.flags: file-group pipeline
 
 F_TOMBSTONE = 1
 F_CRC_OK = 2
@@ -93,8 +92,7 @@ class GckStats(ctypes.Structure):
         ("n_overflow", ctypes.c_uint64),
         ("ms_total", ctypes.c_double),
         ("ms_kernel", ctypes.c_double * 12),
-        ("pipelined", ctypes.c_uint32),
-        ("n_sync_reruns", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32 * 2),
     ]
 
 

@@ -79,13 +79,13 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = _lib.GCK_OPT_PIPELINE if pipeline else 0
+    o.flags = 0
     return o
 
 
@@ -223,14 +223,14 @@ def _result(res: GckResult):
                       files_walked=res.files_walked)
 
 
-def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, pipeline)),
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
                       ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
@@ -256,10 +256,10 @@ def keydir(files, recs):
 class ReplayContext:
     """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
 
-    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, pipeline=False):
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
-        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, pipeline)),
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
                                      ctypes.byref(self._h)))
 
     def load(self, files, reset_after=None):
@@ -306,8 +306,7 @@ class ReplayContext:
                 break
             phases[name] = s.ms_kernel[i]
         return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
-                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
-                    pipelined=bool(s.pipelined), n_sync_reruns=s.n_sync_reruns)
+                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases)
 
     def stream_read_ceiling(self, iters=10):
         """Plain streaming read of the resident arena: (ms per pass, GB/s)."""

@@ -48,7 +48,7 @@ struct DBuf {
 enum Phase {
     PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
     PH_SCAN,          // record slots per chunk, per-file summary
-    PH_HOST,          // D2H summary + host bookkeeping (synchronous path)
+    PH_HOST,          // D2H summary + host bookkeeping
     PH_RECORDS,       // k_compact, k_row_fill / k_row_index, k_row_plan
     PH_CRC,           // k_crc_rows: the HBM-bound kernel
     PH_FINAL,         // k_finalize: CRC verdict + tuples
@@ -57,7 +57,6 @@ enum Phase {
     PH_NPHASE
 };
 
-constexpr int kMaxGroups = 16;  // file groups of the pipelined run
 
 struct Ctx {
     int device = 0;
@@ -80,7 +79,7 @@ struct Ctx {
     DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
     DBuf d_rec_base, d_bsum, d_scratch_off, d_scratch_hdr, d_counters;
     DBuf d_freset;                   // per file: 1 = lastOffset resets after it
-    DBuf d_gbase, d_gcarry, d_gcnt;  // per file group: record base, lastOffset in, counters
+    DBuf d_gbase;                    // record range of the run [0, n)
 
     // records
     uint64_t n_recs = 0;
@@ -99,14 +98,7 @@ struct Ctx {
     uint64_t err_off = 0, n_crc_fail = 0, n_fixups = 0, n_overflow = 0;
     double ms_total = 0, ms_phase[PH_NPHASE] = {};
     hipEvent_t ev[PH_END + 1] = {};
-    bool pipelined = false;
-    uint32_t n_sync_reruns = 0;
 
-    // pipelined run: streams, file groups (first file of each, plus nfiles), events
-    hipStream_t s_crc = nullptr, s_fin = nullptr;
-    std::vector<uint32_t> g_file;
-    hipEvent_t ev_start = nullptr, ev_end = nullptr;
-    std::vector<hipEvent_t> ev_bnd, ev_crc0, ev_crc1, ev_fin0, ev_fin1;
 
     // encoder bookkeeping
     std::vector<uint32_t> walk_to_creation;

@@ -500,16 +500,12 @@ __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uin
     return rec_off[r] + 16 + (uint64_t)h.z + h.w;  // tombstone: KeySize 0, the key is the "value"
 }
 
-// Record range [rng[0], rng[1]) of one file group (device-resident: the group
-// scans of the pipeline produce them without a host round trip).
+// Record range [rng[0], rng[1]) of the run (device-resident).
 //
 // row_first[row] = first record whose value ends after the row's first byte,
-// for the rows [r0, ...) of the group; rows past the group's last record end
-// keep k_row_fill's value rng[1].  Grid-stride over the device range.
-// k_row_fill writes rows (r0, r1]: row r1 (the next group's first row) gets
-// rng[1] = the next group's first record, its final value, before the next
-// group starts, so the row entries a group reads never change under it.  Row 0
-// is 0 from the start of the run.
+// for the rows [r0, ...); rows past the last record end keep k_row_fill's
+// value rng[1] (k_row_fill writes rows (r0, r1]; row r0 is set by the caller).
+// Grid-stride over the device range.
 __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64_t r1,
                            const uint64_t *__restrict__ rng) {
     const uint32_t v = (uint32_t)rng[1];
@@ -528,23 +524,6 @@ __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *_
         const uint64_t hi = (ve_r + kRow - 1) / kRow;
         for (uint64_t row = lo; row < hi; ++row) row_first[row] = (uint32_t)r;
     }
-}
-
-// lastOffset carried into each file of a group (core/db.go:110-123,
-// core/keydir.go:22-53): after a file it is reset iff the file is not the
-// active one, else advanced by the bytes the walk consumed.  One thread; the
-// group's outgoing value feeds the next group.
-__global__ void k_group_carry(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
-                              const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
-                              uint32_t *__restrict__ carry, const uint32_t *__restrict__ carry_in,
-                              uint32_t *__restrict__ carry_out) {
-    uint32_t last = *carry_in;
-    for (uint32_t f = 0; f < nf; ++f) {
-        carry[f] = last;
-        last += (uint32_t)(fterm[f] != T_NONE ? ftpos[f] : flen[f]);
-        if (freset[f]) last = 0;
-    }
-    *carry_out = last;
 }
 
 constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
@@ -1119,14 +1098,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    // the CRC stream carries the critical path of the pipelined run
-    int prio_lo = 0, prio_hi = 0;
-    GCK_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    GCK_HIP(hipStreamCreateWithPriority(&c->s_crc, hipStreamNonBlocking, prio_hi));
-    GCK_HIP(hipStreamCreateWithFlags(&c->s_fin, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
-    GCK_HIP(hipEventCreate(&c->ev_start));
-    GCK_HIP(hipEventCreate(&c->ev_end));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     std::vector<uint32_t> slice, nib, xinv, xfw, xa, xb, zrow, zl;
     make_tables(slice, nib, xinv, xfw, xa, xb, zrow, zl);
@@ -1154,17 +1126,11 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_gcarry, &c->d_gcnt, &c->d_queue};
+                   &c->d_freset, &c->d_gbase, &c->d_queue};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto *v : {&c->ev_bnd, &c->ev_crc0, &c->ev_crc1, &c->ev_fin0, &c->ev_fin1}) {
-        for (auto e : *v) (void)hipEventDestroy(e);
-        v->clear();
-    }
-    if (c->ev_start) (void)hipEventDestroy(c->ev_start);
-    if (c->ev_end) (void)hipEventDestroy(c->ev_end);
-    for (hipStream_t *st : {&c->stream, &c->s_crc, &c->s_fin}) {
+    for (hipStream_t *st : {&c->stream}) {
         if (*st) (void)hipStreamDestroy(*st);
         *st = nullptr;
     }
@@ -1220,8 +1186,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
         (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
-        (rc = c->d_plan.ensure((c->n_rows + kBlockRows * (kMaxGroups + 1)) * kPlanRowBytes)) ||
-        (rc = c->d_queue.ensure((kMaxGroups + 1) * 4)))
+        (rc = c->d_plan.ensure((c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -1242,12 +1207,9 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
 static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
 // Counter slots (d_counters, u32): 1 fixups, 2 chunks whose stage overflowed
-// (re-walked by k_compact), 3 CRC rejects, 5 big rows (sync path), 6 record-
-// table capacity overflow (pipelined path), 8.. validation rounds (sync path),
-// 15 host validation loop.
+// (re-walked by k_compact), 3 CRC rejects, 6 record-table capacity overflow,
+// 8.. validation rounds, 15 host validation loop.
 enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
-// Per-group counter slots (d_gcnt, 8 x u32 per group).
-enum : int { G_VAL = 1 };  // G_VAL + round: validation rounds, the last one must be 0
 constexpr int kRounds = 2;             // device validation/fixup rounds
 
 // Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
@@ -1302,16 +1264,11 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
             c->d_fnrec.as<uint64_t>() + f0, f1 - f0);
 }
 
-// Record table of chunks [c0, c1), row index and row plan of rows [r0, r1).
-// Plan of the file group g whose rows start at r0: the group's blocks are
-// counted from r0, and each group's region is padded by a block so that a
-// group's last partial block never overlaps the next group's plan.
-static uint4 *group_plan(Ctx *c, uint64_t r0, uint32_t g) {
-    return c->d_plan.as<uint4>() + (r0 + (uint64_t)kBlockRows * g) * kPlanRowBytes / 16;
-}
+// Record table of chunks [c0, c1), row index and row plan of rows [r0, r1)
+// (the plan counts blocks from r0).
 
 static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
-                           const uint64_t *rng, uint64_t cap, uint32_t g) {
+                           const uint64_t *rng, uint64_t cap) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
     if (n)
         k_compact<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
@@ -1329,19 +1286,20 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     if (r1 > r0)
         k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
             c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
-            group_plan(c, r0, g));
+            c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16);
 }
 
-// CRC partials of rows [r0, r1) of file group g (k_crc_rows).  Record-slot
-// scratch: cap .. cap + kEpScratch; rend scratch: rows n_rows ...
-static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, uint32_t g) {
+// CRC partials of rows [r0, r1) (k_crc_rows).  Record-slot scratch: cap ..
+// cap + kEpScratch; rend scratch: rows n_rows ...
+static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap) {
     if (r1 <= r0) return GCK_OK;
     const uint64_t nb = (r1 - r0 + kBlockRows - 1) / kBlockRows;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
-    uint32_t *queue = c->d_queue.as<uint32_t>() + g;
+    uint32_t *queue = c->d_queue.as<uint32_t>();
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
-        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, group_plan(c, r0, g), c->d_row_first.as<uint32_t>() + r0, cap,
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16,
+        c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue);
     return GCK_OK;
@@ -1416,10 +1374,12 @@ static int read_file_summaries(Ctx *c, hipStream_t s, std::vector<uint32_t> &fte
     return GCK_OK;
 }
 
-// The synchronous pipeline: every phase over all files, one host round trip
-// after the boundary phases (exact record count, EOF verdicts, carries).
-// Used for single-file corpora and as the fallback of the pipelined run.
-static int ctx_run_sync(Ctx *c) {
+// One replay on the resident arena, every phase over all files in order, one
+// host round trip after the boundary phases (exact record count, EOF
+// verdicts, carries).  The CRC pass needs the record boundaries (its plan),
+// and running the latency-bound boundary kernels beside an HBM-saturating
+// pass slows them ~7x (loaded latency), so the phases do not overlap.
+static int ctx_run(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -1481,9 +1441,9 @@ static int ctx_run_sync(Ctx *c) {
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
 
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total, 0);
+    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, 0))) return rc;
+    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1501,129 +1461,8 @@ static int ctx_run_sync(Ctx *c) {
     float span = 0;
     (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
     c->ms_phase[PH_PIPE] = span;
-    c->pipelined = false;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
-}
-
-// File groups of the pipelined run: consecutive files in walk order,
-// balanced by bytes, at most kMaxGroups.
-static void make_groups(Ctx *c) {
-    const uint32_t nf = c->nfiles;
-    c->g_file.clear();
-    const uint32_t G = nf < (uint32_t)kMaxGroups ? nf : (uint32_t)kMaxGroups;
-    c->g_file.push_back(0);
-    uint64_t acc = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
-        acc += c->f_len[f];
-        const uint32_t g = (uint32_t)c->g_file.size();  // groups closed so far + 1
-        if (f + 1 < nf && g < G && acc * G >= c->data_bytes * g) c->g_file.push_back(f + 1);
-    }
-    c->g_file.push_back(nf);
-}
-
-// The pipelined run: file groups go through boundary discovery, record table
-// and row plan on stream s (in walk order, record bases and lastOffset
-// carried on the device), CRC rows on c->s_crc and finalize on c->s_fin, so
-// group g's CRC overlaps group g+1's boundary work and group g-1's finalize.
-// No host round trip until the end; anything unusual (validation not settled
-// after kRounds, record-table capacity, a startup error) reruns synchronously.
-static int ctx_run_pipe(Ctx *c) {
-    const auto t0 = std::chrono::steady_clock::now();
-    GCK_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint32_t nf = c->nfiles, G = (uint32_t)c->g_file.size() - 1;
-    uint32_t *cnt = c->d_counters.as<uint32_t>();
-    uint64_t *gbase = c->d_gbase.as<uint64_t>();
-    uint32_t *gcarry = c->d_gcarry.as<uint32_t>();
-    uint32_t *gcnt = c->d_gcnt.as<uint32_t>();
-    const uint64_t cap = c->rec_cap;
-    GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
-    GCK_HIP(hipMemsetAsync(gbase, 0, (G + 1) * 8, s));
-    GCK_HIP(hipMemsetAsync(gcarry, 0, (G + 1) * 4, s));
-    GCK_HIP(hipMemsetAsync(gcnt, 0, G * 32, s));
-    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
-    GCK_HIP(hipEventRecord(c->ev_start, s));
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t f0 = c->g_file[g], f1 = c->g_file[g + 1];
-        const uint32_t c0 = c->f_first_chunk[f0], c1 = f1 < nf ? c->f_first_chunk[f1] : c->n_chunks;
-        const uint64_t r0 = c->f_base[f0] / kRow, r1 = f1 < nf ? c->f_base[f1] / kRow : c->n_rows;
-        launch_boundary(c, s, c0, c1, gcnt + g * 8 + G_VAL);
-        launch_scan(c, s, c0, c1, f0, f1, gbase + g, cap);
-        k_group_carry<<<1, 1, 0, s>>>(f1 - f0, c->d_flen.as<uint64_t>() + f0, c->d_freset.as<uint32_t>() + f0,
-                                      c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0,
-                                      c->d_carry.as<uint32_t>() + f0, gcarry + g, gcarry + g + 1);
-        launch_records(c, s, c0, c1, r0, r1, gbase + g, cap, g);
-        GCK_HIP(hipEventRecord(c->ev_bnd[g], s));
-        GCK_HIP(hipStreamWaitEvent(c->s_crc, c->ev_bnd[g], 0));
-        GCK_HIP(hipEventRecord(c->ev_crc0[g], c->s_crc));
-        if (int rc = launch_crc(c, c->s_crc, r0, r1, cap, g)) return rc;
-        GCK_HIP(hipEventRecord(c->ev_crc1[g], c->s_crc));
-        GCK_HIP(hipStreamWaitEvent(c->s_fin, c->ev_crc1[g], 0));
-        GCK_HIP(hipEventRecord(c->ev_fin0[g], c->s_fin));
-        launch_finalize(c, c->s_fin, gbase + g, (uint64_t)(c1 - c0) * c->opts.chunk_cap);
-        GCK_HIP(hipEventRecord(c->ev_fin1[g], c->s_fin));
-    }
-    std::vector<uint32_t> fterm, gc(G * 8);
-    std::vector<uint64_t> ftpos, ffirst, fnrec;
-    if (read_file_summaries(c, c->s_fin, fterm, ftpos, ffirst, fnrec)) return GCK_EDEVICE;
-    uint32_t hcnt[16] = {};
-    GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, c->s_fin));
-    GCK_HIP(hipMemcpyAsync(gc.data(), gcnt, G * 32, hipMemcpyDeviceToHost, c->s_fin));
-    GCK_HIP(hipEventRecord(c->ev_end, c->s_fin));
-    GCK_HIP(hipStreamSynchronize(c->s_fin));
-    GCK_HIP(hipGetLastError());
-    bool settled = hcnt[CNT_CAP] == 0;
-    for (uint32_t g = 0; g < G; ++g) settled &= gc[g * 8 + G_VAL + kRounds] == 0;
-    const uint64_t n_total = account_files(c, fterm, ftpos, ffirst, fnrec, nullptr);
-    if (!settled || c->status != GCK_OK || n_total > 0xFFFFFFF0ull) {
-        ++c->n_sync_reruns;
-        return ctx_run_sync(c);
-    }
-    c->n_recs = n_total;
-    c->n_fixups = hcnt[CNT_FIXUP];
-    c->n_overflow = hcnt[CNT_STAGE];
-    c->n_crc_fail = hcnt[CNT_REJECT];
-    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
-    for (uint32_t g = 0; g < G; ++g) {
-        float a = 0, b = 0;
-        (void)hipEventElapsedTime(&a, c->ev_crc0[g], c->ev_crc1[g]);
-        (void)hipEventElapsedTime(&b, c->ev_fin0[g], c->ev_fin1[g]);
-        c->ms_phase[PH_CRC] += a;
-        c->ms_phase[PH_FINAL] += b;
-    }
-    float span = 0;
-    (void)hipEventElapsedTime(&span, c->ev_start, c->ev_end);
-    c->ms_phase[PH_PIPE] = span;
-    c->pipelined = true;
-    c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return GCK_OK;
-}
-
-static int ctx_run(Ctx *c) {
-    const bool pipe = c->nfiles >= 2 && (c->opts.flags & GCK_OPT_PIPELINE);
-    if (!pipe) return ctx_run_sync(c);
-    GCK_HIP(hipSetDevice(c->device));
-    make_groups(c);
-    const uint32_t G = (uint32_t)c->g_file.size() - 1;
-    // record-table capacity: the stage bound (chunk_cap per chunk) or the last
-    // exact count, whichever is larger; beyond it the run reruns synchronously
-    const uint64_t want = std::max<uint64_t>((uint64_t)c->n_chunks * c->opts.chunk_cap, c->n_recs);
-    int rc;
-    if ((rc = ensure_records(c, want)) || (rc = c->d_gbase.ensure((G + 1) * 8)) ||
-        (rc = c->d_gcarry.ensure((G + 1) * 4)) || (rc = c->d_gcnt.ensure(G * 32)))
-        return rc;
-    c->rec_cap = want;
-    while (c->ev_bnd.size() < G) {
-        hipEvent_t e[5];
-        for (auto &x : e) GCK_HIP(hipEventCreate(&x));
-        c->ev_bnd.push_back(e[0]);
-        c->ev_crc0.push_back(e[1]);
-        c->ev_crc1.push_back(e[2]);
-        c->ev_fin0.push_back(e[3]);
-        c->ev_fin1.push_back(e[4]);
-    }
-    return ctx_run_pipe(c);
 }
 
 }  // namespace gck
@@ -1709,8 +1548,6 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->n_overflow = c->n_overflow;
     out->ms_total = c->ms_total;
     for (int p = 0; p < PH_NPHASE && p < 12; ++p) out->ms_kernel[p] = c->ms_phase[p];
-    out->pipelined = c->pipelined ? 1u : 0u;
-    out->n_sync_reruns = c->n_sync_reruns;
     return GCK_OK;
 }
 
@@ -1791,7 +1628,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
 #define GCK_VARIANT(M)                                                                                              \
     case M:                                                                                                         \
         k_crc_rows<M, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(                                                  \
-            c->arena.as<uint8_t>(), c->n_rows, group_plan(c, 0, 0), c->d_row_first.as<uint32_t>(), c->n_recs,      \
+            c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint4>(), c->d_row_first.as<uint32_t>(), c->n_recs,      \
             c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),      \
             c->d_rend.as<uint32_t>() + c->n_rows, queue);                                                           \
         break;

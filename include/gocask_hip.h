@@ -80,14 +80,9 @@ typedef struct gck_opts {
     uint32_t chunk_bytes;  /* boundary-speculation chunk (default 256 KiB, power of two)  */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
     uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
-    uint32_t flags;        /* GCK_OPT_* (0: defaults)                                      */
+    uint32_t flags;        /* reserved, 0                                                   */
 } gck_opts;
 
-/* gck_opts.flags: GCK_OPT_PIPELINE runs file groups as a pipeline (boundary
- * discovery of group g+1 beside the CRC of group g, no host round trip until
- * the end); the default runs every phase over all files with one host round
- * trip.  Results are identical either way. */
-#define GCK_OPT_PIPELINE 2u
 
 typedef struct gck_result {
     gck_rec *recs;              /* library-owned host array; free with gck_result_free  */
@@ -116,8 +111,7 @@ typedef struct gck_stats {
     uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
     double ms_total;        /* last gck_ctx_run wall time (host clock)                */
     double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
-    uint32_t pipelined;     /* 1: the last run was the file-group pipeline            */
-    uint32_t n_sync_reruns; /* pipelined runs that fell back to the synchronous path  */
+    uint32_t reserved[2];
 } gck_stats;
 
 int gck_ctx_create(const gck_opts *opts, gck_ctx **out);

@@ -167,66 +167,61 @@ CORPORA = [
 ]
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
 @pytest.mark.parametrize("chunk,cap", [(4096, 2), (1 << 15, 256), (1 << 18, 256)])
 @pytest.mark.parametrize("ci", range(len(CORPORA)))
-def test_random_corpora(g, orc, ci, chunk, cap, pipeline):
+def test_random_corpora(g, orc, ci, chunk, cap):
     files, names = orc.gen_corpus(**CORPORA[ci])
     wf, reset = walk_sorted(files, names)
     want, wst = orc.replay(wf, reset)
-    got, gst = g.replay(wf, reset, chunk_bytes=chunk, chunk_cap=cap, pipeline=pipeline)
+    got, gst = g.replay(wf, reset, chunk_bytes=chunk, chunk_cap=cap)
     assert_same(got, gst, want, wst)
     assert np.array_equal(got["flags"] & 2 == 0, want["crc_calc"] != want["crc"])
 
 
-# ----------------------------------------------- pipelined vs synchronous ---
-def test_pipeline_vs_oracle_multi_file(g, orc):
-    # file-group pipeline (boundary work of group g+1 beside the CRC of group g):
-    # 12 rotated files, so 12 groups, walk order != creation order
+# ------------------------------------------------- multi-file runs, reruns ---
+def test_multi_file_context(g, orc):
+    # 12 rotated files (walk order != creation order) through a context
     kw = dict(seed=44, val_fixed=0, key_min=8, key_max=24, key_universe=20000, tomb_permille=10,
               flip_permille=10, max_file_size=6 << 20, n_files=12)
     files, names = orc.gen_corpus(**kw)
     wf, reset = walk_sorted(files, names)
     want, wst = orc.replay(wf, reset)
-    with g.ReplayContext(pipeline=True) as ctx:
+    with g.ReplayContext() as ctx:
         ctx.load(wf, reset)
         ctx.run()
         got, gst = ctx.fetch()
-        st = ctx.stats()
-    assert st["pipelined"] and st["n_sync_reruns"] == 0
     assert_same(got, gst, want, wst)
 
 
-def test_pipeline_equals_sync_c3_shape(g):
-    # C3 shape at 1/8 scale, device-encoded: both run modes give identical tuples
+def test_repeated_runs_identical_c3_shape(g):
+    # C3 shape at 1/8 scale, device-encoded: back-to-back runs on one context
+    # (capacities and the block queue reused) give identical tuples
     kw = dict(seed=3, val_fixed=0, key_min=8, key_max=24, key_universe=600000, tomb_permille=10,
               flip_permille=10, max_file_size=256 << 20, n_files=16)
-    out = {}
-    for pipe in (False, True):
-        with g.ReplayContext(pipeline=pipe) as ctx:
-            ctx.encode(**kw)
+    with g.ReplayContext() as ctx:
+        ctx.encode(**kw)
+        ctx.run()
+        a, ast = ctx.fetch()
+        for _ in range(3):
             ctx.run()
-            ctx.run()  # second run: capacity from the first
-            out[pipe] = ctx.fetch()
-            st = ctx.stats()
-            assert st["pipelined"] == pipe and st["n_sync_reruns"] == 0
-    (a, ast), (b, bst) = out[True], out[False]
+        b, bst = ctx.fetch()
     assert_same(a, ast, b, bst)
+    assert ast["n_crc_fail"] > 0
 
 
-def test_pipeline_falls_back_when_capacity_exceeded(g, orc):
-    # 20-byte records with a 16-record stage: more records than the stage-based
-    # capacity, so the pipelined run must rerun synchronously and still be exact
+def test_stage_overflow_rewalks(g, orc):
+    # 20-byte records with a 16-record stage: chunks overflow their stage and
+    # k_compact re-walks them straight into the record table
     recs = [orc_mod.entry(i, b"k%d" % (i % 7), b"") for i in range(4000)]
     files = [b"".join(recs[:2000]), b"".join(recs[2000:])]
     reset = [True, False]
     want, wst = orc.replay(files, reset)
-    with g.ReplayContext(chunk_bytes=4096, chunk_cap=16, pipeline=True) as ctx:
+    with g.ReplayContext(chunk_bytes=4096, chunk_cap=16) as ctx:
         ctx.load(files, reset)
         ctx.run()
         got, gst = ctx.fetch()
         st = ctx.stats()
-    assert st["n_sync_reruns"] >= 1
+    assert st["n_overflow"] >= 1
     assert_same(got, gst, want, wst)
 
 
