@@ -63,6 +63,7 @@ struct Ctx {
     hipStream_t stream = nullptr;
     gck_opts opts{};
     int n_cu = 256;
+    int fin_blocks_per_cu = 4;  // resident k_finalize workgroups per CU
 
     // arena: files in walk order, each at a kRow-aligned offset
     DBuf arena;

@@ -874,6 +874,18 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 // end, range end) reads its own end block.
 // ValuePos = lastOffset + 16 + KeySize mod 2^32 (core/keydir.go:25), with
 // lastOffset = carry + offset within the file.
+// a * b mod P (multmodp's product), branch-free: 32 unrolled steps of
+// p ^= b & -(bit of a); b *= x.  About 160 VALU and no SALU, where the early-exit
+// loop of multmodp diverges across lanes and branches on every bit.
+__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 31; i >= 0; --i) {
+        p ^= b & (uint32_t)((int32_t)(a << (31 - i)) >> 31);  // bit i of a is x^(31-i)
+        if (i) b = (b >> 1) ^ (kPoly & (uint32_t)(-(int32_t)(b & 1u)));
+    }
+    return p;
+}
 __device__ __forceinline__ uint32_t z4096(const uint32_t *Tz, uint32_t a) {
     return Tz[a & 0xFF] ^ Tz[256 + ((a >> 8) & 0xFF)] ^ Tz[512 + ((a >> 16) & 0xFF)] ^ Tz[768 + (a >> 24)];
 }
@@ -897,7 +909,10 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, con
     return c;
 }
 
-__global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ arena,
+#ifndef GCK_FIN_WPE
+#define GCK_FIN_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint4 *__restrict__ rec_hdr,
                                                   const uint32_t *__restrict__ rec_file,
@@ -940,7 +955,7 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
         const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
         // A(rs) (0 when rs starts a row)
         const uint32_t dp = (uint32_t)(((rs + kRow - 1) & ~(uint64_t)(kRow - 1)) - rs);
-        const uint32_t a_rs = (prev_same && dp) ? pre_prev ^ (ft_prev ? multmodp(xfw[dp], ft_prev) : 0u) : 0u;
+        const uint32_t a_rs = (prev_same && dp) ? pre_prev ^ gf_mul(xfw[dp], ft_prev) : 0u;
         // ft of this record: from lane + 1 if that lane holds record r + 1 of the same file
         const uint64_t nb_same = __ballot(valid && prev_same);
         const uint32_t ft_next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ft_prev, 0x130, 0xF, 0xF, false);  // wave_shl:1
@@ -973,7 +988,7 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
             acc ^= z4096(Tz, h_acc);
         }
         // F(0, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
-        const uint32_t chain = ft ^ (acc ? multmodp(xinv[d], acc) : 0u);
+        const uint32_t chain = ft ^ gf_mul(xinv[d], acc);
         // F(0, prefix): header + key bytes [rs, vs) as aligned words from
         // rs & ~3, the bytes before rs masked to zero (F ignores leading zeros)
         const uint64_t w0 = rs & ~3ull;
@@ -983,15 +998,21 @@ __global__ __launch_bounds__(256) void k_finalize(const uint8_t *__restrict__ ar
 #pragma unroll
         for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
         pw[0] &= ~0u << (8 * lead);
-        uint32_t p = 0;
-        for (uint32_t i = 0; i < L / 4; ++i) p = slice4t(T, p ^ (i < 11 ? pw[i] : wp[i]));
-        if (L & 3) {
-            const uint32_t y = L / 4 < 11 ? pw[L / 4] : wp[L / 4];
-            p = partial_word(T, p, y, L & 3);  // L >= 16: never the masked word
+        // unrolled over the words in registers (no indexed register array),
+        // then the words of long keys from memory
+        const uint32_t nw = L / 4;
+        uint32_t p = 0, y = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 11; ++i) {
+            if (i < nw) p = slice4t(T, p ^ pw[i]);
+            y = i == nw ? pw[i] : y;
         }
-        const uint32_t xv = V < 65536 ? xb[V] : multmodp(xa[V >> 16], xb[V & 0xFFFF]);
-        const uint32_t raw0 = chain ^ (p ? multmodp(xv, p) : 0u);
-        const uint32_t z = V < (1u << 17) ? zl[V] : multmodp(xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        for (uint32_t i = 11; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
+        if (nw >= 11) y = wp[nw];
+        if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
+        const uint32_t xv = V < 65536 ? xb[V] : gf_mul(xa[V >> 16], xb[V & 0xFFFF]);
+        const uint32_t raw0 = chain ^ gf_mul(xv, p);
+        const uint32_t z = V < (1u << 17) ? zl[V] : gf_mul(xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         const uint32_t calc = raw0 ^ z;
         if (valid) {
             const uint64_t fo = rs - fbase[f];
@@ -1097,6 +1118,9 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     }
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
+    int bpc = 0;
+    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), 256, 0));
+    c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
@@ -1307,8 +1331,10 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
 
 static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
     if (!max_recs) return;
-    const uint64_t want = nblk(max_recs, 256);
-    const uint32_t grid = (uint32_t)(want < (uint64_t)c->n_cu * 8 ? want : (uint64_t)c->n_cu * 8);
+    // one wave of workgroups that are all resident at once (a second, partial
+    // round of workgroups would double the kernel's latency-bound time)
+    const uint64_t want = nblk(max_recs, 256), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
+    const uint32_t grid = (uint32_t)(want < res ? want : res);
     k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),

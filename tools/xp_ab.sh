@@ -1,6 +1,9 @@
-# A/B two builds of the library on the same box (box-to-box variance is large).
+# A/B builds of the library on one box (box-to-box variance is large):
+#   bash tools/xp_ab.sh lib1.so lib2.so ...   (each run twice, interleaved)
 set -e
-for lib in gocask_amd/libgocask_hip.so gocask_amd/var/libgocask_hip_plan.so gocask_amd/libgocask_hip.so gocask_amd/var/libgocask_hip_plan.so; do
+for rep in 1 2; do
+for lib in "$@"; do
   echo "LIB=$lib"
-  GCK_X_MODE=2 GCK_LIB_PATH=$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps 5 --warmup 2 | python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['ms_per_step'], {k: round(v,3) for k,v in d['phase_ms'].items()})"
+  GCK_LIB_PATH=$lib timeout -k 10 120 python bench.py --no-cpu-baseline --steps 5 --warmup 2 | python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(d['ms_per_step'], {k: round(v,3) for k,v in d['phase_ms'].items()})"
+done
 done
