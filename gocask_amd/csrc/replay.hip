@@ -43,6 +43,7 @@ constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
@@ -100,10 +101,17 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
     uint32_t n = 0;
     term = T_NONE;
     tpos = 0;
+    // Software-pipelined: the next header's loads are issued before this
+    // record's stores, so a hop waits for one load latency, never for the
+    // previous hop's store acknowledgements (vmcnt counts both, in order).
+    // base / len are consumed here, before the loop, so no load issued
+    // outside the loop is still pending inside it.
+    const uint64_t a0 = base + (p < len ? p : 0);
+    Hdr h = ld_hdr(arena, a0);
+    emit.prime();  // the loop is entered with the back edge's queue shape
     while (p < ce) {
         const uint64_t rem = len - p;
         if (rem < 16) { term = T_ERR; tpos = p; break; }            // ErrUnexpectedEOF
-        const Hdr h = ld_hdr(arena, base + p);
         const uint32_t klen = h.ks ? h.ks : h.vs;                    // db.go:151-155
         const uint64_t rem2 = rem - 16;
         if (klen > 0 && rem2 == 0) { term = T_SILENT; tpos = p; break; }  // ReadFull io.EOF
@@ -115,9 +123,13 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
             if (rem2 - klen < h.vs) { term = T_SILENT; tpos = p; break; }  // Discard io.EOF
             next = p + 16 + (uint64_t)h.ks + h.vs;
         }
+        // the next header (the arena is padded: a read at the file end or
+        // just past the chunk stays in bounds and is never used)
+        const Hdr hn = ld_hdr(arena, base + (next < len ? next : 0));
         emit(n, p, h);
         ++n;
         p = next;
+        h = hn;
     }
     count = n;
     exit = p;
@@ -237,15 +249,22 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     if (lane == 0) ch_entry[c] = found;
 }
 
+// The stage of a chunk: cap slots + 1 scratch slot (records past cap land
+// there; k_compact re-walks such chunks).  Every hop stores, so the number of
+// stores per hop is fixed and the next header's load wait counts them.
 struct ScratchEmit {
     uint64_t *off;
     uint4 *hdr;
     uint32_t cap;
     __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
-        if (i < cap) {
-            off[i] = p;
-            hdr[i] = make_uint4(h.crc, h.ts, h.ks, h.vs);
-        }
+        const uint32_t k = i < cap ? i : cap;
+        off[k] = p;
+        hdr[k] = make_uint4(h.crc, h.ts, h.ks, h.vs);
+    }
+    // the stores of one hop, to the scratch slot
+    __device__ void prime() const {
+        off[cap] = 0;
+        hdr[cap] = make_uint4(0, 0, 0, 0);
     }
 };
 
@@ -256,7 +275,7 @@ __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_
     uint32_t count = 0, term = T_NONE;
     uint64_t exit = kNone, tpos = 0;
     if (entry != kNone) {
-        ScratchEmit em{s_off + (uint64_t)c * cap, s_hdr + (uint64_t)c * cap, cap};
+        ScratchEmit em{s_off + (uint64_t)c * (cap + 1), s_hdr + (uint64_t)c * (cap + 1), cap};
         walk_chain(arena, fbase[f], flen[f], ce, entry, em, count, exit, term, tpos);
     }
     ch_count[c] = count;
@@ -452,6 +471,7 @@ struct DirectEmit {
             rec_file[r] = f;
         }
     }
+    __device__ void prime() const {}
 };
 
 // Record table in walk order: one wavefront per chunk copies its staged
@@ -481,7 +501,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ are
         for (uint32_t i = lane; i < cnt; i += 64) {
             const uint64_t r = rb + i;
             if (r >= n_total) break;
-            const uint64_t si = (uint64_t)c * cap + i;
+            const uint64_t si = (uint64_t)c * (cap + 1) + i;
             rec_off[r] = base + s_off[si];
             rec_hdr[r] = s_hdr[si];
             rec_file[r] = f;
@@ -668,12 +688,23 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
-    const uint32_t nbase = kNibBase + (lane >> 5) * 4096 + l31;
+    const uint32_t nbyte = (kNibBase + (lane >> 5) * 4096 + l31) * 4;  // the lane's shift table (bytes)
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     const uint32_t s_rel = lane * kSlab;
     const uint64_t n_blocks = (n_rows + kBlockRows - 1) / kBlockRows;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
-    const uint64_t scratch = n_total + (uint64_t)(wid & 255) * 64 + lane;  // this lane's scratch slot
+    // (c, pre) stores go through a buffer resource based at the block's first
+    // record: lanes without a record end store at an out-of-range offset, which
+    // the bounds check drops (no traffic), while every lane still issues the
+    // store (a fixed count for the compiler's vmcnt waits)
+    constexpr uint32_t kDrop = 0xFFFFFFF0u;
+    __amdgpu_buffer_rsrc_t ep_rsrc = make_rsrc(out_ep, 0x7FFFFFF0);
+    uint32_t ra0 = 0;
+    auto store_ep = [&](uint32_t off, uint32_t cv, uint32_t pv) {
+        u32x2 v;
+        v.x = cv;
+        v.y = pv;
+        __builtin_amdgcn_raw_buffer_store_b64(v, ep_rsrc, (int)off, 0, 0);
+    };
 
     auto grab = [&]() -> uint32_t {  // next block index from the queue
         uint32_t v = 0;
@@ -753,29 +784,51 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 }
             }
         }
+        // Z_{64(63-lane)}(G) of every row (8 nibble lookups in the lane's
+        // table; address = (nibble << 7) | base, the base's bits 7..10 are
+        // zero), then the NR wave scans interleaved so each DPP read finds
+        // its source written a few instructions earlier (no s_nop hazards)
+        uint32_t P[NR], pre[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            const uint64_t row = row0 + i;
-            const uint32_t j = j0 + i;
-            // Z_{64(63-lane)}(G): the slab referenced to the row end
-            uint32_t pre = 0, rrow = G[i];
             if constexpr ((MODE & 4) == 0) {
                 uint32_t t[8];
 #pragma unroll
-                for (int qn = 0; qn < 8; ++qn) t[qn] = lds[nbase + qn * 512 + (((G[i] >> (4 * qn)) & 15u) << 5)];
-                // inclusive prefix XOR over the wave (DPP row shifts + row broadcasts)
-                uint32_t P = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
-                P ^= dpp<0x111, 0xF>(P);  // row_shr:1
-                P ^= dpp<0x112, 0xF>(P);  // row_shr:2
-                P ^= dpp<0x114, 0xF>(P);  // row_shr:4
-                P ^= dpp<0x118, 0xF>(P);  // row_shr:8
-                P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
-                P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
-                pre = dpp<0x138, 0xF>(P);  // wave_shr:1 -> exclusive (lane 0: 0)
-                rrow = P;
+                for (int qn = 0; qn < 8; ++qn) {
+                    const uint32_t sh = 4 * qn;
+                    const uint32_t x = sh >= 7 ? G[i] >> (sh - 7) : G[i] << (7 - sh);
+                    t[qn] = lds_at(lds, (x & 0x780u) | (nbyte + qn * 2048));
+                }
+                P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+            } else {
+                P[i] = G[i];
             }
-            // blocks of this slab holding a record end (0 past the last row)
-            const uint32_t m = row < n_rows ? (nib >> (4 * i)) & 15u : 0u;
+        }
+        if constexpr ((MODE & 4) == 0) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);  // row_shr:1
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);  // row_shr:2
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);  // row_shr:4
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);  // row_shr:8
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);  // row_bcast:15 -> rows 1, 3
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);  // row_bcast:31 -> rows 2, 3
+#pragma unroll
+            for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);  // wave_shr:1 -> exclusive (lane 0: 0)
+        } else {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) pre[i] = 0;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const uint32_t j = j0 + i;
+            // blocks of this slab holding a record end (the plan is zero past
+            // the last row)
+            const uint32_t m = (nib >> (4 * i)) & 15u;
             const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
             // the register at the start of block b (selects, no branches)
             auto cap = [&](uint32_t b) {
@@ -784,14 +837,14 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 return b == 0 ? 0u : v;
             };
             if constexpr ((MODE & 16) != 0) {
-                asm volatile("" ::"v"(m), "v"(pre), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
+                asm volatile("" ::"v"(m), "v"(pre[i]), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
             } else if (__ballot(m & (m - 1)) == 0) {
                 // common case: at most one record end per slab, its slot is
                 // ra + (cut lanes before)
                 const uint64_t C = __ballot(m != 0);
                 const uint32_t idx =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-                out_ep[m ? (uint64_t)ra + idx : scratch] = make_uint2(cap((uint32_t)__builtin_ctz(m | 16u)), pre);
+                store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
             } else {
                 // a slab with 2..4 record ends (records under 64 B): ids by
                 // an exclusive count over the lanes, four stores per lane
@@ -800,12 +853,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 uint32_t mm = m;
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
-                    out_ep[q < n ? (uint64_t)ra + ex + q : scratch] =
-                        make_uint2(cap((uint32_t)__builtin_ctz(mm | 16u)), pre);
+                    store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
                     mm &= mm - 1;
                 }
             }
-            rend_buf = lane == j ? (uint32_t)__builtin_amdgcn_readlane((int)rrow, 63) : rend_buf;
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P[i], 63);  // F(0, row)
+            rend_buf = lane == j ? total : rend_buf;
         }
     };
 
@@ -824,6 +877,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         const uint64_t qnn = grab();
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
+        ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
+        ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
         const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
         // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
         // lane; the two row buffers alternate, so each has fixed registers
@@ -1092,9 +1147,9 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
 static int ctx_init(Ctx *c, const gck_opts *o) {
     gck_opts d{};
     d.device = 0;
-    d.chunk_bytes = 256 << 10;
+    d.chunk_bytes = 512 << 10;
     d.max_key = 65536;
-    d.chunk_cap = 256;
+    d.chunk_cap = 1024;
     if (o) {
         d.device = o->device;
         if (o->chunk_bytes) d.chunk_bytes = o->chunk_bytes;
@@ -1207,8 +1262,8 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * cap * 8)) ||
-        (rc = c->d_scratch_hdr.ensure((nc + 1) * cap * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * (cap + 1) * 8)) ||
+        (rc = c->d_scratch_hdr.ensure((nc + 1) * (cap + 1) * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_plan.ensure((c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
         return rc;
@@ -1250,8 +1305,8 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
                                         c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
                                         c->d_ch_exit.as<uint64_t>() + c0, c->d_ch_term.as<uint32_t>() + c0,
                                         c->d_ch_tpos.as<uint64_t>() + c0,
-                                        c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * cap,
-                                        c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * cap, cap, n);
+                                        c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * (cap + 1),
+                                        c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * (cap + 1), cap, n);
     for (int r = 0; r <= kRounds; ++r) {
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
                                                 c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
@@ -1299,8 +1354,8 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_ch_file.as<uint32_t>() + c0, c->d_ch_end.as<uint64_t>() + c0,
                                              c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
                                              c->d_rec_base.as<uint64_t>() + c0,
-                                             c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * ccap,
-                                             c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * ccap, ccap, n, cap,
+                                             c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * (ccap + 1),
+                                             c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * (ccap + 1), ccap, n, cap,
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                              c->d_rec_file.as<uint32_t>(), c->d_counters.as<uint32_t>());
     const uint32_t grid = (uint32_t)c->n_cu * 4;
