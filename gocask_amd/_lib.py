@@ -92,7 +92,8 @@ class GckStats(ctypes.Structure):
         ("n_overflow", ctypes.c_uint64),
         ("ms_total", ctypes.c_double),
         ("ms_kernel", ctypes.c_double * 12),
-        ("reserved", ctypes.c_uint32 * 2),
+        ("device_path", ctypes.c_uint32),
+        ("n_reruns", ctypes.c_uint32),
     ]
 
 

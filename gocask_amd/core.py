@@ -306,7 +306,8 @@ class ReplayContext:
                 break
             phases[name] = s.ms_kernel[i]
         return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
-                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases)
+                    n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
+                    device_path=bool(s.device_path), n_reruns=s.n_reruns)
 
     def stream_read_ceiling(self, iters=10):
         """Plain streaming read of the resident arena: (ms per pass, GB/s)."""

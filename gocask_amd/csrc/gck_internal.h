@@ -97,6 +97,8 @@ struct Ctx {
     int32_t status = 0;
     uint32_t err_file = 0, files_walked = 0, final_last_offset = 0;
     uint64_t err_off = 0, n_crc_fail = 0, n_fixups = 0, n_overflow = 0;
+    bool device_path = false;  // the last run had no host round trip (ctx_run_device)
+    uint32_t n_reruns = 0;     // device-only runs redone on the host path
     double ms_total = 0, ms_phase[PH_NPHASE] = {};
     hipEvent_t ev[PH_END + 1] = {};
 

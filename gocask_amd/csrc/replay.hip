@@ -457,6 +457,44 @@ __global__ void k_file_summary(const uint32_t *__restrict__ f_first_chunk,
     f_tpos[f] = tpos;
 }
 
+// The host bookkeeping of a run (core/db.go:110-140), on the device so a run
+// needs no host round trip: per file the lastOffset carried in (reset after
+// every file but the active one, core/db.go:117-119), the first startup error
+// (it aborts filepath.Walk: later files contribute nothing, disk.go:134-141),
+// the run's record range and the final lastOffset.  One thread; res (u64):
+// 0 status, 1 error file, 2 error offset, 3 files walked, 4 final lastOffset,
+// 5 records (unclamped).  rng[1] = min(records, cap).
+__global__ void k_account(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
+                          const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
+                          const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec,
+                          uint32_t *__restrict__ carry, uint64_t *__restrict__ rng, uint64_t cap,
+                          uint64_t *__restrict__ res) {
+    uint32_t last = 0, status = GCK_OK, err_file = 0, walked = nf;
+    uint64_t err_off = 0, n_total = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+        carry[f] = last;
+        const uint64_t valid = fterm[f] != T_NONE ? ftpos[f] : flen[f];
+        n_total = ffirst[f] + fnrec[f];
+        last += (uint32_t)valid;
+        if (fterm[f] == T_ERR) {
+            status = GCK_EUNEXPECTED_EOF;
+            err_file = f;
+            err_off = ftpos[f];
+            walked = f + 1;
+            break;
+        }
+        if (freset[f]) last = 0;
+    }
+    rng[0] = 0;
+    rng[1] = n_total < cap ? n_total : cap;
+    res[0] = status;
+    res[1] = err_file;
+    res[2] = err_off;
+    res[3] = walked;
+    res[4] = last;
+    res[5] = n_total;
+}
+
 struct DirectEmit {
     uint64_t *rec_off;
     uint4 *rec_hdr;
@@ -1185,7 +1223,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xfw.ensure(xfw.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
-        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(64)))
+        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(128)))
         return rc;
     GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
@@ -1460,7 +1498,7 @@ static int read_file_summaries(Ctx *c, hipStream_t s, std::vector<uint32_t> &fte
 // verdicts, carries).  The CRC pass needs the record boundaries (its plan),
 // and running the latency-bound boundary kernels beside an HBM-saturating
 // pass slows them ~7x (loaded latency), so the phases do not overlap.
-static int ctx_run(Ctx *c) {
+static int ctx_run_host(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -1515,8 +1553,11 @@ static int ctx_run(Ctx *c) {
     c->n_recs = n_total;
     if (n_total > 0xFFFFFFF0ull) return GCK_EINVAL;
     int rc;
-    if ((rc = ensure_records(c, n_total))) return rc;
-    c->rec_cap = n_total;
+    // capacity for the records of every file, also those after a startup
+    // error (a later device-only run stages them before it learns of the error)
+    const uint64_t all = nf ? std::max<uint64_t>(n_total, ffirst[nf - 1] + fnrec[nf - 1]) : n_total;
+    if ((rc = ensure_records(c, all))) return rc;
+    c->rec_cap = all;
     const uint64_t rng_h[2] = {0, n_total};
     if (nf) GCK_HIP(hipMemcpyAsync(c->d_carry.p, carry.data(), nf * 4, hipMemcpyHostToDevice, s));
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
@@ -1544,6 +1585,81 @@ static int ctx_run(Ctx *c) {
     c->ms_phase[PH_PIPE] = span;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
+}
+
+// The same run with no host round trip, for a context whose record table
+// was sized by an earlier run (repeated replays of a resident arena): the
+// bookkeeping runs on the device (k_account), the record table is clamped to
+// its capacity, and one copy at the end brings back counters and results.
+// Returns GCK_ERERUN when the run cannot be trusted as is (more records than
+// capacity, or speculation not settled by the device rounds): the caller then
+// reruns on the host path, whose result is exact.
+constexpr int GCK_ERERUN = -1;
+static int ctx_run_device(Ctx *c) {
+    const auto t0 = std::chrono::steady_clock::now();
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint32_t nc = c->n_chunks, nf = c->nfiles;
+    const uint64_t cap = c->rec_cap;
+    uint32_t *cnt = c->d_counters.as<uint32_t>();
+    uint64_t *gbase = c->d_gbase.as<uint64_t>();
+    uint64_t *res = c->d_counters.as<uint64_t>() + 8;
+    GCK_HIP(hipMemsetAsync(cnt, 0, 128, s));
+    GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
+    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
+    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
+    launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
+    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
+    launch_scan(c, s, 0, nc, 0, nf, gbase, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
+    k_account<<<1, 1, 0, s>>>(nf, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(), c->d_fterm.as<uint32_t>(),
+                              c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
+                              c->d_carry.as<uint32_t>(), gbase, cap, res);
+    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
+    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
+    int rc;
+    if ((rc = launch_crc(c, s, 0, c->n_rows, cap))) return rc;
+    GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
+    launch_finalize(c, s, gbase, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_END], s));
+    uint32_t h[32] = {};
+    GCK_HIP(hipMemcpyAsync(h, cnt, 128, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    GCK_HIP(hipGetLastError());
+    const uint64_t *hr = reinterpret_cast<const uint64_t *>(h + 16);
+    if (h[CNT_VAL + kRounds] != 0 || h[CNT_CAP] != 0 || hr[5] > cap) return GCK_ERERUN;
+    c->status = (int32_t)hr[0];
+    c->err_file = (uint32_t)hr[1];
+    c->err_off = hr[2];
+    c->files_walked = (uint32_t)hr[3];
+    c->final_last_offset = (uint32_t)hr[4];
+    c->n_recs = hr[5];
+    c->n_fixups = h[CNT_FIXUP];
+    c->n_overflow = h[CNT_STAGE];
+    c->n_crc_fail = h[CNT_REJECT];
+    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
+    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
+        c->ms_phase[p] = ms;
+    }
+    float span = 0;
+    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
+    c->ms_phase[PH_PIPE] = span;
+    c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->device_path = true;
+    return c->status;
+}
+
+static int ctx_run(Ctx *c) {
+    if (c->rec_cap > 0 && c->nfiles > 0) {
+        const int rc = ctx_run_device(c);
+        if (rc != GCK_ERERUN) return rc;
+        ++c->n_reruns;
+    }
+    c->device_path = false;
+    return ctx_run_host(c);
 }
 
 }  // namespace gck
@@ -1627,6 +1743,8 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->n_chunks = c->n_chunks;
     out->n_fixups = c->n_fixups;
     out->n_overflow = c->n_overflow;
+    out->device_path = c->device_path ? 1u : 0u;
+    out->n_reruns = c->n_reruns;
     out->ms_total = c->ms_total;
     for (int p = 0; p < PH_NPHASE && p < 12; ++p) out->ms_kernel[p] = c->ms_phase[p];
     return GCK_OK;

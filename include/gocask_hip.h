@@ -111,7 +111,8 @@ typedef struct gck_stats {
     uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
     double ms_total;        /* last gck_ctx_run wall time (host clock)                */
     double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
-    uint32_t reserved[2];
+    uint32_t device_path;   /* 1: the last run had no host round trip (record table sized by an earlier run) */
+    uint32_t n_reruns;      /* device-only runs redone on the host path (capacity / unsettled speculation)  */
 } gck_stats;
 
 int gck_ctx_create(const gck_opts *opts, gck_ctx **out);

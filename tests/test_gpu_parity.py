@@ -225,6 +225,61 @@ def test_stage_overflow_rewalks(g, orc):
     assert_same(got, gst, want, wst)
 
 
+# ---------------------------------- second run: no host round trip (device) ---
+def _run_twice(g, files, reset, **kw):
+    with g.ReplayContext(**kw) as ctx:
+        ctx.load(files, reset)
+        ctx.run()
+        first = ctx.fetch()
+        ctx.run()
+        second = ctx.fetch()
+        st = ctx.stats()
+    return first, second, st
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_golden_cases_device_path(g, orc, name):
+    # the second run of a context takes the device-only path (EOF verdicts,
+    # carries and the record count on the device): same answers as the oracle
+    meta, files, reset = load_case(name)
+    want, wst = orc.replay(files, reset)
+    (a, ast), (b, bst), st = _run_twice(g, files, reset)
+    assert_same(a, ast, want, wst)
+    assert_same(b, bst, want, wst)
+    if len(want):
+        assert st["device_path"] and st["n_reruns"] == 0
+
+
+def test_eof_classes_device_path(g, orc):
+    base = b"".join(orc_mod.entry(i, b"key%04d" % i, b"v" * (i % 97)) for i in range(300))
+    tails = [b"", b"\x01" * 9, struct.pack("<IIII", 0, 1, 5, 5) + b"ab", orc_mod.entry(1, b"kk", b"value")[:-2]]
+    for t in tails:
+        files = [base, t, base]
+        reset = [True, False, True]
+        want, wst = orc.replay(files, reset)
+        (a, ast), (b, bst), st = _run_twice(g, files, reset, chunk_bytes=4096)
+        assert_same(b, bst, want, wst)
+        assert st["device_path"]
+
+
+def test_device_path_capacity_rerun(g, orc):
+    # a context sized by a small corpus, then loaded with a larger one: the
+    # device-only run exceeds the record-table capacity and is redone on the
+    # host path, exactly
+    small = [b"".join(orc_mod.entry(i, b"k%d" % i, b"x" * 40) for i in range(100))]
+    big = [b"".join(orc_mod.entry(i, b"k%d" % i, b"y" * 30) for i in range(5000))]
+    want, wst = orc.replay(big, [True])
+    with g.ReplayContext(chunk_bytes=4096) as ctx:
+        ctx.load(small, [True])
+        ctx.run()
+        ctx.load(big, [True])
+        ctx.run()
+        got, gst = ctx.fetch()
+        st = ctx.stats()
+    assert st["n_reruns"] >= 1 and not st["device_path"]
+    assert_same(got, gst, want, wst)
+
+
 def test_tiny_records_and_empty_values(g, orc):
     rng = np.random.default_rng(7)
     recs = []
