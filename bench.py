@@ -65,6 +65,47 @@ def cpu_baseline(cfg_name, sample_bytes):
                        f" single-thread oracle replay + CRC verdict + hash-map keydir, {reps} pass(es)")
 
 
+def host_inclusive(g, ctx, info, steps):
+    """The path as the north star states it: files in (pinned, page-locked)
+    host memory, tuples back in host memory.  Times gck_ctx_load (H2D of
+    every file), gck_ctx_run and gck_ctx_fetch (D2H of the gck_rec tuples)."""
+    import numpy as np
+
+    nf = info["n_files"]
+    sizes = [int(info["sizes"][info["walk_order"][w]]) for w in range(nf)]
+    host = np.empty(sum(sizes), dtype=np.uint8)
+    g.host_register(host)
+    views, off = [], 0
+    for w, n in enumerate(sizes):
+        views.append(ctx.read_file(w, 0, n, out=host[off:off + n]))
+        off += n
+    reset = [w + 1 < nf for w in range(nf)]
+    recs = np.empty(ctx.stats()["n_recs"], dtype=g.REC_DTYPE)
+    g.host_register(recs)
+    t = dict(h2d=0.0, run=0.0, d2h=0.0)
+    n_recs = 0
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        ctx.load(views, reset)
+        t1 = time.perf_counter()
+        ctx.run()
+        t2 = time.perf_counter()
+        n_recs = ctx.fetch_into(recs)
+        t3 = time.perf_counter()
+        t["h2d"] += t1 - t0
+        t["run"] += t2 - t1
+        t["d2h"] += t3 - t2
+    g.host_unregister(host)
+    g.host_unregister(recs)
+    total = sum(t.values())
+    return dict(value=round(host.nbytes * steps / total / GiB, 3), unit="GiB/s", steps=steps,
+                ms_per_step=round(total / steps * 1e3, 2),
+                h2d_ms=round(t["h2d"] / steps * 1e3, 2), run_ms=round(t["run"] / steps * 1e3, 2),
+                d2h_ms=round(t["d2h"] / steps * 1e3, 2), tuple_bytes=n_recs * 40,
+                note="files in pinned host buffers (gck_host_register) -> gck_ctx_load (H2D) -> gck_ctx_run "
+                     "-> gck_ctx_fetch_into (D2H of the gck_rec tuples into a pinned array)")
+
+
 def shard_config(cfg_name, rank):
     """The corpus rank `rank` replays: its own C3-shaped shard of independent
     files (seed + rank), so no data-path collective is needed."""
@@ -96,6 +137,8 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
+                    help="also time K host-in/host-out replays (pinned H2D + run + D2H of the tuples)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,6 +237,8 @@ def main():
             },
             "phase_ms": {k: round(v / args.steps, 4) for k, v in phases_sum.items()},
         }
+        if args.host_inclusive:
+            out["host_inclusive"] = host_inclusive(g, ctx, info, args.host_inclusive)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config, int(args.cpu_sample_gib * GiB))
         if args.verbose:

@@ -223,6 +223,15 @@ def _result(res: GckResult):
                       files_walked=res.files_walked)
 
 
+def host_register(arr):
+    """Pin a host numpy buffer (gck_host_register) for DMA-rate transfers."""
+    check(_lib.load().gck_host_register(arr.ctypes.data, arr.nbytes))
+
+
+def host_unregister(arr):
+    check(_lib.load().gck_host_unregister(arr.ctypes.data))
+
+
 def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
@@ -296,6 +305,13 @@ class ReplayContext:
         finally:
             self._L.gck_result_free(ctypes.byref(res))
 
+    def fetch_into(self, recs):
+        """Tuples of the last run into a REC_DTYPE array (gck_ctx_fetch_into);
+        returns the number of records."""
+        n = ctypes.c_uint64()
+        check(self._L.gck_ctx_fetch_into(self._h, recs.ctypes.data, recs.size, ctypes.byref(n)))
+        return n.value
+
     def stats(self):
         s = GckStats()
         check(self._L.gck_ctx_stats(self._h, ctypes.byref(s)))
@@ -316,9 +332,9 @@ class ReplayContext:
         check(self._L.gck_diag_stream_read(self._h, iters, ctypes.byref(ms), ctypes.byref(gbs)))
         return ms.value, gbs.value
 
-    def read_file(self, file, off=0, length=None):
+    def read_file(self, file, off=0, length=None, out=None):
         n = length
-        buf = np.zeros(n, dtype=np.uint8)
+        buf = np.zeros(n, dtype=np.uint8) if out is None else out
         if n:
             check(self._L.gck_ctx_read_file(self._h, file, off, buf.ctypes.data, n))
         return buf

@@ -1725,10 +1725,25 @@ int gck_ctx_fetch(gck_ctx *ctx, gck_result *out) {
     out->err_off = c->err_off;
     out->files_walked = c->files_walked;
     if (c->n_recs) {
-        out->recs = static_cast<gck_rec *>(malloc(c->n_recs * sizeof(gck_rec)));
-        if (!out->recs) return GCK_ENOMEM;
+        // pinned host memory: the D2H copy runs at DMA rate (and the caller
+        // frees it with gck_result_free)
         GCK_HIP(hipSetDevice(c->device));
+        void *h = nullptr;
+        if (hipHostMalloc(&h, c->n_recs * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) return GCK_ENOMEM;
+        out->recs = static_cast<gck_rec *>(h);
         GCK_HIP(hipMemcpy(out->recs, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost));
+    }
+    return GCK_OK;
+}
+
+int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n) {
+    if (!ctx || !n || (cap && !dst)) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    *n = c->n_recs;
+    if (c->n_recs > cap) return GCK_EINVAL;
+    if (c->n_recs) {
+        GCK_HIP(hipSetDevice(c->device));
+        GCK_HIP(hipMemcpy(dst, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost));
     }
     return GCK_OK;
 }
@@ -1791,9 +1806,21 @@ int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck
 
 void gck_result_free(gck_result *res) {
     if (!res) return;
-    free(res->recs);
+    if (res->recs) (void)hipHostFree(res->recs);
     res->recs = nullptr;
     res->n = 0;
+}
+
+int gck_host_register(const void *p, uint64_t len) {
+    if (!p || !len) return GCK_EINVAL;
+    GCK_HIP(hipHostRegister(const_cast<void *>(p), len, hipHostRegisterDefault));
+    return GCK_OK;
+}
+
+int gck_host_unregister(const void *p) {
+    if (!p) return GCK_EINVAL;
+    GCK_HIP(hipHostUnregister(const_cast<void *>(p)));
+    return GCK_OK;
 }
 
 int gck_device_count(void) {

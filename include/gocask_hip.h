@@ -85,7 +85,7 @@ typedef struct gck_opts {
 
 
 typedef struct gck_result {
-    gck_rec *recs;              /* library-owned host array; free with gck_result_free  */
+    gck_rec *recs;              /* library-owned pinned host array; free with gck_result_free */
     uint64_t n;                 /* records in recs                                      */
     uint64_t n_crc_fail;        /* records whose verdict is a reject                    */
     uint32_t final_last_offset; /* keyDir.lastOffset after replay (later Puts use it)   */
@@ -123,6 +123,10 @@ int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles);
 int gck_ctx_run(gck_ctx *ctx);
 /* Copy the tuples of the last run to host memory. */
 int gck_ctx_fetch(gck_ctx *ctx, gck_result *out);
+/* Copy the tuples of the last run into caller memory (dst holds cap records;
+ * register it with gck_host_register for DMA rate); *n = records of the run.
+ * GCK_EINVAL (and nothing copied) when cap < *n. */
+int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 int gck_ctx_stats(gck_ctx *ctx, gck_stats *out);
 const char *gck_phase_name(int phase);
 /* Device pointers of the last run's outputs (gck_rec array, n records) and the
@@ -205,6 +209,11 @@ void gck_db_close(gck_db *db);
 
 /* Library/device info. */
 int gck_device_count(void);
+/* Pin (page-lock) caller memory, e.g. mmap'd data files, so gck_ctx_load /
+ * gck_replay copy it by DMA at PCIe rate instead of through staging buffers;
+ * unregister before unmapping.  Thin wrappers over hipHostRegister. */
+int gck_host_register(const void *p, uint64_t len);
+int gck_host_unregister(const void *p);
 const char *gck_version(void);
 /* Text of the last HIP failure on this thread (GCK_EDEVICE diagnostics). */
 const char *gck_last_error(void);

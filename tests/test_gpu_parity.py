@@ -280,6 +280,35 @@ def test_device_path_capacity_rerun(g, orc):
     assert_same(got, gst, want, wst)
 
 
+def test_pinned_host_load_and_fetch_into(g, orc):
+    # the host-inclusive path of bench.py: files in registered (pinned) host
+    # memory, tuples copied into a registered REC_DTYPE array
+    kw = dict(seed=45, val_fixed=0, key_min=8, key_max=24, key_universe=5000, tomb_permille=10,
+              flip_permille=10, max_file_size=2 << 20, n_files=3)
+    files, names = orc.gen_corpus(**kw)
+    wf, reset = walk_sorted(files, names)
+    want, wst = orc.replay(wf, reset)
+    host = np.concatenate([np.frombuffer(f, np.uint8) for f in wf])
+    g.host_register(host)
+    views, off = [], 0
+    for f in wf:
+        views.append(host[off:off + len(f)])
+        off += len(f)
+    recs = np.zeros(len(want) + 5, dtype=g.REC_DTYPE)
+    g.host_register(recs)
+    try:
+        with g.ReplayContext() as ctx:
+            ctx.load(views, reset)
+            ctx.run()
+            n = ctx.fetch_into(recs)
+            _, gst = ctx.fetch()
+    finally:
+        g.host_unregister(host)
+        g.host_unregister(recs)
+    assert n == len(want)
+    assert_same(recs[:n], gst, want, wst)
+
+
 def test_tiny_records_and_empty_values(g, orc):
     rng = np.random.default_rng(7)
     recs = []
