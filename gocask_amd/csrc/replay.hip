@@ -457,6 +457,19 @@ __global__ void k_file_summary(const uint32_t *__restrict__ f_first_chunk,
     f_tpos[f] = tpos;
 }
 
+// Zero the run's counters / results (32 u32), record range, row_first[0]
+// and the CRC block queue: one launch instead of four memsets.
+__global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ rng, uint32_t *__restrict__ row_first,
+                           uint32_t *__restrict__ queue) {
+    const uint32_t t = threadIdx.x;
+    if (t < 32) cnt[t] = 0;
+    if (t < 2) rng[t] = 0;
+    if (t == 0) {
+        row_first[0] = 0;
+        *queue = 0;
+    }
+}
+
 // The host bookkeeping of a run (core/db.go:110-140), on the device so a run
 // needs no host round trip: per file the lastOffset carried in (reset after
 // every file but the active one, core/db.go:117-119), the first startup error
@@ -1408,12 +1421,12 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
 
 // CRC partials of rows [r0, r1) (k_crc_rows).  Record-slot scratch: cap ..
 // cap + kEpScratch; rend scratch: rows n_rows ...
-static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap) {
+static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, bool queue_zeroed = false) {
     if (r1 <= r0) return GCK_OK;
     const uint64_t nb = (r1 - r0 + kBlockRows - 1) / kBlockRows;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>();
-    GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
+    if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
         c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16,
         c->d_row_first.as<uint32_t>() + r0, cap,
@@ -1604,9 +1617,7 @@ static int ctx_run_device(Ctx *c) {
     uint32_t *cnt = c->d_counters.as<uint32_t>();
     uint64_t *gbase = c->d_gbase.as<uint64_t>();
     uint64_t *res = c->d_counters.as<uint64_t>() + 8;
-    GCK_HIP(hipMemsetAsync(cnt, 0, 128, s));
-    GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
-    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
+    k_run_init<<<1, 64, 0, s>>>(cnt, gbase, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
     launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
@@ -1619,7 +1630,7 @@ static int ctx_run_device(Ctx *c) {
     launch_records(c, s, 0, nc, 0, c->n_rows, gbase, cap);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
     int rc;
-    if ((rc = launch_crc(c, s, 0, c->n_rows, cap))) return rc;
+    if ((rc = launch_crc(c, s, 0, c->n_rows, cap, true))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, cap);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
