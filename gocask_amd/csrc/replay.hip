@@ -147,9 +147,9 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {
 // at p with KeySize <= 65535 (tombstones: KeySize 0) has bytes p+10 and p+11
 // zero, so the lane flags positions whose bytes 10, 11 are a zero pair (about
 // 2 VALU per position; in value bytes a zero pair is rare) and only flagged
-// positions get the full chain test.  A hit at p is replaced by p+1 when p+1
-// chains too: every true header has a plausible "shadow" one byte earlier
-// (Timestamp's top byte + KeySize<<8, ValueSize<<8).  Keys longer than 65535
+// positions get the full chain test.  A hit at p is replaced by p+k (k <= 3,
+// the largest that chains): a true header has plausible "shadows" 1..3 bytes
+// earlier (Timestamp's top bytes + KeySize shifted).  Keys longer than 65535
 // bytes are never speculated here; validation finds their chunks and re-walks.
 __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ fbase,
@@ -244,7 +244,18 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
             }
             from = wb + 4096;
         }
-        if (found != kNone && found + 1 < ce && chain_ok(arena, base, len, found + 1, mk)) found += 1;
+        // shadows: a true header is preceded by plausible ones 1..3 bytes
+        // earlier (a tombstone's 2-byte shadow has KeySize = the timestamp's
+        // high half and can re-sync onto the true chain after one hop), so
+        // the latest chaining position within 3 bytes wins
+        if (found != kNone) {
+#pragma unroll 1
+            for (uint32_t k = 3; k >= 1; --k)
+                if (found + k < ce && chain_ok(arena, base, len, found + k, mk)) {
+                    found += k;
+                    break;
+                }
+        }
     }
     if (lane == 0) ch_entry[c] = found;
 }
