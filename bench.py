@@ -137,6 +137,7 @@ def main():
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--keydir", action="store_true", help="also time the device keydir (gck_ctx_keydir)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
                     help="also time K host-in/host-out replays (pinned H2D + run + D2H of the tuples)")
     args = ap.parse_args()
@@ -240,6 +241,12 @@ def main():
             },
             "phase_ms": {k: round(v / n_phase, 4) for k, v in phases_sum.items()},
         }
+        if args.keydir:
+            ctx.keydir()  # warm-up (allocations)
+            live, kd_ms = ctx.keydir()
+            out["keydir"] = dict(ms=round(kd_ms, 3), live_entries=len(live), records=st["n_recs"],
+                                 note="gck_ctx_keydir after a run (row f1): last record per key, Puts kept; "
+                                      "not part of value")
         if args.host_inclusive:
             out["host_inclusive"] = host_inclusive(g, ctx, info, args.host_inclusive)
         if world == 1 and not args.no_cpu_baseline:

@@ -312,6 +312,17 @@ class ReplayContext:
         check(self._L.gck_ctx_fetch_into(self._h, recs.ctypes.data, recs.size, ctypes.byref(n)))
         return n.value
 
+    def keydir(self, keep_tombstones=False):
+        """Device keydir of the last run (gck_ctx_keydir + gck_ctx_fetch_keydir):
+        (live REC_DTYPE records in walk order, device ms)."""
+        n, ms = ctypes.c_uint64(), ctypes.c_double()
+        check(self._L.gck_ctx_keydir(self._h, 1 if keep_tombstones else 0, ctypes.byref(n), ctypes.byref(ms)))
+        recs = np.zeros(n.value, dtype=REC_DTYPE)
+        got = ctypes.c_uint64()
+        check(self._L.gck_ctx_fetch_keydir(self._h, recs.ctypes.data if n.value else None, n.value,
+                                           ctypes.byref(got)))
+        return recs, ms.value
+
     def stats(self):
         s = GckStats()
         check(self._L.gck_ctx_stats(self._h, ctypes.byref(s)))

@@ -93,6 +93,11 @@ struct Ctx {
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xfw, d_xa, d_xb, d_zrow, d_zl;
 
+    // device keydir (keydir.hip): key hashes, slot table, live flags, tile
+    // ranks, the live records
+    DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout;
+    uint64_t n_live = 0;
+
     // results of the last run
     int32_t status = 0;
     uint32_t err_file = 0, files_walked = 0, final_last_offset = 0;

@@ -1267,7 +1267,8 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
-                   &c->d_freset, &c->d_gbase, &c->d_queue};
+                   &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
+                   &c->d_kdout};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);

@@ -127,6 +127,17 @@ int gck_ctx_fetch(gck_ctx *ctx, gck_result *out);
  * register it with gck_host_register for DMA rate); *n = records of the run.
  * GCK_EINVAL (and nothing copied) when cap < *n. */
 int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
+
+/* Device keydir of the last run (replaces applying every
+ * record with keyDir.set / unset, core/keydir.go:22-49): for every key its
+ * last record in walk order, kept if it is a Put (with GCK_KD_KEEP_TOMBSTONES
+ * tombstones are kept too, as delete markers for a merge across shards).
+ * *n_live = the entries; *ms (optional) = device time.  The entries, in walk
+ * order of their records, are fetched with gck_ctx_fetch_keydir; a Go caller
+ * sets db.kd.entries[key] for each (key bytes at rec_off + 16 in the file). */
+#define GCK_KD_KEEP_TOMBSTONES 1u
+int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
+int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 int gck_ctx_stats(gck_ctx *ctx, gck_stats *out);
 const char *gck_phase_name(int phase);
 /* Device pointers of the last run's outputs (gck_rec array, n records) and the

@@ -280,6 +280,77 @@ def test_device_path_capacity_rerun(g, orc):
     assert_same(got, gst, want, wst)
 
 
+# ---------------------------------------------- device keydir (row f1) ---
+def _expected_keydir(files, want, keep_tombstones=False):
+    """Apply the oracle's records in walk order (core/keydir.go:22-49):
+    {key: record}; with keep_tombstones, the last record of every key."""
+    kd = {}
+    for r in want:
+        o = int(r["rec_off"]) + 16
+        key = bytes(files[int(r["file"])][o:o + int(r["key_len"])])
+        if int(r["flags"]) & 1 and not keep_tombstones:
+            kd.pop(key, None)
+        else:
+            kd.pop(key, None)  # re-insert: dict order = walk order of the winners
+            kd[key] = r
+    return kd
+
+
+def _check_keydir(files, got, kd):
+    assert len(got) == len(kd), (len(got), len(kd))
+    win = sorted(kd.values(), key=lambda r: (int(r["file"]), int(r["rec_off"])))
+    for a, b in zip(got, win):  # walk order of the winning records
+        for f in FIELDS:
+            assert a[f] == b[f], (f, a, b)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_keydir_golden(g, orc, name):
+    meta, files, reset = load_case(name)
+    want, wst = orc.replay(files, reset)
+    with g.ReplayContext() as ctx:
+        ctx.load(files, reset)
+        ctx.run()
+        live, _ = ctx.keydir()
+        every, _ = ctx.keydir(keep_tombstones=True)
+    _check_keydir(files, live, _expected_keydir(files, want))
+    _check_keydir(files, every, _expected_keydir(files, want, keep_tombstones=True))
+    # the reference's own known answers: the live keys of the fixture
+    if meta["status"] != "unexpected_eof":
+        keys = {bytes(files[int(r["file"])][int(r["rec_off"]) + 16:int(r["rec_off"]) + 16 + int(r["key_len"])])
+                for r in live}
+        assert keys == {k.encode() for k in meta["expect"]}
+
+
+@pytest.mark.parametrize("ci", range(len(CORPORA)))
+def test_keydir_random(g, orc, ci):
+    files, names = orc.gen_corpus(**CORPORA[ci])
+    wf, reset = walk_sorted(files, names)
+    want, wst = orc.replay(wf, reset)
+    with g.ReplayContext() as ctx:
+        ctx.load(wf, reset)
+        ctx.run()
+        live, _ = ctx.keydir()
+        every, _ = ctx.keydir(keep_tombstones=True)
+    _check_keydir(wf, live, _expected_keydir(wf, want))
+    _check_keydir(wf, every, _expected_keydir(wf, want, keep_tombstones=True))
+
+
+def test_keydir_c3_shape_device_encoded(g):
+    # C3 shape at 1/64 scale (16 rotated files, Zipf values, 1 % tombstones,
+    # a key universe of half the records): files read back from the device
+    kw = dict(seed=3, val_fixed=0, key_min=8, key_max=24, key_universe=80000, tomb_permille=10,
+              flip_permille=10, max_file_size=32 << 20, n_files=16)
+    with g.ReplayContext() as ctx:
+        info = ctx.encode(**kw)
+        ctx.run()
+        recs, st = ctx.fetch()
+        files = [ctx.read_file(w, 0, int(info["sizes"][info["walk_order"][w]])) for w in range(info["n_files"])]
+        live, ms = ctx.keydir()
+    assert st["status"] == 0 and len(recs) > 100000
+    _check_keydir(files, live, _expected_keydir(files, recs))
+
+
 def test_pinned_host_load_and_fetch_into(g, orc):
     # the host-inclusive path of bench.py: files in registered (pinned) host
     # memory, tuples copied into a registered REC_DTYPE array
