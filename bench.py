@@ -11,7 +11,9 @@ into HBM by the device encoder before timing starts.
 
 Each rank replays its own C3-shaped shard (16 x 2 GiB files, seed 3+rank):
 weak scaling, no data-path collective (files are independent).
-Rank 0 prints one JSON line.
+After the timed replays, N>1 runs also time the keydir merge across ranks (the
+path's one exchange step, RCCL all-to-all; reported as "keydir_merge", not
+part of value).  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -106,6 +108,35 @@ def host_inclusive(g, ctx, info, steps):
                      "-> gck_ctx_fetch_into (D2H of the gck_rec tuples into a pinned array)")
 
 
+def keydir_merge(g, ctx, dist, n_files, reps=2):
+    """N>1, after the timed replays: the exchange step of the sharded replay
+    (gocask_amd.shard.merge_keydir) -- per-rank keydir with
+    tombstones, hash partition, two RCCL all-to-alls, per-owner merge.  Not
+    part of `value`; the slowest rank's seconds of the last of `reps` runs."""
+    import torch
+
+    from gocask_amd import shard
+
+    base = shard.file_base(dist, n_files, device="cuda")
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_live, ph = shard.merge_keydir(ctx, dist, base)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+    v = torch.tensor([wall, ph["local"], ph["exchange"], ph["merge"]], dtype=torch.float64, device="cuda")
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    c = torch.tensor([n_live, ph["sent_bytes"]], dtype=torch.float64, device="cuda")
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    w, lo, ex, mg = (round(x * 1e3, 3) for x in v.tolist())
+    return dict(ms=w, local_ms=lo, exchange_ms=ex, merge_ms=mg, live_entries=int(c[0].item()),
+                exchanged_bytes=int(c[1].item()),
+                note="global keydir over all ranks' files: keydir with tombstones per rank, key-hash partition, "
+                     "RCCL all-to-all of entries + keys, per-owner last-shard-wins merge; max over ranks; "
+                     "not part of value")
+
+
 def shard_config(cfg_name, rank):
     """The corpus rank `rank` replays: its own C3-shaped shard of independent
     files (seed + rank), so no data-path collective is needed."""
@@ -138,6 +169,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--keydir", action="store_true", help="also time the device keydir (gck_ctx_keydir)")
+    ap.add_argument("--no-merge", action="store_true",
+                    help="N>1: skip the keydir merge across ranks that follows the timed replays")
+    ap.add_argument("--merge", action="store_true",
+                    help="N=1: time the keydir merge too (a one-rank RCCL group)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
                     help="also time K host-in/host-out replays (pinned H2D + run + D2H of the tuples)")
     args = ap.parse_args()
@@ -189,6 +224,20 @@ def main():
         crc_ms.append(stp["ms_phase"]["crc_rows"])
         for k, v in stp["ms_phase"].items():
             phases_sum[k] = phases_sum.get(k, 0.0) + v
+    merge = None
+    if dist is None and args.merge:
+        import socket
+
+        import torch.distributed as dist1
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist1.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        merge = keydir_merge(g, ctx, dist1, info["n_files"])
+        dist1.destroy_process_group()
+    elif dist is not None and not args.no_merge:
+        merge = keydir_merge(g, ctx, dist, info["n_files"])
     stream_gbs = None
     if rank == 0:
         _, stream_gbs = ctx.stream_read_ceiling(5)
@@ -221,7 +270,8 @@ def main():
                 "records_per_gpu": st["n_recs"],
                 "files_per_gpu": info["n_files"],
                 "crc_rejects": st["n_crc_fail"],
-                "parallelism": f"files sharded over {world} GPU(s), replicas of the pipeline, no collective",
+                "parallelism": f"files sharded over {world} GPU(s), no data-path collective"
+                               + ("; keydir merge over RCCL all-to-all after the timed replays" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -247,6 +297,8 @@ def main():
             out["keydir"] = dict(ms=round(kd_ms, 3), live_entries=len(live), records=st["n_recs"],
                                  note="gck_ctx_keydir after a run (row f1): last record per key, Puts kept; "
                                       "not part of value")
+        if merge is not None:
+            out["keydir_merge"] = merge
         if args.host_inclusive:
             out["host_inclusive"] = host_inclusive(g, ctx, info, args.host_inclusive)
         if world == 1 and not args.no_cpu_baseline:

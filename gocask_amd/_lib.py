@@ -44,10 +44,15 @@ REC_DTYPE = np.dtype(
 )
 assert REC_DTYPE.itemsize == 40
 
+# gck_kd_entry: one keydir entry crossing shards (include/gocask_hip.h)
+KD_ENTRY_DTYPE = np.dtype([("hash", "<u8"), ("key_off", "<u8"), ("key_len", "<u4"), ("shard", "<u4"),
+                           ("rec", REC_DTYPE)])
+assert KD_ENTRY_DTYPE.itemsize == 64
+
 # Every symbol include/gocask_hip.h declares (tests check the .so exports them).
 EXPORTED = [
     "gck_replay", "gck_result_free", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
-    "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
+    "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
     "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_stream_pattern", "gck_diag_crc_variant", "gck_encode_corpus", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
     "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count", "gck_host_register", "gck_host_unregister",
@@ -120,6 +125,24 @@ class GckConfig(ctypes.Structure):
 _lib = None
 
 
+def _torch_runtime_first():
+    """torch ships its own HIP runtime (libamdhip64 + ROCr from its wheel) next
+    to the system one this library links; in one process torch's only comes up
+    if it initialises first ("No HIP GPUs are available" otherwise).  The
+    Python host side uses torch for device buffers and torch.distributed (the
+    keydir exchange), so let it initialise before the first call into
+    libgocask_hip.  A process without torch is unaffected."""
+    try:
+        import torch
+    except ImportError:
+        return
+    try:
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # torch without a usable device: the library reports its own errors
+        pass
+
+
 def load():
     """Load the in-tree HIP library.  Raises if it has not been built."""
     global _lib
@@ -127,6 +150,7 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+    _torch_runtime_first()
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.POINTER
     vp = ctypes.c_void_p
@@ -141,6 +165,13 @@ def load():
         "gck_ctx_fetch_into": (ctypes.c_int, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
         "gck_ctx_keydir": (ctypes.c_int, [vp, ctypes.c_uint32, P(ctypes.c_uint64), P(ctypes.c_double)]),
         "gck_ctx_fetch_keydir": (ctypes.c_int, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
+        "gck_kd_pack_sizes": (ctypes.c_int, [vp, ctypes.c_uint32, P(ctypes.c_uint64), P(ctypes.c_uint64)]),
+        "gck_kd_pack": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, vp, ctypes.c_uint64, vp,
+                                       ctypes.c_uint64]),
+        "gck_kd_merge": (ctypes.c_int, [vp, vp, vp, P(ctypes.c_uint64), P(ctypes.c_uint64), ctypes.c_uint32,
+                                        P(ctypes.c_uint64), P(ctypes.c_double)]),
+        "gck_kd_fetch_merged": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, P(ctypes.c_uint64),
+                                               P(ctypes.c_uint64)]),
         "gck_ctx_stats": (ctypes.c_int, [vp, P(GckStats)]),
         "gck_phase_name": (ctypes.c_char_p, [ctypes.c_int]),
         "gck_ctx_device_recs": (ctypes.c_int, [vp, P(vp), P(ctypes.c_uint64)]),

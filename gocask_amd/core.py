@@ -17,7 +17,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (F_CRC_OK, F_TOMBSTONE, GCK_ECRC_FAILED, GCK_EINVALID_KEY, GCK_EKEY_NOT_FOUND, GCK_OK,
-                   GCK_EUNEXPECTED_EOF, REC_DTYPE, GckCorpusCfg, GckFile, GckOpts, GckResult, GckStats, check)
+                   GCK_EUNEXPECTED_EOF, KD_ENTRY_DTYPE, REC_DTYPE, GckCorpusCfg, GckFile, GckOpts, GckResult, GckStats, check)
 
 InMemoryDB = "in:mem:db"  # core/db.go:32-34
 
@@ -312,16 +312,52 @@ class ReplayContext:
         check(self._L.gck_ctx_fetch_into(self._h, recs.ctypes.data, recs.size, ctypes.byref(n)))
         return n.value
 
-    def keydir(self, keep_tombstones=False):
+    def keydir(self, keep_tombstones=False, fetch=True):
         """Device keydir of the last run (gck_ctx_keydir + gck_ctx_fetch_keydir):
-        (live REC_DTYPE records in walk order, device ms)."""
+        (live REC_DTYPE records in walk order, device ms); with fetch=False
+        (entry count, device ms) and the entries stay on the device."""
         n, ms = ctypes.c_uint64(), ctypes.c_double()
         check(self._L.gck_ctx_keydir(self._h, 1 if keep_tombstones else 0, ctypes.byref(n), ctypes.byref(ms)))
+        if not fetch:
+            return n.value, ms.value
         recs = np.zeros(n.value, dtype=REC_DTYPE)
         got = ctypes.c_uint64()
         check(self._L.gck_ctx_fetch_keydir(self._h, recs.ctypes.data if n.value else None, n.value,
                                            ctypes.byref(got)))
         return recs, ms.value
+
+    # -- keydir merge across shards (include/gocask_hip.h, SURVEY.md §8e) --
+    def kd_pack_sizes(self, nparts):
+        """After keydir(keep_tombstones=True): (entries, key bytes) per owner."""
+        cnt = (ctypes.c_uint64 * nparts)()
+        kb = (ctypes.c_uint64 * nparts)()
+        check(self._L.gck_kd_pack_sizes(self._h, nparts, cnt, kb))
+        return list(cnt), list(kb)
+
+    def kd_pack(self, shard, file_base, d_entries, entries_cap, d_keys, keys_cap):
+        """Fill device buffers (raw pointers) with the partitioned entries / keys."""
+        check(self._L.gck_kd_pack(self._h, shard, file_base, d_entries, entries_cap, d_keys, keys_cap))
+
+    def kd_merge(self, d_entries, d_keys, src_counts, src_key_bytes):
+        """Merge received partitions (device pointers, sources in shard order):
+        (live entries, device ms)."""
+        ns = len(src_counts)
+        cnt = (ctypes.c_uint64 * ns)(*src_counts)
+        kb = (ctypes.c_uint64 * ns)(*src_key_bytes)
+        n, ms = ctypes.c_uint64(), ctypes.c_double()
+        check(self._L.gck_kd_merge(self._h, d_entries, d_keys, cnt, kb, ns, ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def kd_fetch_merged(self):
+        """Host copies of the merged entries (KD_ENTRY_DTYPE) and their key blob."""
+        n, nk = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._L.gck_kd_fetch_merged(self._h, None, 0, None, 0, ctypes.byref(n), ctypes.byref(nk)))
+        ents = np.zeros(n.value, dtype=KD_ENTRY_DTYPE)
+        keys = np.zeros(nk.value, dtype=np.uint8)
+        check(self._L.gck_kd_fetch_merged(self._h, ents.ctypes.data if n.value else None, n.value,
+                                          keys.ctypes.data if nk.value else None, nk.value, ctypes.byref(n),
+                                          ctypes.byref(nk)))
+        return ents, keys
 
     def stats(self):
         s = GckStats()

@@ -95,8 +95,16 @@ struct Ctx {
 
     // device keydir (keydir.hip): key hashes, slot table, live flags, tile
     // ranks, the live records
-    DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout;
+    DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout, d_kdidx;
     uint64_t n_live = 0;
+    // keydir merge across shards: pack partition of each live entry, the
+    // merged headers / keys of the entries this rank owns
+    DBuf d_kpart, d_kcrank, d_kbrank, d_kpsum, d_kptot;  // pack: partition, in-tile ranks, tile sums
+    DBuf d_mkoff, d_mtab, d_mlive, d_msrc, d_mhdr, d_mkeys;  // merge
+    uint32_t kd_nparts = 0;                               // of the last gck_kd_pack_sizes
+    uint64_t kd_packed = 0;                               // entries it partitioned
+    uint64_t kd_tot[128] = {};                            // its per-partition counts, key bytes
+    uint64_t n_merged = 0, merged_key_bytes = 0;
 
     // results of the last run
     int32_t status = 0;

@@ -102,17 +102,18 @@ __global__ __launch_bounds__(256) void k_kd_mark(const uint32_t *__restrict__ ta
 }
 
 // Exclusive rank of v inside a workgroup of kKdTile lanes; the total is out.
-__device__ uint32_t block_excl(uint32_t v, uint32_t *wsum, uint32_t &total) {
+template <class T>
+__device__ T block_excl(T v, T *wsum, T &total) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
+    T x = v;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
+        const T y = __shfl_up(x, d);
         if (lane >= (uint32_t)d) x += y;
     }
     if (lane == 63) wsum[w] = x;
     __syncthreads();
-    uint32_t base = 0, tot = 0;
+    T base = 0, tot = 0;
     for (uint32_t i = 0; i < blockDim.x / 64; ++i) {
         base += i < w ? wsum[i] : 0u;
         tot += wsum[i];
@@ -149,13 +150,208 @@ __global__ __launch_bounds__(kKdTile) void k_kd_tile_scan(uint32_t *__restrict__
 
 __global__ __launch_bounds__(kKdTile) void k_kd_scatter(const uint32_t *__restrict__ live, uint64_t n,
                                                         const uint32_t *__restrict__ tile_base,
-                                                        const gck_rec *__restrict__ recs, gck_rec *__restrict__ out) {
+                                                        const gck_rec *__restrict__ recs, gck_rec *__restrict__ out,
+                                                        uint32_t *__restrict__ out_idx) {
     __shared__ uint32_t wsum[kKdTile / 64];
     const uint64_t r = (uint64_t)blockIdx.x * kKdTile + threadIdx.x;
     const uint32_t v = r < n ? live[r] : 0u;
     uint32_t total;
     const uint32_t ex = block_excl(v, wsum, total);
-    if (v) out[tile_base[blockIdx.x] + ex] = recs[r];
+    if (v) {
+        out[tile_base[blockIdx.x] + ex] = recs[r];
+        out_idx[tile_base[blockIdx.x] + ex] = (uint32_t)r;
+    }
+}
+
+// ---- merge across shards (gck_kd_pack / gck_kd_merge) -----------------------
+
+static_assert(sizeof(gck_kd_entry) == 64, "gck_kd_entry is 64 bytes");
+
+__device__ __forceinline__ uint32_t kd_part(uint64_t h, uint32_t nparts) { return (uint32_t)(h >> 40) % nparts; }
+__device__ __forceinline__ uint64_t pad8(uint64_t n) { return (n + 7) & ~7ull; }
+
+// Entry sources of the partition / compaction kernels below.  sel: the entry
+// takes part; put: write its gck_kd_entry and its zero-padded key.
+struct LocalSrc {  // the keydir of the last run (gck_ctx_keydir)
+    const uint8_t *arena;
+    const uint64_t *rec_off, *khash;
+    const gck_rec *recs;  // live entries, walk order
+    const uint32_t *idx;  // their record indices
+    uint32_t shard, file_base;
+    __device__ bool sel(uint64_t) const { return true; }
+    __device__ uint64_t hash(uint64_t i) const { return khash[idx[i]]; }
+    __device__ uint32_t klen(uint64_t i) const { return recs[i].key_len; }
+    __device__ void put(uint64_t i, gck_kd_entry *e, uint64_t key_rel, uint32_t *kdst) const {
+        const uint32_t r = idx[i];
+        gck_rec rec = recs[i];
+        const uint32_t len = rec.key_len;
+        const KeyWords k(arena, rec_off[r] + 16, len);
+        for (uint32_t w = 0; 4ull * w < pad8(len); ++w) kdst[w] = 4 * w < len ? k[w] : 0u;
+        rec.file += file_base;
+        e->hash = khash[r];
+        e->key_off = key_rel;
+        e->key_len = len;
+        e->shard = shard;
+        e->rec = rec;
+    }
+};
+
+struct MergedSrc {  // received entries that won the merge
+    const gck_kd_entry *E;
+    const uint8_t *K;
+    const uint64_t *koff;  // key offset of each entry in K
+    const uint32_t *live;
+    __device__ bool sel(uint64_t i) const { return live[i] != 0; }
+    __device__ uint64_t hash(uint64_t i) const { return E[i].hash; }
+    __device__ uint32_t klen(uint64_t i) const { return E[i].key_len; }
+    __device__ void put(uint64_t i, gck_kd_entry *e, uint64_t key_rel, uint32_t *kdst) const {
+        gck_kd_entry x = E[i];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(K + koff[i]);
+        for (uint32_t w = 0; 4ull * w < pad8(x.key_len); ++w) kdst[w] = src[w];
+        x.key_off = key_rel;
+        *e = x;
+    }
+};
+
+// k_pk_tiles: per tile of kKdTile entries, the partition of each selected
+// entry, its rank among the tile's entries of that partition (count and key
+// bytes) and the tile's per-partition sums: tsum rows 0..nparts-1 count,
+// rows nparts..2*nparts-1 key bytes, one column per tile.
+template <class Src>
+__global__ __launch_bounds__(kKdTile) void k_pk_tiles(Src src, uint64_t n, uint32_t nparts,
+                                                      uint32_t *__restrict__ part, uint32_t *__restrict__ crank,
+                                                      uint64_t *__restrict__ brank, uint64_t *__restrict__ tsum,
+                                                      uint64_t nt) {
+    __shared__ uint64_t wsum[kKdTile / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * kKdTile + threadIdx.x;
+    const bool in = i < n && src.sel(i);
+    uint32_t p = 0;
+    uint64_t bytes = 0;
+    if (in) {
+        p = nparts > 1 ? kd_part(src.hash(i), nparts) : 0u;
+        bytes = pad8(src.klen(i));
+    }
+    uint64_t cr = 0, br = 0;
+    for (uint32_t q = 0; q < nparts; ++q) {
+        const bool mine = in && p == q;
+        uint64_t tc, tb;
+        const uint64_t c = block_excl<uint64_t>(mine ? 1u : 0u, wsum, tc);
+        const uint64_t b = block_excl<uint64_t>(mine ? bytes : 0u, wsum, tb);
+        if (mine) {
+            cr = c;
+            br = b;
+        }
+        if (threadIdx.x == 0) {
+            tsum[(uint64_t)q * nt + blockIdx.x] = tc;
+            tsum[(uint64_t)(nparts + q) * nt + blockIdx.x] = tb;
+        }
+    }
+    if (i < n) {
+        part[i] = in ? p : kEmpty;
+        crank[i] = (uint32_t)cr;
+        brank[i] = br;
+    }
+}
+
+// k_pk_scan: one workgroup per tsum row, exclusive in place; the row total
+// goes to tot[row].
+__global__ __launch_bounds__(kKdTile) void k_pk_scan(uint64_t *__restrict__ tsum, uint64_t nt,
+                                                     uint64_t *__restrict__ tot) {
+    __shared__ uint64_t wsum[kKdTile / 64];
+    uint64_t *row = tsum + (uint64_t)blockIdx.x * nt;
+    uint64_t run = 0;
+    for (uint64_t i0 = 0; i0 < nt; i0 += kKdTile) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t v = i < nt ? row[i] : 0u;
+        uint64_t total;
+        const uint64_t ex = block_excl<uint64_t>(v, wsum, total);
+        if (i < nt) row[i] = run + ex;
+        run += total;
+    }
+    if (threadIdx.x == 0) tot[blockIdx.x] = run;
+}
+
+// k_pk_scatter: each selected entry to its partition, partitions laid out
+// one after another (entries and keys alike), tile order then rank within.
+template <class Src>
+__global__ __launch_bounds__(256) void k_pk_scatter(Src src, uint64_t n, uint32_t nparts,
+                                                    const uint32_t *__restrict__ part,
+                                                    const uint32_t *__restrict__ crank,
+                                                    const uint64_t *__restrict__ brank,
+                                                    const uint64_t *__restrict__ tsum, uint64_t nt,
+                                                    const uint64_t *__restrict__ tot, gck_kd_entry *__restrict__ out,
+                                                    uint8_t *__restrict__ keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t p = part[i];
+        if (p == kEmpty) continue;
+        const uint64_t t = i / kKdTile;
+        uint64_t ebase = 0, kbase = 0;
+        for (uint32_t q = 0; q < p; ++q) {
+            ebase += tot[q];
+            kbase += tot[nparts + q];
+        }
+        const uint64_t e = ebase + tsum[(uint64_t)p * nt + t] + crank[i];
+        const uint64_t kr = tsum[(uint64_t)(nparts + p) * nt + t] + brank[i];
+        src.put(i, out + e, kr, reinterpret_cast<uint32_t *>(keys + kbase + kr));
+    }
+}
+
+// k_mg_koff: offset of each received entry's key in the concatenated blobs;
+// pre = entry prefix over sources [nsrc+1], blob prefix [nsrc+1], error word.
+__global__ __launch_bounds__(256) void k_mg_koff(const gck_kd_entry *__restrict__ E, uint64_t n,
+                                                 uint64_t *__restrict__ pre, uint32_t nsrc,
+                                                 uint64_t *__restrict__ koff) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t s = 0;
+        while (s + 1 < nsrc && i >= pre[s + 1]) ++s;
+        const uint64_t ko = E[i].key_off, blob = pre[nsrc + 2 + s] - pre[nsrc + 1 + s];
+        if ((ko & 7) || ko + pad8(E[i].key_len) > blob) {  // not a packed entry: refuse the merge
+            atomicOr(reinterpret_cast<unsigned long long *>(pre + 2 * (nsrc + 1)), 1ull);
+            koff[i] = pre[nsrc + 1 + s];
+        } else {
+            koff[i] = pre[nsrc + 1 + s] + ko;
+        }
+    }
+}
+
+__device__ bool blob_same(const uint8_t *__restrict__ K, uint64_t a, uint64_t b, uint32_t len) {
+    const uint32_t *x = reinterpret_cast<const uint32_t *>(K + a), *y = reinterpret_cast<const uint32_t *>(K + b);
+    for (uint32_t w = 0; 4ull * w < len; ++w)  // padding bytes are zero on both sides
+        if (x[w] != y[w]) return false;
+    return true;
+}
+
+// k_mg_insert: as k_kd_insert over received entries; the entry index orders
+// shards (sources are concatenated in shard order), so atomicMax keeps the
+// highest shard's entry of every key.
+__global__ __launch_bounds__(256) void k_mg_insert(const gck_kd_entry *__restrict__ E, const uint8_t *__restrict__ K,
+                                                   const uint64_t *__restrict__ koff, uint64_t n,
+                                                   uint32_t *__restrict__ table, uint64_t mask) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = E[r].hash;
+        const uint32_t len = E[r].key_len;
+        for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+            uint32_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (cur == kEmpty) {
+                const uint32_t prev = atomicCAS(table + s, kEmpty, (uint32_t)r);
+                if (prev == kEmpty) break;
+                cur = prev;
+            }
+            if (E[cur].hash == h && E[cur].key_len == len && blob_same(K, koff[cur], koff[r], len)) {
+                atomicMax(table + s, (uint32_t)r);
+                break;
+            }
+        }
+    }
+}
+
+// k_mg_mark: a key's winning entry stays unless it is a delete.
+__global__ __launch_bounds__(256) void k_mg_mark(const uint32_t *__restrict__ table, uint64_t slots,
+                                                 const gck_kd_entry *__restrict__ E, uint32_t *__restrict__ live) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = table[s];
+        if (r != kEmpty && !(E[r].rec.flags & GCK_F_TOMBSTONE)) live[r] = 1;
+    }
 }
 
 }  // namespace gck
@@ -179,7 +375,8 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
     int rc;
     if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 4)) || (rc = c->d_live.ensure(n * 4)) ||
-        (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))))
+        (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))) ||
+        (rc = c->d_kdidx.ensure(n * 4)))
         return rc;
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
@@ -197,7 +394,8 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
     k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);
     k_kd_scatter<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>(),
-                                                  c->d_out.as<gck_rec>(), c->d_kdout.as<gck_rec>());
+                                                  c->d_out.as<gck_rec>(), c->d_kdout.as<gck_rec>(),
+                                                  c->d_kdidx.as<uint32_t>());
     GCK_HIP(hipEventRecord(b, s));
     uint32_t live = 0;
     GCK_HIP(hipMemcpyAsync(&live, c->d_ktile.as<uint32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
@@ -221,6 +419,157 @@ int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n) 
     if (c->n_live) {
         GCK_HIP(hipSetDevice(c->device));
         GCK_HIP(hipMemcpy(dst, c->d_kdout.p, c->n_live * sizeof(gck_rec), hipMemcpyDeviceToHost));
+    }
+    return GCK_OK;
+}
+
+int gck_kd_pack_sizes(gck_ctx *ctx, uint32_t nparts, uint64_t *counts, uint64_t *key_bytes) {
+    if (!ctx || !counts || !key_bytes || nparts == 0 || nparts > 64) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    c->kd_nparts = 0;
+    const uint64_t n = c->n_live;
+    const uint64_t nt = n ? (n + kKdTile - 1) / kKdTile : 1;
+    int rc;
+    if ((rc = c->d_kpart.ensure(n * 4)) || (rc = c->d_kcrank.ensure(n * 4)) || (rc = c->d_kbrank.ensure(n * 8)) ||
+        (rc = c->d_kpsum.ensure(2 * nparts * nt * 8)) || (rc = c->d_kptot.ensure(2 * 64 * 8)))
+        return rc;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    uint64_t tot[128] = {};
+    if (n) {
+        const LocalSrc src{c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_khash.as<uint64_t>(),
+                           c->d_kdout.as<gck_rec>(), c->d_kdidx.as<uint32_t>(), 0u, 0u};
+        k_pk_tiles<LocalSrc><<<(uint32_t)nt, kKdTile, 0, s>>>(src, n, nparts, c->d_kpart.as<uint32_t>(),
+                                                              c->d_kcrank.as<uint32_t>(), c->d_kbrank.as<uint64_t>(),
+                                                              c->d_kpsum.as<uint64_t>(), nt);
+        k_pk_scan<<<2 * nparts, kKdTile, 0, s>>>(c->d_kpsum.as<uint64_t>(), nt, c->d_kptot.as<uint64_t>());
+        GCK_HIP(hipMemcpyAsync(tot, c->d_kptot.p, 2 * nparts * 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        GCK_HIP(hipGetLastError());
+    }
+    for (uint32_t p = 0; p < nparts; ++p) {
+        counts[p] = tot[p];
+        key_bytes[p] = tot[nparts + p];
+        c->kd_tot[p] = tot[p];
+        c->kd_tot[nparts + p] = tot[nparts + p];
+    }
+    c->kd_nparts = nparts;
+    c->kd_packed = n;
+    return GCK_OK;
+}
+
+int gck_kd_pack(gck_ctx *ctx, uint32_t shard, uint32_t file_base, gck_kd_entry *d_entries, uint64_t entries_cap,
+                uint8_t *d_keys, uint64_t keys_cap) {
+    if (!ctx) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    const uint32_t np = c->kd_nparts;
+    if (!np || c->kd_packed != c->n_live) return GCK_EINVAL;  // gck_kd_pack_sizes first
+    uint64_t ne = 0, nk = 0;
+    for (uint32_t p = 0; p < np; ++p) {
+        ne += c->kd_tot[p];
+        nk += c->kd_tot[np + p];
+    }
+    if (ne > entries_cap || nk > keys_cap || (ne && (!d_entries || !d_keys))) return GCK_EINVAL;
+    if (!ne) return GCK_OK;
+    const uint64_t n = c->n_live, nt = (n + kKdTile - 1) / kKdTile;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const LocalSrc src{c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_khash.as<uint64_t>(),
+                       c->d_kdout.as<gck_rec>(), c->d_kdidx.as<uint32_t>(), shard, file_base};
+    k_pk_scatter<LocalSrc><<<(uint32_t)c->n_cu * 4, 256, 0, s>>>(
+        src, n, np, c->d_kpart.as<uint32_t>(), c->d_kcrank.as<uint32_t>(), c->d_kbrank.as<uint64_t>(),
+        c->d_kpsum.as<uint64_t>(), nt, c->d_kptot.as<uint64_t>(), d_entries, d_keys);
+    GCK_HIP(hipStreamSynchronize(s));
+    GCK_HIP(hipGetLastError());
+    return GCK_OK;
+}
+
+int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_keys, const uint64_t *src_counts,
+                 const uint64_t *src_key_bytes, uint32_t nsrc, uint64_t *n_live, double *ms) {
+    if (!ctx || !n_live || !src_counts || !src_key_bytes || nsrc == 0 || nsrc > 65536) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    *n_live = 0;
+    c->n_merged = 0;
+    c->merged_key_bytes = 0;
+    c->kd_nparts = 0;  // the pack state shares buffers with the merge
+    std::vector<uint64_t> pre(2 * (nsrc + 1) + 1, 0);
+    for (uint32_t i = 0; i < nsrc; ++i) {
+        pre[i + 1] = pre[i] + src_counts[i];
+        pre[nsrc + 2 + i] = pre[nsrc + 1 + i] + src_key_bytes[i];
+    }
+    const uint64_t n = pre[nsrc];
+    if (ms) *ms = 0;
+    if (!n) return GCK_OK;
+    if (n >= kEmpty || !d_entries || !d_keys) return GCK_EINVAL;
+    uint64_t slots = 1024;
+    while (slots < 2 * n) slots <<= 1;
+    const uint64_t nt = (n + kKdTile - 1) / kKdTile;
+    int rc;
+    if ((rc = c->d_msrc.ensure(pre.size() * 8)) || (rc = c->d_mkoff.ensure(n * 8)) ||
+        (rc = c->d_mtab.ensure(slots * 4)) || (rc = c->d_mlive.ensure(n * 4)) || (rc = c->d_kpart.ensure(n * 4)) ||
+        (rc = c->d_kcrank.ensure(n * 4)) || (rc = c->d_kbrank.ensure(n * 8)) || (rc = c->d_kpsum.ensure(2 * nt * 8)) ||
+        (rc = c->d_kptot.ensure(2 * 64 * 8)))
+        return rc;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    GCK_HIP(hipEventRecord(a, s));
+    GCK_HIP(hipMemcpyAsync(c->d_msrc.p, pre.data(), pre.size() * 8, hipMemcpyHostToDevice, s));
+    GCK_HIP(hipMemsetAsync(c->d_mtab.p, 0xFF, slots * 4, s));
+    GCK_HIP(hipMemsetAsync(c->d_mlive.p, 0, n * 4, s));
+    const uint32_t grid = (uint32_t)c->n_cu * 8;
+    k_mg_koff<<<grid, 256, 0, s>>>(d_entries, n, c->d_msrc.as<uint64_t>(), nsrc, c->d_mkoff.as<uint64_t>());
+    k_mg_insert<<<grid, 256, 0, s>>>(d_entries, d_keys, c->d_mkoff.as<uint64_t>(), n, c->d_mtab.as<uint32_t>(),
+                                     slots - 1);
+    k_mg_mark<<<grid, 256, 0, s>>>(c->d_mtab.as<uint32_t>(), slots, d_entries, c->d_mlive.as<uint32_t>());
+    const MergedSrc src{d_entries, d_keys, c->d_mkoff.as<uint64_t>(), c->d_mlive.as<uint32_t>()};
+    k_pk_tiles<MergedSrc><<<(uint32_t)nt, kKdTile, 0, s>>>(src, n, 1u, c->d_kpart.as<uint32_t>(),
+                                                           c->d_kcrank.as<uint32_t>(), c->d_kbrank.as<uint64_t>(),
+                                                           c->d_kpsum.as<uint64_t>(), nt);
+    k_pk_scan<<<2, kKdTile, 0, s>>>(c->d_kpsum.as<uint64_t>(), nt, c->d_kptot.as<uint64_t>());
+    uint64_t tot[2] = {}, err = 0;
+    GCK_HIP(hipMemcpyAsync(tot, c->d_kptot.p, 16, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(&err, c->d_msrc.as<uint64_t>() + 2 * (nsrc + 1), 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    GCK_HIP(hipGetLastError());
+    if (err) {
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        return GCK_EINVAL;
+    }
+    if ((rc = c->d_mhdr.ensure(tot[0] * sizeof(gck_kd_entry))) || (rc = c->d_mkeys.ensure(tot[1]))) return rc;
+    k_pk_scatter<MergedSrc><<<grid, 256, 0, s>>>(src, n, 1u, c->d_kpart.as<uint32_t>(), c->d_kcrank.as<uint32_t>(),
+                                                 c->d_kbrank.as<uint64_t>(), c->d_kpsum.as<uint64_t>(), nt,
+                                                 c->d_kptot.as<uint64_t>(), c->d_mhdr.as<gck_kd_entry>(),
+                                                 c->d_mkeys.as<uint8_t>());
+    GCK_HIP(hipEventRecord(b, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    GCK_HIP(hipGetLastError());
+    float t = 0;
+    (void)hipEventElapsedTime(&t, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms) *ms = t;
+    c->n_merged = tot[0];
+    c->merged_key_bytes = tot[1];
+    *n_live = tot[0];
+    return GCK_OK;
+}
+
+int gck_kd_fetch_merged(gck_ctx *ctx, gck_kd_entry *dst, uint64_t cap, uint8_t *keys, uint64_t keys_cap,
+                        uint64_t *n, uint64_t *n_key_bytes) {
+    if (!ctx || !n || !n_key_bytes) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    *n = c->n_merged;
+    *n_key_bytes = c->merged_key_bytes;
+    if (!dst && !keys) return GCK_OK;  // size query
+    if (c->n_merged > cap || c->merged_key_bytes > keys_cap || (c->n_merged && (!dst || !keys))) return GCK_EINVAL;
+    if (c->n_merged) {
+        GCK_HIP(hipSetDevice(c->device));
+        GCK_HIP(hipMemcpy(dst, c->d_mhdr.p, c->n_merged * sizeof(gck_kd_entry), hipMemcpyDeviceToHost));
+        GCK_HIP(hipMemcpy(keys, c->d_mkeys.p, c->merged_key_bytes, hipMemcpyDeviceToHost));
     }
     return GCK_OK;
 }

@@ -138,6 +138,47 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 #define GCK_KD_KEEP_TOMBSTONES 1u
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
 int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
+
+/* ---- keydir merge across shards ----------------------------
+ * Files shard over GPUs in walk order: shard s holds a contiguous run of files,
+ * every one but the last shard's last file with reset_after = 1, so each shard
+ * replays on its own.  The merged keydir equals the one keyDir.set / unset
+ * (core/keydir.go:22-49) would build over all files in walk order:
+ *   1. every shard: gck_ctx_run, then gck_ctx_keydir(GCK_KD_KEEP_TOMBSTONES)
+ *      (a shard's last word on a key may be a delete that hides an earlier
+ *      shard's Put);
+ *   2. gck_kd_pack_sizes / gck_kd_pack: the shard's entries as gck_kd_entry
+ *      records plus a key blob, partitioned by key hash over nparts owners
+ *      (partition-major, walk order within a partition);
+ *   3. the caller exchanges partitions (all-to-all, e.g. RCCL over xGMI), each
+ *      owner concatenating what it receives in shard order;
+ *   4. gck_kd_merge on the owner: per key, the entry of the highest shard wins;
+ *      a winning tombstone drops the key.  gck_kd_fetch_merged copies the
+ *      owner's live entries (shard order, then walk order) and their keys.
+ * The partition of a key is (hash >> 40) % nparts on every shard. */
+typedef struct gck_kd_entry {
+    uint64_t hash;    /* 64-bit hash of the key bytes                                */
+    uint64_t key_off; /* offset of the key in its blob (8-byte aligned, zero padded) */
+    uint32_t key_len; /* key bytes                                                   */
+    uint32_t shard;   /* shard that wrote the entry                                  */
+    gck_rec rec;      /* the record; rec.file is global (file_base + walk index)     */
+} gck_kd_entry;       /* 64 bytes */
+
+/* After gck_ctx_keydir: partition the keydir entries over nparts (1..64)
+ * owners; counts[p] entries and key_bytes[p] blob bytes go to owner p. */
+int gck_kd_pack_sizes(gck_ctx *ctx, uint32_t nparts, uint64_t *counts, uint64_t *key_bytes);
+/* Fill DEVICE buffers: entries (>= sum counts) partition-major, keys (>= sum
+ * key_bytes) partition-major; key_off is relative to the partition's blob. */
+int gck_kd_pack(gck_ctx *ctx, uint32_t shard, uint32_t file_base, gck_kd_entry *d_entries, uint64_t entries_cap,
+                uint8_t *d_keys, uint64_t keys_cap);
+/* Merge the partitions an owner received: DEVICE arrays of nsrc sources in
+ * shard order, src_counts[s] entries / src_key_bytes[s] blob bytes each. */
+int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_keys, const uint64_t *src_counts,
+                 const uint64_t *src_key_bytes, uint32_t nsrc, uint64_t *n_live, double *ms);
+/* Host copies of the merged entries (key_off into the merged blob) and keys;
+ * dst = keys = NULL only reports the sizes. */
+int gck_kd_fetch_merged(gck_ctx *ctx, gck_kd_entry *dst, uint64_t cap, uint8_t *keys, uint64_t keys_cap,
+                        uint64_t *n, uint64_t *n_key_bytes);
 int gck_ctx_stats(gck_ctx *ctx, gck_stats *out);
 const char *gck_phase_name(int phase);
 /* Device pointers of the last run's outputs (gck_rec array, n records) and the

@@ -1,0 +1,226 @@
+"""Keydir merge across shards on one GPU, through the C-ABI.
+
+A corpus is cut into shards of consecutive files (walk order); every shard is
+replayed by its own context, its keydir (tombstones kept) packed into nparts
+partitions, each owner merges partition p of every shard in shard order.  The
+owners' entries together must equal the keydir keyDir.set / unset builds over
+the whole corpus in walk order (core/keydir.go:22-49), computed from the
+oracle's records.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("rec_off", "file", "key_len", "value_pos", "value_size", "crc", "ts", "flags", "crc_calc")
+
+
+@pytest.fixture(scope="module")
+def g():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    import gocask_amd
+
+    assert gocask_amd.device_count() > 0, "no GPU visible"
+    return gocask_amd
+
+
+def _walk(files, names):
+    walk = sorted(range(len(files)), key=lambda i: names[i])
+    wf = [files[i] for i in walk]
+    return wf, [i + 1 < len(wf) for i in range(len(wf))]
+
+
+def _global_keydir(files, recs):
+    """{key: record} over all files in walk order, deletes applied."""
+    kd = {}
+    for r in recs:
+        o = int(r["rec_off"]) + 16
+        key = bytes(files[int(r["file"])][o:o + int(r["key_len"])])
+        if int(r["flags"]) & 1:
+            kd.pop(key, None)
+        else:
+            kd[key] = r
+    return kd
+
+
+def _pack_shards(g, torch, shards, nparts):
+    """Replay every shard on its own context and pack its keydir."""
+    out, base = [], 0
+    for s, (files, reset) in enumerate(shards):
+        ctx = g.ReplayContext()
+        ctx.load(files, reset)
+        ctx.run()
+        ctx.keydir(keep_tombstones=True, fetch=False)
+        counts, kb = ctx.kd_pack_sizes(nparts)
+        ents = torch.empty(max(sum(counts) * 64, 1), dtype=torch.uint8, device="cuda")
+        keys = torch.empty(max(sum(kb), 1), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        ctx.kd_pack(s, base, ents.data_ptr(), sum(counts), keys.data_ptr(), sum(kb))
+        out.append((ctx, ents, keys, counts, kb, len(files)))
+        base += len(files)
+    return out
+
+
+def _merge_owner(torch, packed, p, owner_ctx):
+    """Owner p: partition p of every shard, in shard order (what the
+    all-to-all delivers), merged on owner_ctx."""
+    e_parts, k_parts, cnts, kbs = [], [], [], []
+    for _, ents, keys, counts, kb, _ in packed:
+        eo, ko = sum(counts[:p]) * 64, sum(kb[:p])
+        e_parts.append(ents[eo:eo + counts[p] * 64])
+        k_parts.append(keys[ko:ko + kb[p]])
+        cnts.append(counts[p])
+        kbs.append(kb[p])
+    pad = torch.zeros(8, dtype=torch.uint8, device="cuda")
+    E = torch.cat(e_parts + [pad])
+    K = torch.cat(k_parts + [pad])
+    torch.cuda.synchronize()
+    n, _ = owner_ctx.kd_merge(E.data_ptr(), K.data_ptr(), cnts, kbs)
+    ents, keys = owner_ctx.kd_fetch_merged()
+    assert len(ents) == n
+    return ents, keys
+
+
+def _check_merged(files, owners, want_kd, nparts, shard_of_file):
+    seen = {}
+    for p, (ents, keys) in enumerate(owners):
+        if len(ents):
+            assert np.all((ents["hash"] >> np.uint64(40)) % np.uint64(nparts) == np.uint64(p))
+            order = list(zip(ents["rec"]["file"].tolist(), ents["rec"]["rec_off"].tolist()))
+            assert order == sorted(order)  # shard order, then walk order
+        for e in ents:
+            ko, kl = int(e["key_off"]), int(e["key_len"])
+            assert ko % 8 == 0
+            key = bytes(keys[ko:ko + kl])
+            assert not keys[ko + kl:ko + ((kl + 7) & ~7)].any()  # zero padding
+            assert key not in seen, "key owned twice"
+            seen[key] = e
+    assert set(seen) == set(want_kd), (len(seen), len(want_kd))
+    for key, e in seen.items():
+        r = want_kd[key]
+        for f in FIELDS:
+            assert e["rec"][f] == r[f], (key, f, e["rec"][f], r[f])
+        assert e["key_len"] == r["key_len"] and e["shard"] == shard_of_file[int(r["file"])]
+        o = int(r["rec_off"]) + 16
+        assert key == bytes(files[int(r["file"])][o:o + int(r["key_len"])])
+
+
+@pytest.mark.parametrize("cuts,nparts", [((2, 4), 1), ((2, 4), 3), ((1, 3, 5), 4), ((3,), 8), ((), 2)])
+def test_merge_shards_equals_global_keydir(g, orc, cuts, nparts):
+    import torch
+
+    # a small key universe and 20 % deletes: keys cross shards, deletes in a
+    # later shard must hide Puts of an earlier one
+    files, names = orc.gen_corpus(seed=71, val_fixed=0, key_min=8, key_max=24, key_universe=1500,
+                                  tomb_permille=200, max_file_size=1 << 19, n_files=6)
+    wf, reset = _walk(files, names)
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] == 0
+    bounds = [0, *cuts, len(wf)]
+    shards = [(wf[a:b], reset[a:b]) for a, b in zip(bounds, bounds[1:])]
+    shard_of_file = [s for s, (a, b) in enumerate(zip(bounds, bounds[1:])) for _ in range(a, b)]
+    packed = _pack_shards(g, torch, shards, nparts)
+    try:
+        owners = [_merge_owner(torch, packed, p, packed[p % len(packed)][0]) for p in range(nparts)]
+    finally:
+        for c, *_ in packed:
+            c.close()
+    _check_merged(wf, owners, _global_keydir(wf, want), nparts, shard_of_file)
+
+
+def test_merge_with_empty_shard(g, orc):
+    import torch
+
+    files, names = orc.gen_corpus(seed=72, val_fixed=0, key_min=8, key_max=16, key_universe=300,
+                                  tomb_permille=100, max_file_size=1 << 18, n_files=3)
+    wf, reset = _walk(files, names)
+    want, _ = orc.replay(wf, reset)
+    empty = np.zeros(0, dtype=np.uint8)
+    # shard 1 holds one empty data file between the others
+    shards = [(wf[:2], reset[:2]), ([empty], [True]), (wf[2:], reset[2:])]
+    packed = _pack_shards(g, torch, shards, 2)
+    try:
+        assert sum(packed[1][3]) == 0
+        owners = [_merge_owner(torch, packed, p, packed[0][0]) for p in range(2)]
+    finally:
+        for c, *_ in packed:
+            c.close()
+    files_all = wf[:2] + [empty] + wf[2:]
+    recs = want.copy()
+    recs["file"] = np.where(recs["file"] >= 2, recs["file"] + 1, recs["file"])
+    _check_merged(files_all, owners, _global_keydir(files_all, recs), 2, [0, 0, 1, 2])
+
+
+def test_merge_single_shard_is_live_keydir(g, orc):
+    import torch
+
+    files, names = orc.gen_corpus(seed=73, val_fixed=0, key_min=8, key_max=24, key_universe=5000,
+                                  tomb_permille=50, max_file_size=1 << 20, n_files=4)
+    wf, reset = _walk(files, names)
+    packed = _pack_shards(g, torch, [(wf, reset)], 1)
+    ctx = packed[0][0]
+    try:
+        live, _ = ctx.keydir()
+        ents, _ = _merge_owner(torch, packed, 0, ctx)
+    finally:
+        ctx.close()
+    assert len(ents) == len(live)
+    for f in FIELDS:
+        assert np.array_equal(ents["rec"][f], live[f]), f
+
+
+def test_merge_rejects_foreign_entries(g, orc):
+    import torch
+
+    files, names = orc.gen_corpus(seed=74, val_fixed=100, key_min=8, key_max=8, key_universe=100,
+                                  max_file_size=1 << 16, n_files=1)
+    packed = _pack_shards(g, torch, [([files[0]], [False])], 1)
+    ctx, ents, keys, counts, kb, _ = packed[0]
+    try:
+        e = ents[:counts[0] * 64].view(torch.int64).view(-1, 8)
+        e[0, 1] += 3  # key_off no longer 8-aligned
+        torch.cuda.synchronize()
+        with pytest.raises(Exception):
+            ctx.kd_merge(ents.data_ptr(), keys.data_ptr(), counts, kb)
+        e[0, 1] -= 3
+        e[1, 1] = kb[0]  # key past the blob
+        torch.cuda.synchronize()
+        with pytest.raises(Exception):
+            ctx.kd_merge(ents.data_ptr(), keys.data_ptr(), counts, kb)
+    finally:
+        ctx.close()
+
+
+def test_merge_keydir_rccl_world1(g, orc):
+    """gocask_amd.shard.merge_keydir through a one-rank "nccl" (RCCL) group."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from gocask_amd import shard
+
+    files, names = orc.gen_corpus(seed=75, val_fixed=0, key_min=8, key_max=24, key_universe=3000,
+                                  tomb_permille=50, max_file_size=1 << 20, n_files=3)
+    wf, reset = _walk(files, names)
+    want, _ = orc.replay(wf, reset)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        with g.ReplayContext() as ctx:
+            ctx.load(wf, reset)
+            ctx.run()
+            base = shard.file_base(dist, len(wf), device="cuda")
+            n, t = shard.merge_keydir(ctx, dist, base)
+            ents, keys = ctx.kd_fetch_merged()
+    finally:
+        dist.destroy_process_group()
+    assert base == 0 and n == len(ents)
+    _check_merged(wf, [(ents, keys)], _global_keydir(wf, want), 1, [0] * len(wf))
