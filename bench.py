@@ -297,6 +297,13 @@ def main():
             out["keydir"] = dict(ms=round(kd_ms, 3), live_entries=len(live), records=st["n_recs"],
                                  note="gck_ctx_keydir after a run (row f1): last record per key, Puts kept; "
                                       "not part of value")
+            ctx.scrub_keydir()  # warm-up
+            _, _, bad, sc_ms = ctx.scrub_keydir()
+            vbytes = int(live["value_size"].sum(dtype="u8"))
+            out["scrub"] = dict(ms=round(sc_ms, 3), entries=len(live), value_bytes=vbytes, crc_rejects=bad,
+                                gbs=round(vbytes / (sc_ms * 1e-3) / 1e9, 1),
+                                note="gck_ctx_scrub_keydir (row f3): Get of every live key on the device -- "
+                                     "value at (File, ValuePos) re-read and CRC-checked; not part of value")
         if merge is not None:
             out["keydir_merge"] = merge
         if args.host_inclusive:

@@ -16,7 +16,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from ._lib import (F_CRC_OK, F_TOMBSTONE, GCK_ECRC_FAILED, GCK_EINVALID_KEY, GCK_EKEY_NOT_FOUND, GCK_OK,
+from ._lib import (F_CRC_OK, F_TOMBSTONE, GCK_ECRC_FAILED, GCK_EINVAL, GCK_EINVALID_KEY, GCK_EKEY_NOT_FOUND, GCK_OK,
                    GCK_EUNEXPECTED_EOF, KD_ENTRY_DTYPE, REC_DTYPE, GckCorpusCfg, GckFile, GckOpts, GckResult, GckStats, check)
 
 InMemoryDB = "in:mem:db"  # core/db.go:32-34
@@ -268,6 +268,7 @@ class ReplayContext:
     def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
+        self._n_live = 0
         check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
                                      ctypes.byref(self._h)))
 
@@ -318,6 +319,7 @@ class ReplayContext:
         (entry count, device ms) and the entries stay on the device."""
         n, ms = ctypes.c_uint64(), ctypes.c_double()
         check(self._L.gck_ctx_keydir(self._h, 1 if keep_tombstones else 0, ctypes.byref(n), ctypes.byref(ms)))
+        self._n_live = n.value
         if not fetch:
             return n.value, ms.value
         recs = np.zeros(n.value, dtype=REC_DTYPE)
@@ -325,6 +327,49 @@ class ReplayContext:
         check(self._L.gck_ctx_fetch_keydir(self._h, recs.ctypes.data if n.value else None, n.value,
                                            ctypes.byref(got)))
         return recs, ms.value
+
+    # -- batched Get / scrub (include/gocask_hip.h) --
+    def get_batch(self, keys, values=True):
+        """DB.Get for every key against the device keydir (keydir() first):
+        (status int32[n], value_size u32[n], crc_calc u32[n], values list or
+        None); values[i] is bytes for GCK_OK keys, else None."""
+        n = len(keys)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(k) for k in keys], dtype=np.uint64)
+        blob = np.frombuffer(b"".join(bytes(k) for k in keys) or b"\0", dtype=np.uint8)
+        st = np.zeros(n, dtype=np.int32)
+        vs = np.zeros(n, dtype=np.uint32)
+        cc = np.zeros(n, dtype=np.uint32)
+        ms = ctypes.c_double()
+        if not values:
+            check(self._L.gck_ctx_get_batch(self._h, blob.ctypes.data, off.ctypes.data, n, st.ctypes.data,
+                                            vs.ctypes.data, cc.ctypes.data, None, 0, None, ctypes.byref(ms)))
+            return st, vs, cc, None
+        vo = np.zeros(n, dtype=np.uint64)
+        cap = 1 << 20
+        while True:
+            buf = np.zeros(cap, dtype=np.uint8)
+            rc = self._L.gck_ctx_get_batch(self._h, blob.ctypes.data, off.ctypes.data, n, st.ctypes.data,
+                                           vs.ctypes.data, cc.ctypes.data, buf.ctypes.data, cap, vo.ctypes.data,
+                                           ctypes.byref(ms))
+            need = int(vs[st == GCK_OK].sum(dtype=np.uint64))
+            if rc == GCK_EINVAL and need > cap:
+                cap = need
+                continue
+            check(rc)
+            break
+        vals = [bytes(buf[int(vo[i]):int(vo[i]) + int(vs[i])]) if st[i] == GCK_OK else None for i in range(n)]
+        return st, vs, cc, vals
+
+    def scrub_keydir(self):
+        """Get of every live keydir entry on the device: (status int32[n_live],
+        crc_calc u32[n_live], n_bad, device ms)."""
+        st = np.zeros(self._n_live, dtype=np.int32)
+        cc = np.zeros(self._n_live, dtype=np.uint32)
+        bad, ms = ctypes.c_uint64(), ctypes.c_double()
+        check(self._L.gck_ctx_scrub_keydir(self._h, st.ctypes.data if st.size else None,
+                                           cc.ctypes.data if cc.size else None, ctypes.byref(bad), ctypes.byref(ms)))
+        return st, cc, bad.value, ms.value
 
     # -- keydir merge across shards (include/gocask_hip.h, SURVEY.md §8e) --
     def kd_pack_sizes(self, nparts):

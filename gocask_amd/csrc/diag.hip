@@ -48,19 +48,65 @@ __global__ __launch_bounds__(1024) void k_stream_rows(const uint8_t *__restrict_
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Random-access probes with k_walk's access shape (a 16 B load per hop):
+// DEP = each lane's next address depends on the bytes it just loaded (a chain
+// walk); otherwise the lane's hops are independent (8 loads in flight).
+template <bool DEP>
+__global__ __launch_bounds__(256) void k_chase(const uint8_t *__restrict__ arena, uint64_t len, uint32_t lanes,
+                                               uint32_t hops, uint32_t *sink) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= lanes) return;
+    const uint64_t n16 = (len >> 4) - 4;
+    uint64_t x = 0x9E3779B97F4A7C15ull * (t + 1);
+    auto pick = [&](uint64_t v) {
+        v = (v ^ (v >> 31)) * 0xBF58476D1CE4E5B9ull;
+        v ^= v >> 29;
+        return (((v & 0xFFFFFFFFull) * n16) >> 32) << 4;
+    };
+    uint32_t acc = 0;
+    if (DEP) {
+        uint64_t o = pick(x);
+        for (uint32_t h = 0; h < hops; ++h) {
+            const uint4 a = *reinterpret_cast<const uint4 *>(arena + o);
+            acc += a.x ^ a.y ^ a.z ^ a.w;
+            o = pick(x + acc + h);
+        }
+    } else {
+        for (uint32_t h = 0; h < hops; h += 8) {
+            uint4 a[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = *reinterpret_cast<const uint4 *>(arena + pick(x + h + j));
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += a[j].x ^ a[j].y ^ a[j].z ^ a[j].w;
+        }
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 }  // namespace gck
 
 using namespace gck;
 
-// pattern 0: k_stream_read; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>.
+// pattern 0: k_stream_read; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>;
+// 3..8: k_chase<dependent> with 8 Ki << (pattern-3) lanes; 9..14: the same
+// lane counts, independent loads.  The chase patterns make 10,240,000 hops in
+// all (C3's record count); *gbs reports hops per ns (G hops/s) for them.
 extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs) {
-    if (!ctx || iters <= 0 || pattern < 0 || pattern > 2) return GCK_EINVAL;
+    if (!ctx || iters <= 0 || pattern < 0 || pattern > 14) return GCK_EINVAL;
     Ctx *c = &ctx->c;
     GCK_HIP(hipSetDevice(c->device));
     if (!c->n_rows) return GCK_EINVAL;
     uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    const uint32_t lanes = pattern >= 3 ? 8192u << ((pattern - 3) % 6) : 0u;
+    const uint32_t hops = lanes ? ((10240000u / lanes + 7) & ~7u) : 0u;
     auto launch = [&]() {
-        if (pattern == 0)
+        if (pattern >= 9)
+            k_chase<false><<<(lanes + 255) / 256, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), c->arena_len, lanes, hops,
+                                                                      sink);
+        else if (pattern >= 3)
+            k_chase<true><<<(lanes + 255) / 256, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), c->arena_len, lanes, hops,
+                                                                     sink);
+        else if (pattern == 0)
             k_stream_read<<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
         else if (pattern == 1)
             k_stream_rows<true><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
@@ -81,7 +127,7 @@ extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, dou
     (void)hipEventDestroy(b);
     const double per = ms / iters;
     if (ms_per_iter) *ms_per_iter = per;
-    if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
+    if (gbs) *gbs = lanes ? (double)lanes * hops / (per * 1e-3) / 1e9 : (double)c->arena_len / (per * 1e-3) / 1e9;
     return GCK_OK;
 }
 

@@ -105,6 +105,10 @@ struct Ctx {
     uint64_t kd_packed = 0;                               // entries it partitioned
     uint64_t kd_tot[128] = {};                            // its per-partition counts, key bytes
     uint64_t n_merged = 0, merged_key_bytes = 0;
+    bool kd_valid = false;   // d_ktab / d_khash / d_kdout describe the last run
+    uint64_t kd_slots = 0;   // table slots (power of two; 0: no records)
+    // batched Get / scrub (get.hip): query keys, per-item state, values
+    DBuf d_gkeys, d_gkoff, d_gstat, d_gitem, d_gvsize, d_gexp, d_gcrc, d_gvoff, d_gvals;
 
     // results of the last run
     int32_t status = 0;

@@ -1,0 +1,339 @@
+// get.hip — batched DB.Get and keydir scrub on the device.
+//
+// DB.Get (core/db.go:287-316): an empty key is ErrInvalidKey; a key missing from
+// the keydir is ErrKeyNotFound; otherwise ValueSize bytes are read from the
+// entry's File at ValuePos (a short read is an error of the file system) and
+// crc32.ChecksumIEEE of them must equal the entry's CRC (ErrCRCFailed).  Here
+// the keydir is the device table of gck_ctx_keydir and the files are the
+// resident arena, so a batch of Gets is one lookup kernel and one verify
+// kernel; gck_ctx_scrub_keydir runs the verify over every live entry.
+#include "kd_common.h"
+
+namespace gck {
+
+// LDS tables (32 KiB per workgroup): slicing-by-4 (T), and multiplication by
+// the constants Z_1008 (Zs) and Z_{16 * 2^k}, k = 0..5 (Zt), each as four
+// byte tables: Z(A) = XOR_k Z[k][byte k of A] (Z is linear in A).
+struct CrcTabs {
+    uint32_t T[4][256];
+    uint32_t Zs[4][256];
+    uint32_t Zt[6][4][256];
+};
+
+__device__ void crc_tables(CrcTabs &t) {
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+        t.T[0][i] = c;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        uint32_t c = t.T[0][i];
+        for (int k = 1; k < 4; ++k) {
+            c = (c >> 8) ^ t.T[0][c & 0xFF];
+            t.T[k][i] = c;
+        }
+    }
+    for (uint32_t e = threadIdx.x; e < 7 * 1024; e += blockDim.x) {
+        const uint32_t m = e >> 10, k = (e >> 8) & 3, i = e & 0xFF;
+        const uint32_t z = xpow8n(m == 0 ? 1008u : (16u << (m - 1)));
+        const uint32_t v = multmodp(z, i << (8 * k));
+        if (m == 0)
+            t.Zs[k][i] = v;
+        else
+            t.Zt[m - 1][k][i] = v;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
+    return Z[0][a & 0xFF] ^ Z[1][(a >> 8) & 0xFF] ^ Z[2][(a >> 16) & 0xFF] ^ Z[3][a >> 24];
+}
+
+// crc32.ChecksumIEEE of p[0, L) by one wavefront.  The value is read as a
+// virtual buffer of J = ceil(L / 1 KiB) stripes, zero-padded at the FRONT
+// (F(0, .) ignores leading zeros), lane l taking the 16 bytes at 16 l of every
+// stripe: coalesced loads.  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner
+// over the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement
+// of the value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).
+// A shuffle tree then joins the lanes, lane l's part shifted past the 16 (63-l)
+// bytes after it: F(~0, V); crc = that ^ 0xFFFFFFFF.
+__device__ uint32_t wave_crc(const uint8_t *__restrict__ p, uint64_t L, const CrcTabs &t) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (L < 4) {  // fewer bytes than the init register
+        uint32_t c = 0xFFFFFFFFu;
+        for (uint64_t i = 0; i < L; ++i) c = t.T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
+        return ~c;
+    }
+    const uint64_t J = (L + 1023) >> 10, pad = (J << 10) - L;
+    const uint8_t *base = p + (16ull * lane - pad);  // (virtual position 16 l of stripe 0), maybe before p
+    uint32_t A = 0;
+    for (uint64_t j = 0; j < J; ++j) {
+        const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (v >= pad) {
+            const uint8_t *q = base + (j << 10);
+            const uint32_t *a = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(q) & ~(uintptr_t)3);
+            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 3);
+            uint32_t d[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) d[i] = a[i];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        } else if (v + 16 > pad) {  // straddles the value's start: bytes before it are zero
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (v + b >= pad) w[b >> 2] |= (uint32_t)p[v + b - pad] << (8 * (b & 3));
+        }
+        if (v + 16 > pad && v < pad + 4) {  // complement the value's first 4 bytes (may reach stripe 1)
+#pragma unroll
+            for (int b = 0; b < 16; ++b)
+                if (v + b >= pad && v + b < pad + 4) w[b >> 2] ^= 0xFFu << (8 * (b & 3));
+        }
+        uint32_t c = zmul(t.Zs, A);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            c ^= w[i];
+            c = t.T[3][c & 0xFF] ^ t.T[2][(c >> 8) & 0xFF] ^ t.T[1][(c >> 16) & 0xFF] ^ t.T[0][c >> 24];
+        }
+        A = c;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {  // lanes l = 0 mod 2^(k+1): Z_{16 * 2^k}(left) ^ right
+        const uint32_t right = __shfl_down(A, 1u << k);
+        A = zmul(t.Zt[k], A) ^ right;
+    }
+    return ~__shfl(A, 0);
+}
+
+// k_get_lookup: one lane per query key (keys: a blob padded by 8 bytes, koff:
+// n+1 offsets).  Probes the keydir table like k_kd_insert; a key whose winning
+// record is a tombstone is not in the keydir.  Found keys become verify items:
+// the arena offset of ValueSize bytes at ValuePos of the entry's file.
+__global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ keys,
+                                                    const uint64_t *__restrict__ koff, uint32_t n,
+                                                    const uint32_t *__restrict__ table, uint64_t slots,
+                                                    const uint64_t *__restrict__ khash,
+                                                    const uint8_t *__restrict__ arena,
+                                                    const uint64_t *__restrict__ rec_off,
+                                                    const uint4 *__restrict__ rec_hdr,
+                                                    const gck_rec *__restrict__ recs,
+                                                    const uint64_t *__restrict__ fbase,
+                                                    const uint64_t *__restrict__ flen, int32_t *__restrict__ status,
+                                                    uint64_t *__restrict__ item, uint32_t *__restrict__ vsize,
+                                                    uint32_t *__restrict__ expect) {
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const uint64_t len64 = koff[q + 1] - koff[q];
+        vsize[q] = 0;
+        if (len64 == 0) {
+            status[q] = GCK_EINVALID_KEY;  // core/db.go:295-297
+            continue;
+        }
+        int32_t st = GCK_EKEY_NOT_FOUND;
+        if (slots && len64 < 0xFFFFFFFFull) {
+            const uint32_t len = (uint32_t)len64;
+            const KeyWords k(keys, koff[q], len);
+            const uint64_t h = key_hash(k, len), mask = slots - 1;
+            for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+                const uint32_t cur = table[s];
+                if (cur == kEmpty) break;
+                if (khash[cur] != h || key_len(rec_hdr[cur]) != len) continue;
+                const KeyWords a(arena, rec_off[cur] + 16, len);
+                bool same = true;
+                for (uint32_t i = 0; same && 4 * i < len; ++i) same = a[i] == k[i];
+                if (!same) continue;
+                const gck_rec r = recs[cur];
+                if (!(r.flags & GCK_F_TOMBSTONE)) {
+                    if ((uint64_t)r.value_pos + r.value_size > flen[r.file]) {
+                        st = GCK_EIO;  // Disk.ReadFileAt short read
+                    } else {
+                        st = GCK_OK;   // pending the CRC
+                        item[q] = fbase[r.file] + r.value_pos;
+                        vsize[q] = r.value_size;
+                        expect[q] = r.crc;
+                    }
+                }
+                break;
+            }
+        }
+        status[q] = st;
+    }
+}
+
+// k_scrub_items: the live keydir entries as verify items (Get of every key).
+__global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__ live, uint64_t n,
+                                                     const uint64_t *__restrict__ fbase,
+                                                     const uint64_t *__restrict__ flen, int32_t *__restrict__ status,
+                                                     uint64_t *__restrict__ item, uint32_t *__restrict__ vsize,
+                                                     uint32_t *__restrict__ expect) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const gck_rec r = live[i];
+        const bool ok = (uint64_t)r.value_pos + r.value_size <= flen[r.file];
+        status[i] = ok ? GCK_OK : GCK_EIO;
+        item[i] = ok ? fbase[r.file] + r.value_pos : 0;
+        vsize[i] = ok ? r.value_size : 0;
+        expect[i] = r.crc;
+    }
+}
+
+// k_verify: one wavefront per item still GCK_OK: CRC of its bytes; a mismatch
+// is GCK_ECRC_FAILED; a match copies the value to dst + dst_off (if dst).
+__global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ arena, uint64_t n,
+                                                const uint64_t *__restrict__ item,
+                                                const uint32_t *__restrict__ vsize,
+                                                const uint32_t *__restrict__ expect, int32_t *__restrict__ status,
+                                                uint32_t *__restrict__ crc_out, const uint64_t *__restrict__ dst_off,
+                                                uint8_t *__restrict__ dst) {
+    __shared__ CrcTabs T;
+    crc_tables(T);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += waves) {
+        if (status[i] != GCK_OK) {
+            if (lane == 0) crc_out[i] = 0;
+            continue;
+        }
+        const uint8_t *p = arena + item[i];
+        const uint64_t L = vsize[i];
+        const uint32_t crc = wave_crc(p, L, T);
+        const bool ok = crc == expect[i];
+        if (lane == 0) {
+            crc_out[i] = crc;
+            if (!ok) status[i] = GCK_ECRC_FAILED;  // core/db.go:311-313
+        }
+        if (ok && dst) {
+            uint8_t *d = dst + dst_off[i];
+            for (uint64_t j = lane; j < L; j += 64) d[j] = p[j];
+        }
+    }
+}
+
+}  // namespace gck
+
+using namespace gck;
+
+extern "C" {
+
+int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, uint32_t n, int32_t *status,
+                      uint32_t *value_size, uint32_t *crc_calc, uint8_t *values, uint64_t values_cap,
+                      uint64_t *val_off, double *ms) {
+    if (!ctx || !key_off || !status || !value_size || !crc_calc || (values && !val_off)) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    if (!c->kd_valid) return GCK_EINVAL;  // gck_ctx_keydir after the run first
+    if (ms) *ms = 0;
+    if (!n) return GCK_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (key_off[i + 1] < key_off[i]) return GCK_EINVAL;
+    const uint64_t kb = key_off[n];
+    if (kb && !keys) return GCK_EINVAL;
+    int rc;
+    if ((rc = c->d_gkeys.ensure(kb + 16)) || (rc = c->d_gkoff.ensure((n + 1) * 8ull)) ||
+        (rc = c->d_gstat.ensure(n * 4ull)) || (rc = c->d_gitem.ensure(n * 8ull)) ||
+        (rc = c->d_gvsize.ensure(n * 4ull)) || (rc = c->d_gexp.ensure(n * 4ull)) ||
+        (rc = c->d_gcrc.ensure(n * 4ull)) || (rc = c->d_gvoff.ensure(n * 8ull)))
+        return rc;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    GCK_HIP(hipEventRecord(a, s));
+    GCK_HIP(hipMemsetAsync(c->d_gkeys.p, 0, kb + 16, s));
+    if (kb) GCK_HIP(hipMemcpyAsync(c->d_gkeys.p, keys, kb, hipMemcpyHostToDevice, s));
+    GCK_HIP(hipMemcpyAsync(c->d_gkoff.p, key_off, (n + 1) * 8ull, hipMemcpyHostToDevice, s));
+    k_get_lookup<<<(n + 255) / 256, 256, 0, s>>>(
+        c->d_gkeys.as<uint8_t>(), c->d_gkoff.as<uint64_t>(), n, c->d_ktab.as<uint32_t>(), c->kd_slots,
+        c->d_khash.as<uint64_t>(), c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+        c->d_out.as<gck_rec>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
+        c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>());
+    uint8_t *dvals = nullptr;
+    if (values) {  // value offsets of the found keys, back to back
+        GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            val_off[i] = status[i] == GCK_OK ? tot : ~0ull;
+            if (status[i] == GCK_OK) tot += value_size[i];
+        }
+        if (tot > values_cap) {
+            (void)hipEventDestroy(a);
+            (void)hipEventDestroy(b);
+            return GCK_EINVAL;
+        }
+        if ((rc = c->d_gvals.ensure(tot))) return rc;
+        GCK_HIP(hipMemcpyAsync(c->d_gvoff.p, val_off, n * 8ull, hipMemcpyHostToDevice, s));
+        dvals = c->d_gvals.as<uint8_t>();
+    }
+    const uint32_t grid = std::min<uint32_t>((n + 3) / 4, (uint32_t)c->n_cu * 16);
+    k_verify<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
+                                  c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
+                                  c->d_gvoff.as<uint64_t>(), dvals);
+    GCK_HIP(hipEventRecord(b, s));
+    GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(crc_calc, c->d_gcrc.p, n * 4ull, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    if (values) {
+        uint64_t tot = 0;
+        for (uint32_t i = 0; i < n; ++i)
+            if (val_off[i] != ~0ull) {
+                if (status[i] != GCK_OK) val_off[i] = ~0ull;  // CRC failed: no value
+                tot = std::max(tot, (val_off[i] == ~0ull ? 0 : val_off[i] + value_size[i]));
+            }
+        if (tot) GCK_HIP(hipMemcpy(values, dvals, tot, hipMemcpyDeviceToHost));
+    }
+    GCK_HIP(hipGetLastError());
+    float t = 0;
+    (void)hipEventElapsedTime(&t, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms) *ms = t;
+    return GCK_OK;
+}
+
+int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint64_t *n_bad, double *ms) {
+    if (!ctx || !n_bad) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    if (!c->kd_valid) return GCK_EINVAL;
+    *n_bad = 0;
+    if (ms) *ms = 0;
+    const uint64_t n = c->n_live;
+    if (!n) return GCK_OK;
+    int rc;
+    if ((rc = c->d_gstat.ensure(n * 4)) || (rc = c->d_gitem.ensure(n * 8)) || (rc = c->d_gvsize.ensure(n * 4)) ||
+        (rc = c->d_gexp.ensure(n * 4)) || (rc = c->d_gcrc.ensure(n * 4)))
+        return rc;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    GCK_HIP(hipEventRecord(a, s));
+    k_scrub_items<<<(uint32_t)c->n_cu * 8, 256, 0, s>>>(c->d_kdout.as<gck_rec>(), n, c->d_fbase.as<uint64_t>(),
+                                                       c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
+                                                       c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
+                                                       c->d_gexp.as<uint32_t>());
+    k_verify<<<(uint32_t)c->n_cu * 16, 256, 0, s>>>(c->arena.as<uint8_t>(), n, c->d_gitem.as<uint64_t>(),
+                                                    c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>(),
+                                                    c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(), nullptr,
+                                                    nullptr);
+    GCK_HIP(hipEventRecord(b, s));
+    std::vector<int32_t> st(status ? 0 : n);
+    int32_t *sp = status ? status : st.data();
+    GCK_HIP(hipMemcpyAsync(sp, c->d_gstat.p, n * 4, hipMemcpyDeviceToHost, s));
+    if (crc_calc) GCK_HIP(hipMemcpyAsync(crc_calc, c->d_gcrc.p, n * 4, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    GCK_HIP(hipGetLastError());
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; ++i) bad += sp[i] != GCK_OK;
+    *n_bad = bad;
+    float t = 0;
+    (void)hipEventElapsedTime(&t, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms) *ms = t;
+    return GCK_OK;
+}
+
+}  // extern "C"

@@ -7,37 +7,9 @@
 // entry if it is a tombstone.  This file computes exactly that set on the
 // device from the last gck_ctx_run, so only live entries cross PCIe and enter
 // the Go map (gck_ctx_fetch_keydir).
-#include "gck_internal.h"
+#include "kd_common.h"
 
 namespace gck {
-
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
-constexpr int kKdTile = 1024;  // records per compaction tile (one workgroup)
-
-// Key of a record: KeySize bytes after the header, or ValueSize bytes for a
-// tombstone (KeySize 0; core/db.go:151-155).
-__device__ __forceinline__ uint32_t key_len(const uint4 &h) { return h.z ? h.z : h.w; }
-
-__device__ __forceinline__ uint64_t mix64d(uint64_t x) {
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
-// Word i (4 key bytes, little-endian) of a key at arena offset o, read as
-// aligned dwords and funnel-shifted; bytes past the key are masked to zero
-// (the arena is padded, so the word after the key is always readable).
-struct KeyWords {
-    const uint32_t *w;
-    uint32_t sh, len;
-    __device__ KeyWords(const uint8_t *arena, uint64_t o, uint32_t n)
-        : w(reinterpret_cast<const uint32_t *>(arena + (o & ~3ull))), sh((uint32_t)(o & 3)), len(n) {}
-    __device__ __forceinline__ uint32_t operator[](uint32_t i) const {
-        const uint32_t v = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
-        const uint32_t left = len - 4 * i;
-        return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
-    }
-};
 
 // k_key_hash: one lane per record, a 64-bit hash of its key bytes.
 __global__ __launch_bounds__(256) void k_key_hash(const uint8_t *__restrict__ arena,
@@ -46,10 +18,7 @@ __global__ __launch_bounds__(256) void k_key_hash(const uint8_t *__restrict__ ar
                                                   uint64_t *__restrict__ khash) {
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t len = key_len(rec_hdr[r]);
-        const KeyWords k(arena, rec_off[r] + 16, len);
-        uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)len << 32);
-        for (uint32_t i = 0; 4 * i < len; ++i) h = mix64d(h ^ k[i]) + i;
-        khash[r] = mix64d(h);
+        khash[r] = key_hash(KeyWords(arena, rec_off[r] + 16, len), len);
     }
 }
 
@@ -365,8 +334,13 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     Ctx *c = &ctx->c;
     *n_live = 0;
     c->n_live = 0;
+    c->kd_valid = false;
     const uint64_t n = c->n_recs;
-    if (!n) return GCK_OK;
+    if (!n) {
+        c->kd_valid = true;
+        c->kd_slots = 0;
+        return GCK_OK;
+    }
     if (n >= kEmpty) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -407,6 +381,8 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     (void)hipEventDestroy(b);
     if (ms) *ms = t;
     c->n_live = live;
+    c->kd_valid = true;
+    c->kd_slots = slots;
     *n_live = live;
     return GCK_OK;
 }

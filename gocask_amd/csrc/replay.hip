@@ -1269,7 +1269,9 @@ static void ctx_free(Ctx *c) {
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
-                   &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys};
+                   &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
+                   &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
+                   &c->d_gvoff, &c->d_gvals};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1679,6 +1681,7 @@ static int ctx_run_device(Ctx *c) {
 static int ctx_run(Ctx *c) {
     c->n_live = 0;  // the keydir (and its pack) belong to the previous run
     c->kd_nparts = 0;
+    c->kd_valid = false;
     if (c->rec_cap > 0 && c->nfiles > 0) {
         const int rc = ctx_run_device(c);
         if (rc != GCK_ERERUN) return rc;

@@ -139,6 +139,24 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
 int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 
+/* ---- batched Get / keydir scrub -------------------------
+ * DB.Get (core/db.go:287-316) for n keys against the device keydir of the last
+ * run (call gck_ctx_keydir first, any flags): keys[key_off[i], key_off[i+1]) is
+ * key i.  Per key: status[i] = GCK_OK, GCK_EINVALID_KEY (empty key),
+ * GCK_EKEY_NOT_FOUND (absent or deleted), GCK_EIO (ValuePos + ValueSize past the
+ * end of the entry's file: Disk.ReadFileAt's short read) or GCK_ECRC_FAILED;
+ * value_size[i] = the entry's ValueSize; crc_calc[i] = CRC-32/IEEE recomputed
+ * on the device from the resident file bytes at (File, ValuePos).  With values
+ * != NULL the values of the GCK_OK keys are copied back to back, val_off[i]
+ * their offsets (UINT64_MAX for the others); GCK_EINVAL if they exceed
+ * values_cap (status / value_size are then filled, for a retry). */
+int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, uint32_t n, int32_t *status,
+                      uint32_t *value_size, uint32_t *crc_calc, uint8_t *values, uint64_t values_cap,
+                      uint64_t *val_off, double *ms);
+/* Integrity scrub: Get of every live keydir entry (gck_ctx_keydir order);
+ * status / crc_calc (optional, n_live each) as above; *n_bad = entries not OK. */
+int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint64_t *n_bad, double *ms);
+
 /* ---- keydir merge across shards ----------------------------
  * Files shard over GPUs in walk order: shard s holds a contiguous run of files,
  * every one but the last shard's last file with reset_after = 1, so each shard
