@@ -11,13 +11,12 @@
 
 namespace gck {
 
-// LDS tables (32 KiB per workgroup): slicing-by-4 (T), and multiplication by
-// the constants Z_1008 (Zs) and Z_{16 * 2^k}, k = 0..5 (Zt), each as four
-// byte tables: Z(A) = XOR_k Z[k][byte k of A] (Z is linear in A).
+// LDS tables (8 KiB per workgroup): slicing-by-4 (T), and multiplication by
+// the constant Z_1008 as four byte tables: Z(A) = XOR_k Zs[k][byte k of A]
+// (Z is linear in A).
 struct CrcTabs {
     uint32_t T[4][256];
     uint32_t Zs[4][256];
-    uint32_t Zt[6][4][256];
 };
 
 __device__ void crc_tables(CrcTabs &t) {
@@ -34,61 +33,77 @@ __device__ void crc_tables(CrcTabs &t) {
             t.T[k][i] = c;
         }
     }
-    for (uint32_t e = threadIdx.x; e < 7 * 1024; e += blockDim.x) {
-        const uint32_t m = e >> 10, k = (e >> 8) & 3, i = e & 0xFF;
-        const uint32_t z = xpow8n(m == 0 ? 1008u : (16u << (m - 1)));
-        const uint32_t v = multmodp(z, i << (8 * k));
-        if (m == 0)
-            t.Zs[k][i] = v;
-        else
-            t.Zt[m - 1][k][i] = v;
-    }
+    const uint32_t z = xpow8n(1008);
+    for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) t.Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
     __syncthreads();
+}
+
+// a * b mod P (reflected), 32 steps without early exit (a varies by lane).
+__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+        p ^= (a & (0x80000000u >> i)) ? b : 0u;
+        b = (b >> 1) ^ ((b & 1u) ? kPoly : 0u);
+    }
+    return p;
 }
 
 __device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
     return Z[0][a & 0xFF] ^ Z[1][(a >> 8) & 0xFF] ^ Z[2][(a >> 16) & 0xFF] ^ Z[3][a >> 24];
 }
 
-// crc32.ChecksumIEEE of p[0, L) by one wavefront.  The value is read as a
-// virtual buffer of J = ceil(L / 1 KiB) stripes, zero-padded at the FRONT
-// (F(0, .) ignores leading zeros), lane l taking the 16 bytes at 16 l of every
-// stripe: coalesced loads.  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner
-// over the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement
-// of the value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).
-// A shuffle tree then joins the lanes, lane l's part shifted past the 16 (63-l)
-// bytes after it: F(~0, V); crc = that ^ 0xFFFFFFFF.
-__device__ uint32_t wave_crc(const uint8_t *__restrict__ p, uint64_t L, const CrcTabs &t) {
+// The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
+// pad bytes): aligned dword loads, only of dwords that reach into the value.
+__device__ __forceinline__ void stripe_load(const uint8_t *p, uint64_t v, uint64_t pad, uint32_t d[5]) {
+    const uintptr_t q = reinterpret_cast<uintptr_t>(p) + v - pad, a = q & ~(uintptr_t)3;
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(p);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) d[i] = a + 4 * i + 4 > p0 ? reinterpret_cast<const uint32_t *>(a)[i] : 0u;
+}
+
+// Start of a value's CRC: J = ceil(L / 1 KiB) stripes, pad = J KiB - L.
+struct CrcJob {
+    const uint8_t *p;
+    uint64_t L, J, pad;
+    __device__ CrcJob(const uint8_t *p_, uint64_t L_) : p(p_), L(L_), J((L_ + 1023) >> 10), pad((J << 10) - L_) {}
+};
+
+// crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
+// virtual buffer of J stripes of 1 KiB, zero-padded at the FRONT (F(0, .)
+// ignores leading zeros), lane l taking the 16 bytes at 16 l of every stripe:
+// coalesced loads, the next stripe's issued before this one is folded (after
+// the last one: the first stripe of the next value, `nx`).  dn holds this
+// value's first stripe on entry.  Lane state: A <- F(Z_1008(A), chunk), i.e.
+// Horner over the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the
+// complement of the value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3
+// ^ 0xFF)).  Lane l's part is finally shifted past the 16 (63-l) bytes after it
+// (kl = x^(8 * 16 (63-l))) and the lanes XOR-reduced: F(~0, V); crc = ~that.
+__device__ uint32_t wave_crc(const CrcJob &jb, uint32_t dn[5], const CrcJob *nx, uint32_t kl, const CrcTabs &t) {
     const uint32_t lane = threadIdx.x & 63;
-    if (L < 4) {  // fewer bytes than the init register
-        uint32_t c = 0xFFFFFFFFu;
-        for (uint64_t i = 0; i < L; ++i) c = t.T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
-        return ~c;
-    }
-    const uint64_t J = (L + 1023) >> 10, pad = (J << 10) - L;
-    const uint8_t *base = p + (16ull * lane - pad);  // (virtual position 16 l of stripe 0), maybe before p
     uint32_t A = 0;
-    for (uint64_t j = 0; j < J; ++j) {
+    for (uint64_t j = 0; j < jb.J; ++j) {
         const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        if (v >= pad) {
-            const uint8_t *q = base + (j << 10);
-            const uint32_t *a = reinterpret_cast<const uint32_t *>(reinterpret_cast<uintptr_t>(q) & ~(uintptr_t)3);
-            const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(q) & 3);
-            uint32_t d[5];
+        uint32_t d[5];
 #pragma unroll
-            for (int i = 0; i < 5; ++i) d[i] = a[i];
+        for (int i = 0; i < 5; ++i) d[i] = dn[i];
+        if (j + 1 < jb.J)
+            stripe_load(jb.p, v + 1024, jb.pad, dn);
+        else if (nx)
+            stripe_load(nx->p, 16ull * lane, nx->pad, dn);
+        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(jb.p) + v - jb.pad) & 3);
+        uint32_t w[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        } else if (v + 16 > pad) {  // straddles the value's start: bytes before it are zero
+        for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+        if (v < jb.pad + 4) {  // chunks at the value's start: bytes before it are zero, its first 4 complemented
 #pragma unroll
-            for (int b = 0; b < 16; ++b)
-                if (v + b >= pad) w[b >> 2] |= (uint32_t)p[v + b - pad] << (8 * (b & 3));
-        }
-        if (v + 16 > pad && v < pad + 4) {  // complement the value's first 4 bytes (may reach stripe 1)
-#pragma unroll
-            for (int b = 0; b < 16; ++b)
-                if (v + b >= pad && v + b < pad + 4) w[b >> 2] ^= 0xFFu << (8 * (b & 3));
+            for (int i = 0; i < 4; ++i) {
+                const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
+                const uint32_t keep = lead >= 4 ? 0u : lead <= 0 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (8 * lead);
+                const int64_t cl = lead + 4;  // bytes of dword i before the value's byte 4
+                const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
+                w[i] = (w[i] & keep) ^ (flip & keep);
+            }
         }
         uint32_t c = zmul(t.Zs, A);
 #pragma unroll
@@ -98,12 +113,17 @@ __device__ uint32_t wave_crc(const uint8_t *__restrict__ p, uint64_t L, const Cr
         }
         A = c;
     }
+    A = gmul(kl, A);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {  // lanes l = 0 mod 2^(k+1): Z_{16 * 2^k}(left) ^ right
-        const uint32_t right = __shfl_down(A, 1u << k);
-        A = zmul(t.Zt[k], A) ^ right;
-    }
-    return ~__shfl(A, 0);
+    for (int k = 32; k >= 1; k >>= 1) A ^= __shfl_xor(A, k);
+    return ~A;
+}
+
+// Values shorter than the init register, on lane 0's bytes (broadcast).
+__device__ uint32_t short_crc(const uint8_t *p, uint64_t L, const CrcTabs &t) {
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint64_t i = 0; i < L; ++i) c = t.T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
+    return ~c;
 }
 
 // k_get_lookup: one lane per query key (keys: a blob padded by 8 bytes, koff:
@@ -176,8 +196,10 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
     }
 }
 
-// k_verify: one wavefront per item still GCK_OK: CRC of its bytes; a mismatch
-// is GCK_ECRC_FAILED; a match copies the value to dst + dst_off (if dst).
+// k_verify: a wavefront takes 64 items (one per lane: status, location, size,
+// expected CRC in one coalesced load each), then the CRC of every item still
+// GCK_OK in turn, all lanes on one value; a mismatch is GCK_ECRC_FAILED, a
+// match copies the value to dst + dst_off (if dst).
 __global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ arena, uint64_t n,
                                                 const uint64_t *__restrict__ item,
                                                 const uint32_t *__restrict__ vsize,
@@ -187,23 +209,53 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ aren
     __shared__ CrcTabs T;
     crc_tables(T);
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += waves) {
-        if (status[i] != GCK_OK) {
-            if (lane == 0) crc_out[i] = 0;
-            continue;
+    const uint32_t kl = xpow8n(16ull * (63 - lane));  // lane l's chunk is followed by 16 (63-l) bytes of its stripe
+    const uint64_t groups = (n + 63) >> 6, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); gi < groups; gi += waves) {
+        const uint64_t mine = (gi << 6) + lane;
+        const bool have = mine < n;
+        const bool ok = have && status[mine] == GCK_OK;
+        const uint64_t off = ok ? item[mine] : 0;
+        const uint32_t len = ok ? vsize[mine] : 0u, want = ok ? expect[mine] : 0u;
+        const uint64_t doff = ok && dst ? dst_off[mine] : 0;
+        uint32_t crc = 0, dn[5] = {0u, 0u, 0u, 0u, 0u};
+        uint64_t todo = __ballot(ok && len >= 4);
+        for (uint64_t sm = __ballot(ok && len < 4); sm; sm &= sm - 1) {  // 0..3-byte values
+            const int t = __builtin_ctzll(sm);
+            const uint32_t c = short_crc(arena + __shfl(off, t), __shfl(len, t), T);
+            if (lane == (uint32_t)t) crc = c;
         }
-        const uint8_t *p = arena + item[i];
-        const uint64_t L = vsize[i];
-        const uint32_t crc = wave_crc(p, L, T);
-        const bool ok = crc == expect[i];
-        if (lane == 0) {
-            crc_out[i] = crc;
-            if (!ok) status[i] = GCK_ECRC_FAILED;  // core/db.go:311-313
+        if (todo) {
+            const int t0 = __builtin_ctzll(todo);
+            const CrcJob first(arena + __shfl(off, t0), __shfl(len, t0));
+            stripe_load(first.p, 16ull * lane, first.pad, dn);
         }
-        if (ok && dst) {
-            uint8_t *d = dst + dst_off[i];
-            for (uint64_t j = lane; j < L; j += 64) d[j] = p[j];
+        while (todo) {
+            const int t = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const CrcJob cur(arena + __shfl(off, t), __shfl(len, t));
+            uint32_t c;
+            if (todo) {
+                const int t2 = __builtin_ctzll(todo);
+                const CrcJob nx(arena + __shfl(off, t2), __shfl(len, t2));
+                c = wave_crc(cur, dn, &nx, kl, T);
+            } else {
+                c = wave_crc(cur, dn, nullptr, kl, T);
+            }
+            if (lane == (uint32_t)t) crc = c;
+        }
+        if (dst) {  // the values that passed, copied by the whole wave
+            for (uint64_t cp = __ballot(ok && crc == want); cp; cp &= cp - 1) {
+                const int t = __builtin_ctzll(cp);
+                uint8_t *d = dst + __shfl(doff, t);
+                const uint8_t *src = arena + __shfl(off, t);
+                const uint32_t L = __shfl(len, t);
+                for (uint64_t j = lane; j < L; j += 64) d[j] = src[j];
+            }
+        }
+        if (have) {
+            crc_out[mine] = crc;
+            if (ok && crc != want) status[mine] = GCK_ECRC_FAILED;  // core/db.go:311-313
         }
     }
 }
@@ -265,7 +317,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
         GCK_HIP(hipMemcpyAsync(c->d_gvoff.p, val_off, n * 8ull, hipMemcpyHostToDevice, s));
         dvals = c->d_gvals.as<uint8_t>();
     }
-    const uint32_t grid = std::min<uint32_t>((n + 3) / 4, (uint32_t)c->n_cu * 16);
+    const uint32_t grid = std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 16);
     k_verify<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
                                   c->d_gvoff.as<uint64_t>(), dvals);
