@@ -119,10 +119,32 @@ __device__ uint32_t wave_crc(const CrcJob &jb, uint32_t dn[5], const CrcJob *nx,
     return ~A;
 }
 
-// Values shorter than the init register, on lane 0's bytes (broadcast).
-__device__ uint32_t short_crc(const uint8_t *p, uint64_t L, const CrcTabs &t) {
-    uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = 0; i < L; ++i) c = t.T[0][(c ^ p[i]) & 0xFF] ^ (c >> 8);
+constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
+
+// crc32.ChecksumIEEE of a small value by one lane (lanes run different
+// values): aligned dwords, 64 bytes of loads in flight per round, slicing-by-4
+// per word, the last 0..3 bytes one at a time.
+__device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t) {
+    const uintptr_t q = reinterpret_cast<uintptr_t>(p);
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(q & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(q & 3), nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
+    uint32_t c = 0xFFFFFFFFu, pos = 0;
+    for (uint32_t b = 0; __ballot(b < nw); b += 16) {
+        uint32_t d[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+            if (pos + 4 <= L) {
+                c ^= w;
+                c = t.T[3][c & 0xFF] ^ t.T[2][(c >> 8) & 0xFF] ^ t.T[1][(c >> 16) & 0xFF] ^ t.T[0][c >> 24];
+            } else {
+                for (uint32_t k = 0; pos + k < L; ++k) c = t.T[0][(c ^ (w >> (8 * k))) & 0xFF] ^ (c >> 8);
+            }
+            pos = pos + 4 <= L ? pos + 4 : L;
+        }
+    }
     return ~c;
 }
 
@@ -219,11 +241,11 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ aren
         const uint32_t len = ok ? vsize[mine] : 0u, want = ok ? expect[mine] : 0u;
         const uint64_t doff = ok && dst ? dst_off[mine] : 0;
         uint32_t crc = 0, dn[5] = {0u, 0u, 0u, 0u, 0u};
-        uint64_t todo = __ballot(ok && len >= 4);
-        for (uint64_t sm = __ballot(ok && len < 4); sm; sm &= sm - 1) {  // 0..3-byte values
-            const int t = __builtin_ctzll(sm);
-            const uint32_t c = short_crc(arena + __shfl(off, t), __shfl(len, t), T);
-            if (lane == (uint32_t)t) crc = c;
+        const bool small = ok && len <= kLaneMax;
+        uint64_t todo = __ballot(ok && !small);
+        if (__ballot(small)) {  // small values: a lane each, all at once
+            const uint32_t c = lane_crc(arena + off, len, small, T);
+            if (small) crc = c;
         }
         if (todo) {
             const int t0 = __builtin_ctzll(todo);
