@@ -154,8 +154,7 @@ __device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTa
 // the arena offset of ValueSize bytes at ValuePos of the entry's file.
 __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ keys,
                                                     const uint64_t *__restrict__ koff, uint32_t n,
-                                                    const uint32_t *__restrict__ table, uint64_t slots,
-                                                    const uint64_t *__restrict__ khash,
+                                                    const unsigned long long *__restrict__ table, uint64_t slots,
                                                     const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ rec_off,
                                                     const uint4 *__restrict__ rec_hdr,
@@ -176,10 +175,12 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
             const uint32_t len = (uint32_t)len64;
             const KeyWords k(keys, koff[q], len);
             const uint64_t h = key_hash(k, len), mask = slots - 1;
+            const uint32_t tag = slot_tag(h);
             for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-                const uint32_t cur = table[s];
-                if (cur == kEmpty) break;
-                if (khash[cur] != h || key_len(rec_hdr[cur]) != len) continue;
+                const unsigned long long v = table[s];
+                if (v == kEmptySlot) break;
+                const uint32_t cur = (uint32_t)v;
+                if ((uint32_t)(v >> 32) != tag || key_len(rec_hdr[cur]) != len) continue;
                 const KeyWords a(arena, rec_off[cur] + 16, len);
                 bool same = true;
                 for (uint32_t i = 0; same && 4 * i < len; ++i) same = a[i] == k[i];
@@ -316,8 +317,8 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     if (kb) GCK_HIP(hipMemcpyAsync(c->d_gkeys.p, keys, kb, hipMemcpyHostToDevice, s));
     GCK_HIP(hipMemcpyAsync(c->d_gkoff.p, key_off, (n + 1) * 8ull, hipMemcpyHostToDevice, s));
     k_get_lookup<<<(n + 255) / 256, 256, 0, s>>>(
-        c->d_gkeys.as<uint8_t>(), c->d_gkoff.as<uint64_t>(), n, c->d_ktab.as<uint32_t>(), c->kd_slots,
-        c->d_khash.as<uint64_t>(), c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+        c->d_gkeys.as<uint8_t>(), c->d_gkoff.as<uint64_t>(), n, c->d_ktab.as<unsigned long long>(), c->kd_slots,
+        c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
         c->d_out.as<gck_rec>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
         c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>());
     uint8_t *dvals = nullptr;

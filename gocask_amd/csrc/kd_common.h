@@ -41,4 +41,13 @@ __device__ __forceinline__ uint64_t key_hash(const KeyWords &k, uint32_t len) {
     return mix64d(h);
 }
 
+// Table slot: the key's hash tag (bits 32..63 of its hash, never all ones)
+// above the index of its record; all ones = empty.  Same key => same tag, so
+// a 64-bit max keeps the larger record index.
+constexpr unsigned long long kEmptySlot = ~0ull;
+__device__ __forceinline__ uint32_t slot_tag(uint64_t h) {
+    const uint32_t t = (uint32_t)(h >> 32);
+    return t == 0xFFFFFFFFu ? 0xFFFFFFFEu : t;
+}
+
 }  // namespace gck

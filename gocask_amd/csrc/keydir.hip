@@ -11,17 +11,6 @@
 
 namespace gck {
 
-// k_key_hash: one lane per record, a 64-bit hash of its key bytes.
-__global__ __launch_bounds__(256) void k_key_hash(const uint8_t *__restrict__ arena,
-                                                  const uint64_t *__restrict__ rec_off,
-                                                  const uint4 *__restrict__ rec_hdr, uint64_t n,
-                                                  uint64_t *__restrict__ khash) {
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t len = key_len(rec_hdr[r]);
-        khash[r] = key_hash(KeyWords(arena, rec_off[r] + 16, len), len);
-    }
-}
-
 __device__ bool same_key(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off, uint64_t a,
                          uint64_t b, uint32_t len) {
     const KeyWords ka(arena, rec_off[a] + 16, len), kb(arena, rec_off[b] + 16, len);
@@ -30,28 +19,38 @@ __device__ bool same_key(const uint8_t *__restrict__ arena, const uint64_t *__re
     return true;
 }
 
-// k_kd_insert: one lane per record into an open-addressing table of record
-// indices.  A slot is claimed by CAS; records of the same key (hash, length
-// and bytes equal) keep the largest index with atomicMax, so the last writer
-// in walk order wins whatever order the lanes run in.  Keys are never removed,
-// so a probe sequence never skips a key's slot.
+// k_kd_insert: one lane per record: the 64-bit hash of its key (kept in
+// khash for the merge), then an open-addressing insert into a table of
+// (tag, record index) slots.  A slot is claimed by CAS; a probe compares the
+// slot's tag before any key bytes; records of the same key (tag, length and
+// bytes equal) keep the largest index with a 64-bit atomicMax, so the last
+// writer in walk order wins whatever order the lanes run in.  Keys are never
+// removed, so a probe sequence never skips a key's slot.
 __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ arena,
                                                    const uint64_t *__restrict__ rec_off,
-                                                   const uint4 *__restrict__ rec_hdr,
-                                                   const uint64_t *__restrict__ khash, uint64_t n,
-                                                   uint32_t *__restrict__ table, uint64_t mask) {
+                                                   const uint4 *__restrict__ rec_hdr, uint64_t n,
+                                                   uint64_t *__restrict__ khash,
+                                                   unsigned long long *__restrict__ table, uint64_t mask) {
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t h = khash[r];
         const uint32_t len = key_len(rec_hdr[r]);
+        const uint64_t h = key_hash(KeyWords(arena, rec_off[r] + 16, len), len);
+        khash[r] = h;
+        const uint32_t tag = slot_tag(h);
+        const unsigned long long mine = ((unsigned long long)tag << 32) | r;
         for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-            uint32_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur == kEmpty) {
-                const uint32_t prev = atomicCAS(table + s, kEmpty, (uint32_t)r);
-                if (prev == kEmpty) break;  // claimed
+            // a plain read: a slot only goes EMPTY -> (tag, i) -> (tag, larger
+            // i), so a stale value is EMPTY (the CAS then returns the truth) or
+            // an older record of the same key
+            unsigned long long cur = table[s];
+            if (cur == kEmptySlot) {
+                const unsigned long long prev = atomicCAS(table + s, kEmptySlot, mine);
+                if (prev == kEmptySlot) break;  // claimed
                 cur = prev;
             }
-            if (khash[cur] == h && key_len(rec_hdr[cur]) == len && same_key(arena, rec_off, cur, r, len)) {
-                atomicMax(table + s, (uint32_t)r);  // same key: the later record wins
+            if ((uint32_t)(cur >> 32) != tag) continue;
+            const uint32_t ci = (uint32_t)cur;
+            if (key_len(rec_hdr[ci]) == len && same_key(arena, rec_off, ci, r, len)) {
+                if (ci < r) atomicMax(table + s, mine);  // same key: the later record wins
                 break;
             }
         }
@@ -61,12 +60,14 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
 // k_kd_mark: one lane per slot; the key's winning record is live if it is a
 // Put (or, for a merge across shards, always: tombstones then stay as delete
 // markers).
-__global__ __launch_bounds__(256) void k_kd_mark(const uint32_t *__restrict__ table, uint64_t slots,
+__global__ __launch_bounds__(256) void k_kd_mark(const unsigned long long *__restrict__ table, uint64_t slots,
                                                  const uint4 *__restrict__ rec_hdr, uint32_t keep_tombstones,
                                                  uint32_t *__restrict__ live) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = table[s];
-        if (r != kEmpty && (keep_tombstones || rec_hdr[r].z != 0)) live[r] = 1;
+        const unsigned long long v = table[s];
+        if (v == kEmptySlot) continue;
+        const uint32_t r = (uint32_t)v;
+        if (keep_tombstones || rec_hdr[r].z != 0) live[r] = 1;
     }
 }
 
@@ -345,10 +346,10 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     uint64_t slots = 1024;
-    while (slots < 2 * n) slots <<= 1;  // load factor <= 1/2
+    while (slots < n + n / 4) slots <<= 1;  // load <= 0.8 with every key distinct; slots hold keys, not records
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
     int rc;
-    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 4)) || (rc = c->d_live.ensure(n * 4)) ||
+    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 8)) || (rc = c->d_live.ensure(n * 4)) ||
         (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))) ||
         (rc = c->d_kdidx.ensure(n * 4)))
         return rc;
@@ -356,14 +357,12 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
     GCK_HIP(hipEventRecord(a, s));
-    GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 4, s));
+    GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8, s));
     GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
     const uint32_t grid = (uint32_t)c->n_cu * 8;
-    k_key_hash<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), n,
-                                    c->d_khash.as<uint64_t>());
-    k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
-                                     c->d_khash.as<uint64_t>(), n, c->d_ktab.as<uint32_t>(), slots - 1);
-    k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<uint32_t>(), slots, c->d_rec_hdr.as<uint4>(),
+    k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), n,
+                                     c->d_khash.as<uint64_t>(), c->d_ktab.as<unsigned long long>(), slots - 1);
+    k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_hdr.as<uint4>(),
                                    (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>());
     k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
     k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);
