@@ -43,28 +43,69 @@ DESCR = {
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
-def cpu_baseline(cfg_name, sample_bytes):
-    """Oracle (C port of the reference replay: header decode, CRC verdict,
-    hash-map keydir) on host cores, 1 thread, on a bounded sample of the same
-    workload: the first file of the corpus (same spec, same seed)."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _timed(fn, min_s=4.0):
+    reps, t = 0, 0.0
+    while t < min_s or reps < 1:
+        t0 = time.perf_counter()
+        out = fn()
+        t += time.perf_counter() - t0
+        reps += 1
+    return out, reps, t
+
+
+def cpu_baseline(cfg_name, sample_bytes, max_threads=16, min_s=4.0, mt_file_bytes=256 << 20):
+    """Oracle (C port of the reference replay) on host cores, on bounded samples
+    of the same workload (SURVEY.md §8d's three variants):
+      ref_faithful  1 thread: header decode, every byte through a 4 KiB buffer (bufio), key,
+                    hash-map keydir, no CRC (core/db.go:125-178);
+      ref_crc       1 thread: the same plus the CRC verdict per record (the primary value);
+      all_cores     one thread per file (up to max_threads, the box's CPU share), + CRC,
+                    a keydir per file (no cross-file merge)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
+    from concurrent.futures import ThreadPoolExecutor
 
     oracle.build()
     kw = dict(CONFIGS[cfg_name])
     kw["n_files"] = 1
     kw["max_file_size"] = min(kw["max_file_size"], sample_bytes)
     files, _ = oracle.gen_corpus(**kw)
-    reps, t = 0, 0.0
-    while t < 4.0 or reps < 1:
-        t0 = time.perf_counter()
-        live, st = oracle.baseline(files, [False])
-        t += time.perf_counter() - t0
-        reps += 1
     nbytes = sum(len(f) for f in files)
-    return dict(value=round(nbytes * reps / t / GiB, 3), unit="GiB/s", cores=1, kind="port",
-                sample=f"first file of the {cfg_name.upper()} corpus ({nbytes / GiB:.2f} GiB, {st['n_recs']} records),"
-                       f" single-thread oracle replay + CRC verdict + hash-map keydir, {reps} pass(es)")
+    (_, st), reps, t = _timed(lambda: oracle.baseline(files, [False]), min_s)
+    (_, _), reps0, t0 = _timed(lambda: oracle.baseline(files, [False], verify_crc=False), min_s)
+    what = f"first file of the {cfg_name.upper()} corpus ({nbytes / GiB:.2f} GiB, {st['n_recs']} records)"
+    variants = dict(
+        ref_faithful=dict(value=round(nbytes * reps0 / t0 / GiB, 3), cores=1,
+                          sample=what + ", bytes through a 4 KiB buffer, no CRC (the reference's replay)"),
+        ref_crc=dict(value=round(nbytes * reps / t / GiB, 3), cores=1, sample=what + ", + CRC verdict"),
+    )
+    nproc = os.cpu_count() or 1
+    nt = max(1, min(nproc, max_threads, 16))
+    kw_mt = dict(CONFIGS[cfg_name])
+    kw_mt["n_files"] = nt
+    kw_mt["max_file_size"] = min(kw_mt["max_file_size"], mt_file_bytes)
+    mfiles, _ = oracle.gen_corpus(**kw_mt)
+    mbytes = sum(len(f) for f in mfiles)
+    with ThreadPoolExecutor(max_workers=nt) as ex:
+        def run_all():
+            return list(ex.map(lambda f: oracle.baseline([f], [True]), mfiles))
+        _, reps2, t2 = _timed(run_all, min_s)
+    variants["all_cores"] = dict(value=round(mbytes * reps2 / t2 / GiB, 3), cores=nt,
+                                 sample=f"{len(mfiles)} files of the {cfg_name.upper()} spec ({mbytes / GiB:.2f} GiB), "
+                                        f"one thread per file, + CRC verdict, a keydir per file")
+    return dict(value=variants["ref_crc"]["value"], unit="GiB/s", cores=1, kind="port",
+                sample=what + f", single-thread oracle replay + CRC verdict + hash-map keydir, {reps} pass(es)",
+                variants=variants, nproc=nproc, cpu_model=_cpu_model())
 
 
 def host_inclusive(g, ctx, info, steps):

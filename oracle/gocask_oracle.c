@@ -185,21 +185,43 @@ static inline int hm_eq(const hmap *m, uint64_t a, const uint8_t *p, uint32_t n)
     return m->kl[a] == n && memcmp(m->kp[a], p, n) == 0;
 }
 
-static void hm_set(hmap *m, uint64_t idx) {
+/* returns 1 when idx's key was not in the map */
+static int hm_set(hmap *m, uint64_t idx) {
     const uint8_t *p = m->kp[idx];
     uint32_t n = m->kl[idx];
     uint64_t h = hkey(p, n), i = h & m->mask;
     for (;;) {
-        if (!m->slot[i]) { m->slot[i] = idx + 1; m->hash[i] = h; return; }
-        if (m->hash[i] == h && hm_eq(m, m->slot[i] - 1, p, n)) { m->slot[i] = idx + 1; return; }
+        if (!m->slot[i]) { m->slot[i] = idx + 1; m->hash[i] = h; return 1; }
+        if (m->hash[i] == h && hm_eq(m, m->slot[i] - 1, p, n)) { m->slot[i] = idx + 1; return 0; }
         i = (i + 1) & m->mask;
     }
 }
 
-static void hm_del(hmap *m, const uint8_t *p, uint32_t n) {
+/* double the slots (the timed baseline grows its map as Go's does) */
+static int hm_grow(hmap *m) {
+    const uint64_t ocap = m->mask + 1, cap = ocap * 2;
+    uint64_t *slot = calloc(cap, sizeof(uint64_t)), *hash = calloc(cap, sizeof(uint64_t));
+    if (!slot || !hash) { free(slot); free(hash); return -1; }
+    for (uint64_t j = 0; j < ocap; j++) {
+        if (!m->slot[j]) continue;
+        uint64_t i = m->hash[j] & (cap - 1);
+        while (slot[i]) i = (i + 1) & (cap - 1);
+        slot[i] = m->slot[j];
+        hash[i] = m->hash[j];
+    }
+    free(m->slot);
+    free(m->hash);
+    m->slot = slot;
+    m->hash = hash;
+    m->mask = cap - 1;
+    return 0;
+}
+
+/* returns 1 when the key was present */
+static int hm_del(hmap *m, const uint8_t *p, uint32_t n) {
     uint64_t h = hkey(p, n), i = h & m->mask;
     for (;;) {
-        if (!m->slot[i]) return; /* delete of an absent key is a no-op */
+        if (!m->slot[i]) return 0; /* delete of an absent key is a no-op */
         if (m->hash[i] == h && hm_eq(m, m->slot[i] - 1, p, n)) break;
         i = (i + 1) & m->mask;
     }
@@ -215,6 +237,7 @@ static void hm_del(hmap *m, const uint8_t *p, uint32_t n) {
         }
     }
     m->slot[i] = 0;
+    return 1;
 }
 
 static int cmp_u64(const void *a, const void *b) {
@@ -249,13 +272,20 @@ uint64_t orc_keydir(const orc_file *files, const orc_rec *recs, uint64_t n, uint
 /* Timed CPU baseline: the same loop as orc_replay, but with the keydir map
  * update inline and no per-record output array (what the single-goroutine
  * reference does in core/db.go:131-140 + keydir.go:22-49). */
-uint64_t orc_baseline(const orc_file *files, uint32_t nfiles, int verify_crc, orc_status *st) {
-    uint64_t total = 0;
-    for (uint32_t f = 0; f < nfiles; f++) total += files[f].len / 16 + 1;
+/* flags: 1 = CRC verdict per record; 2 = copy the key and value bytes
+ * through a 4 KiB buffer, as walkFile's bufio.Reader (core/db.go:126) does
+ * for ReadFull(key) and Discard(ValueSize). */
+uint64_t orc_baseline(const orc_file *files, uint32_t nfiles, int flags, orc_status *st) {
+    const int verify_crc = flags & 1, bufio = flags & 2;
+    uint8_t buf[4096];
+    uint64_t sink = 0;
+    /* the map and the key arrays grow as the reference's map does (doubling),
+     * instead of being sized for the worst case of 16-byte records */
     hmap m;
-    if (hm_init(&m, total)) return 0;
-    m.kp = malloc(sizeof(*m.kp) * total);
-    m.kl = malloc(sizeof(*m.kl) * total);
+    uint64_t kcap = 1u << 16, keys = 0;
+    if (hm_init(&m, kcap / 2)) return 0;
+    m.kp = malloc(sizeof(*m.kp) * kcap);
+    m.kl = malloc(sizeof(*m.kl) * kcap);
     uint32_t last = 0;
     uint64_t n = 0, bad = 0;
     memset(st, 0, sizeof(*st));
@@ -276,15 +306,30 @@ uint64_t orc_baseline(const orc_file *files, uint32_t nfiles, int verify_crc, or
             if (rem < klen) { st->status = ORC_EUNEXPECTED_EOF; goto out; }
             const uint8_t *key = d + p;
             p += klen;
+            if (bufio) { /* the record's bytes through the reader's buffer */
+                const uint64_t e = tomb ? p : (len - p < vs ? len : p + vs);
+                for (uint64_t q = p - klen - 16; q < e; q += sizeof buf) {
+                    const uint64_t k = e - q < sizeof buf ? e - q : sizeof buf;
+                    memcpy(buf, d + q, k);
+                    sink += buf[k - 1];
+                }
+            }
             if (tomb) {
-                hm_del(&m, key, klen);
+                keys -= (uint64_t)hm_del(&m, key, klen);
                 last += 16u + klen;
             } else {
                 if (len - p < vs) break;
                 p += vs;
+                if (n >= kcap) {
+                    kcap *= 2;
+                    m.kp = realloc(m.kp, sizeof(*m.kp) * kcap);
+                    m.kl = realloc(m.kl, sizeof(*m.kl) * kcap);
+                    if (!m.kp || !m.kl) { st->status = -1; goto out; }
+                }
                 m.kp[n] = key;
                 m.kl[n] = klen;
-                hm_set(&m, n);
+                keys += (uint64_t)hm_set(&m, n);
+                if (keys * 2 > m.mask + 1 && hm_grow(&m)) { st->status = -1; goto out; }
                 last += 16u + ks + vs;
             }
             if (verify_crc && orc_crc32_fast(d + p - vs, vs) != hcrc) bad++;
@@ -298,6 +343,7 @@ out:
     uint64_t live = 0;
     for (uint64_t i = 0; i <= m.mask; i++) live += m.slot[i] != 0;
     st->err_off = bad; /* baseline: number of CRC rejects (diagnostic) */
+    st->err_file = (uint32_t)sink; /* keeps the buffered copies live */
     free(m.kp);
     free(m.kl);
     hm_free(&m);

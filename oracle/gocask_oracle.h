@@ -76,11 +76,12 @@ int orc_replay(const orc_file *files, uint32_t nfiles, int verify_crc,
 uint64_t orc_keydir(const orc_file *files, const orc_rec *recs, uint64_t n,
                     uint64_t *live_out);
 
-/* Faithful timed CPU baseline: replay + CRC verdict + hash-map keydir, the way
- * the single-goroutine reference does it (one pass, map insert per record).
+/* Faithful timed CPU baseline: replay + hash-map keydir, the way the
+ * single-goroutine reference does it (one pass, map insert per record, the
+ * map grown by doubling).  flags: 1 = CRC verdict per record, 2 = every
+ * record byte through a 4 KiB buffer (the reference's bufio.Reader).
  * Returns number of live keys. */
-uint64_t orc_baseline(const orc_file *files, uint32_t nfiles, int verify_crc,
-                      orc_status *st);
+uint64_t orc_baseline(const orc_file *files, uint32_t nfiles, int flags, orc_status *st);
 
 /* ------------------------------------------------------------------------
  * Synthetic corpus spec (see DESIGN.md "Corpus").  Independent CPU

@@ -160,12 +160,15 @@ def keydir(files, recs, reset_after=None):
     return out
 
 
-def baseline(files, reset_after=None, verify_crc=True):
+def baseline(files, reset_after=None, verify_crc=True, bufio=True):
+    """Timed CPU baseline (orc_baseline): the replay loop with the keydir map
+    inline; bufio copies every record's bytes through a 4 KiB buffer as the
+    reference's bufio.Reader does; verify_crc adds the CRC verdict."""
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     st = OrcStatus()
-    live = lib().orc_baseline(fa, len(arrs), 1 if verify_crc else 0, ctypes.byref(st))
+    live = lib().orc_baseline(fa, len(arrs), (1 if verify_crc else 0) | (2 if bufio else 0), ctypes.byref(st))
     return live, dict(status=st.status, n_recs=st.n_recs, crc_rejects=st.err_off,
                       final_last_offset=st.final_last_offset)
 

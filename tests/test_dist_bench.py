@@ -62,3 +62,15 @@ def test_shards_are_disjoint_corpora(orc):
     f0, _ = orc.gen_corpus(**{**kw0, **small})
     f1, _ = orc.gen_corpus(**{**kw1, **small})
     assert bytes(f0[0][:4096]) != bytes(f1[0][:4096])
+
+
+def test_cpu_baseline_variants(orc):
+    """bench.py's cpu_baseline: SURVEY.md §8d's three variants on a tiny sample."""
+    import bench
+
+    out = bench.cpu_baseline("c3", 4 << 20, max_threads=2, min_s=0.05, mt_file_bytes=2 << 20)
+    assert out["kind"] == "port" and out["cores"] == 1 and out["value"] > 0
+    v = out["variants"]
+    assert set(v) == {"ref_faithful", "ref_crc", "all_cores"}
+    assert v["ref_crc"]["value"] == out["value"] and v["all_cores"]["cores"] == 2
+    assert all(x["value"] > 0 for x in v.values())
