@@ -28,9 +28,14 @@ KD_ENTRY_BYTES = 64
 def exchange(dist, send, send_splits, group=None):
     """All-to-all of a flat uint8 tensor laid out as consecutive per-rank parts
     of send_splits bytes.  Returns (received tensor, received split sizes), the
-    parts in rank order."""
+    parts in rank order, on send's device.  RCCL moves device tensors
+    directly; a gloo group (CPU tests, ranks sharing one GPU) is staged
+    through host memory."""
     import torch
 
+    if send.is_cuda and dist.get_backend(group) == "gloo":
+        recv, rs = exchange(dist, send.cpu(), send_splits, group)
+        return recv.to(send.device), rs
     ss = torch.tensor([int(x) for x in send_splits], dtype=torch.int64, device=send.device)
     rs = torch.empty_like(ss)
     dist.all_to_all_single(rs, ss, group=group)
@@ -49,6 +54,8 @@ def file_base(dist, n_files, group=None, device="cpu"):
     import torch
 
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
     t = torch.tensor([int(n_files)], dtype=torch.int64, device=device)
     all_n = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(all_n, t, group=group)

@@ -224,3 +224,74 @@ def test_merge_keydir_rccl_world1(g, orc):
         dist.destroy_process_group()
     assert base == 0 and n == len(ents)
     _check_merged(wf, [(ents, keys)], _global_keydir(wf, want), 1, [0] * len(wf))
+
+
+def _rank_worker(rank, world, port, q):
+    """One rank of a world-2 merge: its shard of the corpus on cuda:0, the
+    exchange over gloo (staged through host memory)."""
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    import oracle as orc
+    import gocask_amd as g
+    from gocask_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        files, names = orc.gen_corpus(**MERGE_CORPUS)
+        wf, reset = _walk(files, names)
+        a, b = SPLIT[rank], SPLIT[rank + 1]
+        with g.ReplayContext() as ctx:
+            ctx.load(wf[a:b], reset[a:b])
+            ctx.run()
+            base = shard.file_base(dist, b - a)
+            n, _ = shard.merge_keydir(ctx, dist, base)
+            ents, keys = ctx.kd_fetch_merged()
+        q.put((rank, base, n, ents.tobytes(), keys.tobytes()))
+    except Exception as e:  # reported to the parent
+        q.put((rank, None, repr(e), b"", b""))
+    finally:
+        dist.destroy_process_group()
+
+
+MERGE_CORPUS = dict(seed=76, val_fixed=0, key_min=8, key_max=24, key_universe=2000, tomb_permille=150,
+                    max_file_size=1 << 19, n_files=5)
+SPLIT = [0, 2, 5]  # rank 0: files 0-1, rank 1: files 2-4 (walk order)
+
+
+def test_merge_keydir_two_ranks(g, orc):
+    """gocask_amd.shard.merge_keydir as bench.py runs it at N>1, with two
+    processes (ranks) on one GPU and a gloo group: the owners' entries
+    together must be the global keydir of all files in walk order."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from gocask_amd._lib import KD_ENTRY_DTYPE
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r, base, n, _, _ in res:
+        assert base is not None, n
+    assert [r[1] for r in res] == [0, 2]  # file_base: the files of lower ranks
+    owners = [(np.frombuffer(e, dtype=KD_ENTRY_DTYPE), np.frombuffer(k, dtype=np.uint8)) for _, _, _, e, k in res]
+    assert [len(o[0]) for o in owners] == [r[2] for r in res]
+    files, names = orc.gen_corpus(**MERGE_CORPUS)
+    wf, reset = _walk(files, names)
+    want, _ = orc.replay(wf, reset)
+    _check_merged(wf, owners, _global_keydir(wf, want), 2, [0, 0, 1, 1, 1])
+    for p in procs:
+        assert p.exitcode == 0
