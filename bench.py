@@ -166,9 +166,10 @@ def keydir_merge(g, ctx, dist, n_files, reps=2):
         n_live, ph = shard.merge_keydir(ctx, dist, base)
         torch.cuda.synchronize()
         wall = time.perf_counter() - t0
-    v = torch.tensor([wall, ph["local"], ph["exchange"], ph["merge"]], dtype=torch.float64, device="cuda")
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    v = torch.tensor([wall, ph["local"], ph["exchange"], ph["merge"]], dtype=torch.float64, device=dev)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    c = torch.tensor([n_live, ph["sent_bytes"]], dtype=torch.float64, device="cuda")
+    c = torch.tensor([n_live, ph["sent_bytes"]], dtype=torch.float64, device=dev)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     w, lo, ex, mg = (round(x * 1e3, 3) for x in v.tolist())
     return dict(ms=w, local_ms=lo, exchange_ms=ex, merge_ms=mg, live_entries=int(c[0].item()),
@@ -224,19 +225,23 @@ def main():
     import torch
 
     dist = None
+    # one GPU per rank; GCK_DIST_BACKEND=gloo rehearses N>1 with ranks sharing
+    # fewer GPUs (device = local rank mod the GPUs present)
+    device = local_rank % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get("GCK_DIST_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(backend)
     elif torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
+        torch.cuda.set_device(device)
 
     import gocask_amd as g
 
     cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=local_rank, chunk_bytes=args.chunk_kib << 10)
+    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10)
     info = ctx.encode(**cfg)
     setup_s = time.perf_counter() - t_setup
 
@@ -255,7 +260,7 @@ def main():
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
     my_bytes = st["bytes"]
-    elapsed, total_bytes = reduce_over_ranks(dist, elapsed, my_bytes, "cuda")
+    elapsed, total_bytes = reduce_over_ranks(dist, elapsed, my_bytes, "cpu" if backend == "gloo" else "cuda")
     # per-phase device times (HIP events) of a few more, untimed steps: the
     # timed loop above does nothing but replays
     crc_ms, phases_sum, n_phase = [], {}, 3
