@@ -477,3 +477,39 @@ def test_config5_bitflips_reject_set(g):
     assert np.array_equal(rejected, flipped)
     tomb = (got["flags"] & 1) == 1
     assert np.array_equal(tomb, (spec.H(5, 3, ops) % np.uint64(1000)) < np.uint64(10))
+
+
+def test_keys_longer_than_speculation_bound(g, orc):
+    # keys of 64 KiB and more are never speculated (the prefilter needs
+    # KeySize <= 65535): chunks whose only headers carry such keys get a
+    # wrong or no entry and validation + fixup must recover the chain; also a
+    # tombstone whose "key" is that long and values past 64 KiB
+    rng = np.random.default_rng(11)
+
+    def rb(n):
+        return bytes(rng.integers(0, 256, n, dtype=np.uint8))
+
+    parts = []
+    for i in range(60):
+        r = i % 6
+        if r == 0:
+            parts.append(orc_mod.entry(i, b"big%02d" % i + rb(70000 + 997 * i), rb(int(rng.integers(0, 300)))))
+        elif r == 1:
+            parts.append(orc_mod.tombstone(i, b"tomb%02d" % i + rb(66000 + 13 * i)))
+        elif r == 2:
+            parts.append(orc_mod.entry(i, b"k%03d" % i, rb(200000 + 31 * i)))
+        else:
+            parts.append(orc_mod.entry(i, b"k%03d" % i, rb(int(rng.integers(1, 5000)))))
+    data = b"".join(parts)
+    want, wst = orc.replay([data], [False])
+    for chunk, mk in ((4096, 0), (1 << 16, 0), (1 << 16, 1024)):
+        got, gst = g.replay([data], [False], chunk_bytes=chunk, **({"max_key": mk} if mk else {}))
+        assert_same(got, gst, want, wst)
+    with g.ReplayContext(chunk_bytes=4096) as ctx:  # keydir and Get of the long keys
+        ctx.load([data], [False])
+        ctx.run()
+        live, _ = ctx.keydir()
+        keys = [bytes(data[int(r["rec_off"]) + 16:int(r["rec_off"]) + 16 + int(r["key_len"])]) for r in live]
+        st, vs, cc, vals = ctx.get_batch(keys)
+    assert len(live) == 50 and all(s == 0 for s in st)
+    assert max(len(k) for k in keys) > 65535
