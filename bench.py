@@ -213,6 +213,8 @@ def main():
     ap.add_argument("--keydir", action="store_true", help="also time the device keydir (gck_ctx_keydir)")
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: skip the keydir merge across ranks that follows the timed replays")
+    ap.add_argument("--fused", action="store_true",
+                    help="experimental GCK_OPT_FUSED path (boundary discovery inside the streaming CRC pass)")
     ap.add_argument("--merge", action="store_true",
                     help="N=1: time the keydir merge too (a one-rank RCCL group)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
@@ -241,7 +243,8 @@ def main():
 
     cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10)
+    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10,
+                          flags=g.core.OPT_FUSED if args.fused else 0)
     info = ctx.encode(**cfg)
     setup_s = time.perf_counter() - t_setup
 
@@ -321,7 +324,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_crc_rows",
+                "kernel": "k_fuse" if args.fused else "k_crc_rows",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -79,13 +79,16 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+OPT_FUSED = 1  # GCK_OPT_FUSED (include/gocask_hip.h): experimental fused boundary + CRC pass
+
+
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, flags=0):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = 0
+    o.flags = flags
     return o
 
 
@@ -265,11 +268,11 @@ def keydir(files, recs):
 class ReplayContext:
     """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
 
-    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, flags=0):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
         self._n_live = 0
-        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, flags)),
                                      ctypes.byref(self._h)))
 
     def load(self, files, reset_after=None):

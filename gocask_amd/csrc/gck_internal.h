@@ -89,6 +89,7 @@ struct Ctx {
     // rows
     uint64_t n_rows = 0;
     DBuf d_row_first, d_rend, d_plan, d_queue;
+    DBuf d_fep, d_redo, d_flist;  // GCK_OPT_FUSED: (c, pre) stage per chunk; chunks to stream again (flags, list)
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xfw, d_xa, d_xb, d_zrow, d_zl;

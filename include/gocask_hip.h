@@ -80,9 +80,14 @@ typedef struct gck_opts {
     uint32_t chunk_bytes;  /* boundary-speculation chunk (default 256 KiB, power of two)  */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
     uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
-    uint32_t flags;        /* reserved, 0                                                   */
+    uint32_t flags;        /* GCK_OPT_*                                                     */
 } gck_opts;
 
+
+/* Experimental: boundary discovery fused into the streaming CRC pass (one
+ * wavefront per chunk follows the header chain through the words it streams);
+ * results are identical, runs it cannot settle are redone on the standard path. */
+#define GCK_OPT_FUSED 1u
 
 typedef struct gck_result {
     gck_rec *recs;              /* library-owned pinned host array; free with gck_result_free */
