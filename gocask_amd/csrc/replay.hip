@@ -611,6 +611,10 @@ __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *_
 
 constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
 constexpr int kBlockRows = 64;   // rows per plan block = per k_crc_rows work item
+#ifndef GCK_CLAIM
+#define GCK_CLAIM 2
+#endif
+constexpr uint32_t kClaim = GCK_CLAIM;  // consecutive blocks per k_crc_rows queue claim
 constexpr int kPlanLaneBytes = 32;  // plan bytes per lane per block (64 rows x 4 bits)
 constexpr int kPlanRowBytes = kPlanLaneBytes * 64 / kBlockRows;  // = 32: plan bytes per row
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
@@ -769,10 +773,18 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         __builtin_amdgcn_raw_buffer_store_b64(v, ep_rsrc, (int)off, 0, 0);
     };
 
-    auto grab = [&]() -> uint32_t {  // next block index from the queue
-        uint32_t v = 0;
-        if (lane == 0) v = atomicAdd(queue, 1u);
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    // blocks are claimed kClaim at a time (consecutive): one queue atomic, and
+    // the pipeline drain its result forces, per kClaim blocks
+    uint32_t last = kClaim - 1;
+    auto grab = [&]() -> uint32_t {  // next block index
+        if (last % kClaim == kClaim - 1) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(queue, 1u);
+            last = kClaim * (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        } else {
+            ++last;
+        }
+        return last;
     };
     struct Plan {
         uint4 a, b;  // the lane's 64 row nibbles
