@@ -1007,6 +1007,14 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 // (a & m) | (b & ~m) with a scalar mask, opaque to the compiler: a select
 // tree written with ?: is folded back into an indexed load from a stack copy
 // (scratch), which also makes every later vmcnt wait drain the row prefetch.
+// x as a wave-uniform (SGPR) value: the chain state is uniform by
+// construction, but the compiler's divergence analysis loses that through the
+// parse loop and would keep it (and every branch on it) in VGPRs/exec masks.
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ uint32_t vsel(uint32_t m, uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
@@ -1191,17 +1199,38 @@ __global__ __launch_bounds__(1024) void k_fuse(const uint8_t *__restrict__ arena
                 r_h[q][0] = r_h[q][1] = 0u;
             }
             while (!done) {
+                p = uni64(p);
                 if (p >= ce) { done = true; break; }
                 const uint64_t rem = len - p;
                 if (rem < 16) { term = T_ERR; tpos = p; done = true; break; }  // ErrUnexpectedEOF
                 if (p + 16 > WE) break;                                         // the header continues in the next step
                 // KeySize / ValueSize: bytes p+8 .. p+15, in window dwords d8 .. d8+2
-                const int64_t d8 = ((int64_t)p + 8 - (int64_t)W0) >> 2;
-                const uint32_t sh = (uint32_t)(p & 3);
+                const int64_t d8 = (int64_t)uni64((uint64_t)(((int64_t)p + 8 - (int64_t)W0) >> 2));
+                const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p & 3));
                 uint32_t a2, a3, a4;
                 if (d8 >= 0 && (d8 >> 10) == ((d8 + 2) >> 10) && (d8 >> 10) < NR) {
                     // one row: words k .. k+2 of every slab, then the lane (the next one past word 15)
                     const uint32_t row = (uint32_t)(d8 >> 10), ln = (uint32_t)(d8 >> 4) & 63u, k = (uint32_t)d8 & 15u;
+#ifndef GCK_PICK_TREE
+                    // a uniform branch on (row, k): three readlanes from fixed
+                    // registers (no select tree)
+                    a2 = a3 = a4 = 0;
+#define GCK_H3(K)                                                                              \
+    case K:                                                                                    \
+        a2 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][K], (int)ln);                       \
+        a3 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][(K + 1) & 15], (int)(ln + ((K + 1) >> 4))); \
+        a4 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][(K + 2) & 15], (int)(ln + ((K + 2) >> 4))); \
+        break;
+#pragma unroll
+                    for (int i = 0; i < NR; ++i)
+                        if (row == (uint32_t)i) {
+                            switch (k) {
+                                GCK_H3(0) GCK_H3(1) GCK_H3(2) GCK_H3(3) GCK_H3(4) GCK_H3(5) GCK_H3(6) GCK_H3(7)
+                                GCK_H3(8) GCK_H3(9) GCK_H3(10) GCK_H3(11) GCK_H3(12) GCK_H3(13) GCK_H3(14) GCK_H3(15)
+                            }
+                        }
+#undef GCK_H3
+#else
                     uint32_t o0 = 0, o1 = 0, o2 = 0;
 #pragma unroll
                     for (int i = 0; i < NR; ++i)
@@ -1209,6 +1238,7 @@ __global__ __launch_bounds__(1024) void k_fuse(const uint8_t *__restrict__ arena
                     a2 = (uint32_t)__builtin_amdgcn_readlane((int)o0, (int)(ln + ((k + 0) >> 4)));
                     a3 = (uint32_t)__builtin_amdgcn_readlane((int)o1, (int)(ln + ((k + 1) >> 4)));
                     a4 = (uint32_t)__builtin_amdgcn_readlane((int)o2, (int)(ln + ((k + 2) >> 4)));
+#endif
                 } else {
                     // the carry (d < 0), the end of a row (lane 63, words 14-15)
                     // or the start of the next (lane 0, words 0-2): constant
