@@ -1244,9 +1244,10 @@ __global__ __launch_bounds__(1024) void k_fuse(const uint8_t *__restrict__ arena
                     // or the start of the next (lane 0, words 0-2): constant
                     // register indices, no select tree
                     auto edge = [&](int64_t d) -> uint32_t {
-                        if (d < 0) {
+                        if (d < 0) {  // readfirstlane: an asm result counts as divergent
                             const uint32_t j = (uint32_t)(d + 4), m1 = (j & 1u) ? ~0u : 0u, m2 = (j & 2u) ? ~0u : 0u;
-                            return vsel(m2, vsel(m1, carry[3], carry[2]), vsel(m1, carry[1], carry[0]));
+                            return (uint32_t)__builtin_amdgcn_readfirstlane(
+                                (int)vsel(m2, vsel(m1, carry[3], carry[2]), vsel(m1, carry[1], carry[0])));
                         }
                         const uint32_t row = (uint32_t)(d >> 10), wd = (uint32_t)d & 1023u;
                         uint32_t v = 0;
