@@ -460,3 +460,42 @@ def zipf_table():
 
 def device_count():
     return _lib.load().gck_device_count()
+
+
+def encode_batch(ops, device="cuda"):
+    """Bulk serializeEntry on the device (row f4, `gck_encode_batch`).
+
+    ops: iterable of (ts, key, value) -- value None means a Delete of key.
+    Returns the serialized bytes as a uint8 torch tensor on `device`, and the
+    record offsets (n+1, int64 tensor), exactly as DB.Put / DB.Delete append
+    them (core/db.go:185-212, :245-247, serializeEntry :272-284)."""
+    import torch
+
+    ops = list(ops)
+    n = len(ops)
+    keys = b"".join(k for _, k, _ in ops)
+    vals = b"".join(v for _, _, v in ops if v is not None)
+    koff = np.zeros(n + 1, dtype=np.uint64)
+    voff = np.zeros(n + 1, dtype=np.uint64)
+    koff[1:] = np.cumsum([len(k) for _, k, _ in ops], dtype=np.uint64) if n else koff[1:]
+    voff[1:] = np.cumsum([0 if v is None else len(v) for _, _, v in ops], dtype=np.uint64) if n else voff[1:]
+    ts = np.array([t & 0xFFFFFFFF for t, _, _ in ops], dtype=np.uint32)
+    tomb = np.array([v is None for _, _, v in ops], dtype=np.uint8)
+
+    def dev(a, dtype):
+        return torch.from_numpy(np.array(a, copy=True).view(dtype)).to(device)
+
+    d_keys = dev(np.frombuffer(keys or b"\0", dtype=np.uint8), np.uint8)
+    d_vals = dev(np.frombuffer(vals or b"\0", dtype=np.uint8), np.uint8)
+    d_koff, d_voff = dev(koff, np.int64), dev(voff, np.int64)
+    d_ts, d_tomb = dev(ts, np.int32), dev(tomb, np.uint8)
+    need = int(16 * n + len(keys) + sum(len(v) for _, _, v in ops if v is not None))
+    out = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+    out_off = torch.empty(n + 1, dtype=torch.int64, device=device)
+    total = ctypes.c_uint64(0)
+    stream = torch.cuda.current_stream(out.device).cuda_stream
+    _lib.check(_lib.load().gck_encode_batch(d_keys.data_ptr(), d_koff.data_ptr(), d_vals.data_ptr(),
+                                            d_voff.data_ptr(), d_ts.data_ptr(), d_tomb.data_ptr(), n,
+                                            out.data_ptr(), out.numel(), out_off.data_ptr(),
+                                            ctypes.byref(total), stream))
+    return out[: total.value], out_off

@@ -215,3 +215,91 @@ int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------ bulk serializeEntry (f4) ---
+// gck_encode_batch: caller records (already in HBM) -> GoCask bytes, back to
+// back, as DB.Put / DB.Delete write them (core/db.go:185-212, :245-247,
+// serializeEntry :272-284).  One wavefront per record: the lanes copy key and
+// value with strided byte stores and CRC the payload in 64 contiguous
+// segments, combined through Z_n (gck_math.h):
+//   F(0, V) = XOR_l Z_{|V| - end_l}(F(0, seg_l)),  crc = ~(F(0,V) ^ Z_|V|(~0)).
+namespace gck {
+
+__global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict__ keys,
+                                                      const uint64_t *__restrict__ key_off,
+                                                      const uint8_t *__restrict__ vals,
+                                                      const uint64_t *__restrict__ val_off,
+                                                      const uint32_t *__restrict__ ts,
+                                                      const uint8_t *__restrict__ tomb, uint64_t n,
+                                                      const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out) {
+    __shared__ uint32_t T[256];
+    for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
+        uint32_t c = v;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+        T[v] = c;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = wave; i < n; i += n_waves) {
+        const bool del = tomb[i] != 0;
+        const uint8_t *key = keys + key_off[i];
+        const uint64_t kl = key_off[i + 1] - key_off[i];
+        const uint8_t *val = vals + val_off[i];
+        const uint64_t vl = del ? 0 : val_off[i + 1] - val_off[i];
+        uint8_t *dst = out + out_off[i];
+        for (uint64_t j = lane; j < kl; j += 64) dst[16 + j] = key[j];
+        for (uint64_t j = lane; j < vl; j += 64) dst[16 + kl + j] = val[j];
+        // the CRC payload: the value (Put) or the key (Delete)
+        const uint8_t *pl = del ? key : val;
+        const uint64_t len = del ? kl : vl;
+        const uint64_t seg = (len + 63) / 64, b = min(len, lane * seg), e = min(len, b + seg);
+        uint32_t c = 0;
+        for (uint64_t j = b; j < e; ++j) c = T[(c ^ pl[j]) & 0xff] ^ (c >> 8);
+        uint32_t f = c ? multmodp(xpow8n(len - e), c) : 0u;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) f ^= (uint32_t)__shfl_xor((int)f, m, 64);
+        const uint32_t crc = ~(f ^ multmodp(xpow8n(len), 0xFFFFFFFFu));
+        const uint32_t hv[4] = {crc, ts[i], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
+        if (lane < 16) dst[lane] = (uint8_t)(hv[lane / 4] >> (8 * (lane % 4)));
+    }
+}
+
+}  // namespace gck
+
+extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint8_t *vals,
+                                const uint64_t *val_off, const uint32_t *ts, const uint8_t *tomb, uint64_t n,
+                                uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *total,
+                                void *stream) {
+    if (!key_off || !val_off || !out_off || !total || (n && (!keys || !out || !ts || !tomb))) return GCK_EINVAL;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GCK_EDEVICE;
+    hipStream_t s = (hipStream_t)stream;
+    // record offsets: a sequential sum over the sizes (17 B per record crosses
+    // PCIe twice; the bytes themselves never leave the device)
+    std::vector<uint64_t> ko(n + 1), vo(n + 1), off(n + 1);
+    std::vector<uint8_t> tb(n);
+    GCK_HIP(hipMemcpyAsync(ko.data(), key_off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(vo.data(), val_off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (n) GCK_HIP(hipMemcpyAsync(tb.data(), tomb, n, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    off[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (ko[i + 1] < ko[i] || vo[i + 1] < vo[i]) return GCK_EINVAL;
+        const uint64_t kl = ko[i + 1] - ko[i], vl = tb[i] ? 0 : vo[i + 1] - vo[i];
+        if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) return GCK_EINVAL;  // u32 header fields
+        off[i + 1] = off[i] + 16 + kl + vl;
+    }
+    *total = off[n];
+    if (*total > out_cap) return GCK_EINVAL;  // *total says how much is needed
+    GCK_HIP(hipMemcpyAsync(out_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    if (n) {
+        const uint64_t waves = std::min<uint64_t>(n, 256ull * 64);
+        k_encode_batch<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n,
+                                                                   out_off, out);
+        GCK_HIP(hipGetLastError());
+    }
+    GCK_HIP(hipStreamSynchronize(s));
+    return GCK_OK;
+}

@@ -249,6 +249,21 @@ int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n);
 /* The encoder's Zipf threshold table (65472 u32), for cross-checks. */
 void gck_encode_zipf_table(uint32_t *thr);
 
+/* Bulk serializeEntry (row f4; replaces the per-record encode of DB.Put /
+ * DB.Delete, core/db.go:185-212 and :245-247, serializeEntry :272-284, header
+ * encode core/header.go:38-48, for bulk loads and compaction).  Record i is a
+ * Put of key i / value i, or, when tomb[i] != 0, a Delete of key i
+ * (header{CRC32(key), ts, 0, len(key)} || key), written back to back into out
+ * in order.  keys/vals are concatenated bytes with n+1 offsets
+ * (key_off/val_off); every pointer except total is DEVICE memory; out_off
+ * (n+1) receives each record's offset in out; *total = bytes written (or
+ * needed: GCK_EINVAL with nothing written when out_cap < *total).  stream:
+ * a hipStream_t, NULL for the default stream; returns after the bytes are
+ * written. */
+int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint8_t *vals,
+                     const uint64_t *val_off, const uint32_t *ts, const uint8_t *tomb, uint64_t n,
+                     uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *total, void *stream);
+
 /* ---- host-side DB mirror (core.NewDB / gocask.Open / Get / Keys) ------------ */
 typedef struct gck_db gck_db;
 
