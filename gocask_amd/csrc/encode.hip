@@ -242,27 +242,116 @@ __global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict_
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t i = wave; i < n; i += n_waves) {
+    // records in groups of 64 per wavefront: payloads up to kLaneMax bytes are
+    // encoded by one lane each (a serial CRC, no GF(2) combine), larger ones by
+    // the whole wavefront, one after another
+    constexpr uint64_t kLaneMax = 2048;
+    for (uint64_t g = wave * 64; g < n; g += n_waves * 64) {
+        const uint64_t li = g + lane;
+        bool big = false;
+        if (li < n) {
+            const bool del = tomb[li] != 0;
+            const uint8_t *key = keys + key_off[li];
+            const uint64_t kl = key_off[li + 1] - key_off[li];
+            const uint8_t *val = vals + val_off[li];
+            const uint64_t vl = del ? 0 : val_off[li + 1] - val_off[li];
+            big = (del ? kl : vl) > kLaneMax;
+            if (!big) {
+                uint8_t *dst = out + out_off[li];
+                uint32_t c = 0xFFFFFFFFu;
+                // bytes of src to d, eight aligned dwords in flight; CRC'd when crc
+                auto put = [&](const uint8_t *src, uint8_t *d, uint64_t len, bool crc) {
+                    auto one = [&](uint64_t j, uint8_t x) {
+                        d[j] = x;
+                        if (crc) c = T[(c ^ x) & 0xff] ^ (c >> 8);
+                    };
+                    uint64_t j = 0;
+                    const uint64_t al = min(len, (uint64_t)((4u - ((uintptr_t)src & 3u)) & 3u));
+                    for (; j < al; ++j) one(j, src[j]);
+                    const uint32_t *pw = reinterpret_cast<const uint32_t *>(src + j);
+                    const uint64_t nw = (len - j) / 4;
+                    uint64_t q = 0;
+                    for (; q + 8 <= nw; q += 8) {
+                        uint32_t v[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(pw + q + k);
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) one(j + 4 * (q + k) + b, (uint8_t)(v[k] >> (8 * b)));
+                    }
+                    for (; q < nw; ++q) {
+                        const uint32_t w = pw[q];
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) one(j + 4 * q + b, (uint8_t)(w >> (8 * b)));
+                    }
+                    for (j += 4 * nw; j < len; ++j) one(j, src[j]);
+                };
+                put(key, dst + 16, kl, del);
+                put(val, dst + 16 + kl, vl, !del);
+                const uint32_t hv[4] = {~c, ts[li], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
+#pragma unroll
+                for (int k = 0; k < 16; ++k) dst[k] = (uint8_t)(hv[k / 4] >> (8 * (k % 4)));
+            }
+        }
+        uint64_t bigs = __ballot(big);
+        while (bigs) {
+        const uint64_t i = g + (uint64_t)__builtin_ctzll(bigs);
+        bigs &= bigs - 1;
         const bool del = tomb[i] != 0;
         const uint8_t *key = keys + key_off[i];
         const uint64_t kl = key_off[i + 1] - key_off[i];
         const uint8_t *val = vals + val_off[i];
         const uint64_t vl = del ? 0 : val_off[i + 1] - val_off[i];
         uint8_t *dst = out + out_off[i];
-        for (uint64_t j = lane; j < kl; j += 64) dst[16 + j] = key[j];
-        for (uint64_t j = lane; j < vl; j += 64) dst[16 + kl + j] = val[j];
+        // coalesced byte copies, eight loads in flight per lane before the stores
+        auto copy = [&](const uint8_t *src, uint8_t *d, uint64_t len) {
+            uint64_t j = lane;
+            for (; j + 7 * 64 < len; j += 8 * 64) {
+                uint8_t v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(src + j + 64 * k);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) d[j + 64 * k] = v[k];
+            }
+            for (; j < len; j += 64) d[j] = src[j];
+        };
+        copy(key, dst + 16, kl);
+        copy(val, dst + 16 + kl, vl);
         // the CRC payload: the value (Put) or the key (Delete)
         const uint8_t *pl = del ? key : val;
         const uint64_t len = del ? kl : vl;
         const uint64_t seg = (len + 63) / 64, b = min(len, lane * seg), e = min(len, b + seg);
+        // the lane's segment: head bytes up to a 4 B boundary, aligned dwords
+        // eight at a time (independent loads in flight), tail bytes
         uint32_t c = 0;
-        for (uint64_t j = b; j < e; ++j) c = T[(c ^ pl[j]) & 0xff] ^ (c >> 8);
+        auto byte = [&](uint8_t x) { c = T[(c ^ x) & 0xff] ^ (c >> 8); };
+        auto word = [&](uint32_t w) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) byte((uint8_t)(w >> (8 * k)));
+        };
+        uint64_t j = b;
+        const uint64_t al = min(e, b + ((4u - ((uintptr_t)(pl + b) & 3u)) & 3u));
+        for (; j < al; ++j) byte(pl[j]);
+        const uint32_t *pw = reinterpret_cast<const uint32_t *>(pl + j);
+        const uint64_t nw = (e - j) / 4;
+        uint64_t q = 0;
+        for (; q + 8 <= nw; q += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(pw + q + k);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) word(v[k]);
+        }
+        for (; q < nw; ++q) word(pw[q]);
+        for (j += 4 * nw; j < e; ++j) byte(pl[j]);
         uint32_t f = c ? multmodp(xpow8n(len - e), c) : 0u;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) f ^= (uint32_t)__shfl_xor((int)f, m, 64);
         const uint32_t crc = ~(f ^ multmodp(xpow8n(len), 0xFFFFFFFFu));
         const uint32_t hv[4] = {crc, ts[i], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
         if (lane < 16) dst[lane] = (uint8_t)(hv[lane / 4] >> (8 * (lane % 4)));
+        }
     }
 }
 
@@ -295,7 +384,7 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
     if (*total > out_cap) return GCK_EINVAL;  // *total says how much is needed
     GCK_HIP(hipMemcpyAsync(out_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (n) {
-        const uint64_t waves = std::min<uint64_t>(n, 256ull * 64);
+        const uint64_t waves = std::min<uint64_t>((n + 63) / 64, 256ull * 64);
         k_encode_batch<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n,
                                                                    out_off, out);
         GCK_HIP(hipGetLastError());

@@ -45,7 +45,8 @@ def test_encode_batch_empty_and_zero_length():
 
     out, off = core.encode_batch([])
     assert out.numel() == 0 and off.cpu().numpy().tolist() == [0]
-    ops = [(5, b"k", b""), (6, b"", b"v"), (7, b"gone", None), (2**32 + 9, b"x" * 64, b"y" * 4096)]
+    ops = [(5, b"k", b""), (6, b"", b"v"), (7, b"gone", None), (2**32 + 9, b"x" * 64, b"y" * 4096),
+           (8, bytes(range(256)) * 20, None), (9, b"q" * 3000, bytes(range(7)) * 300), (10, b"", b"")]
     out, _ = core.encode_batch(ops)
     assert bytes(out.cpu().numpy()) == _expected(ops)
 
