@@ -238,7 +238,20 @@ __global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict_
         for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
         T[v] = c;
     }
+    __shared__ uint32_t X8[64];  // x^(8 * 2^k) mod P: powers by set bits, no squarings
+    if (threadIdx.x == 0) {
+        uint32_t x = kX0 >> 8;
+        for (int k = 0; k < 64; ++k) {
+            X8[k] = x;
+            x = multmodp(x, x);
+        }
+    }
     __syncthreads();
+    auto zpow = [&](uint64_t m) {  // x^(8m) mod P
+        uint32_t r = kX0;
+        for (; m; m &= m - 1) r = multmodp(X8[__builtin_ctzll(m)], r);
+        return r;
+    };
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -345,10 +358,10 @@ __global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict_
         }
         for (; q < nw; ++q) word(pw[q]);
         for (j += 4 * nw; j < e; ++j) byte(pl[j]);
-        uint32_t f = c ? multmodp(xpow8n(len - e), c) : 0u;
+        uint32_t f = c ? multmodp(zpow(len - e), c) : 0u;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) f ^= (uint32_t)__shfl_xor((int)f, m, 64);
-        const uint32_t crc = ~(f ^ multmodp(xpow8n(len), 0xFFFFFFFFu));
+        const uint32_t crc = ~(f ^ multmodp(zpow(len), 0xFFFFFFFFu));
         const uint32_t hv[4] = {crc, ts[i], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
         if (lane < 16) dst[lane] = (uint8_t)(hv[lane / 4] >> (8 * (lane % 4)));
         }
