@@ -255,10 +255,13 @@ __global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict_
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    // records in groups of 64 per wavefront: payloads up to kLaneMax bytes are
+    // records in groups of 64 per wavefront: payloads up to kLaneMax bytes (1 KiB: A/B of 512..4096, tools/xp_lane_max.sh) are
     // encoded by one lane each (a serial CRC, no GF(2) combine), larger ones by
     // the whole wavefront, one after another
-    constexpr uint64_t kLaneMax = 2048;
+#ifndef GCK_LANE_MAX
+#define GCK_LANE_MAX 1024
+#endif
+    constexpr uint64_t kLaneMax = GCK_LANE_MAX;
     for (uint64_t g = wave * 64; g < n; g += n_waves * 64) {
         const uint64_t li = g + lane;
         bool big = false;
