@@ -1774,6 +1774,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if (o) {
         d.device = o->device;
         if (o->chunk_bytes) d.chunk_bytes = o->chunk_bytes;
+        else if (o->flags & GCK_OPT_FUSED) d.chunk_bytes = 256 << 10;  // shorter serial re-streams (§10d)
         if (o->max_key) d.max_key = o->max_key;
         if (o->chunk_cap) d.chunk_cap = o->chunk_cap;
         d.flags = o->flags;

@@ -77,7 +77,7 @@ typedef struct gck_rec {
 
 typedef struct gck_opts {
     int32_t device;        /* HIP device ordinal (default 0)                               */
-    uint32_t chunk_bytes;  /* boundary-speculation chunk (default 256 KiB, power of two)  */
+    uint32_t chunk_bytes;  /* boundary-speculation chunk (0: 512 KiB, 256 KiB fused; pow2) */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
     uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
     uint32_t flags;        /* GCK_OPT_*                                                     */
