@@ -297,9 +297,10 @@ def main():
         launches = 1
         achieved = my_bytes / (crc_avg * 1e-3) / 1e9
         traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}{'_fused' if args.fused else ''}.json")
         if os.path.exists(tf):
-            traffic = json.load(open(tf)).get("crc_rows_hbm_bytes_per_launch")
+            t = json.load(open(tf))
+            traffic = t.get("fuse_hbm_bytes_per_launch" if args.fused else "crc_rows_hbm_bytes_per_launch")
         out = {
             "metric": "device-resident data-file GiB/s CRC-verified+header-decoded, 1 GPU (+2/4/8)",
             "value": round(value, 2),
