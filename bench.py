@@ -213,8 +213,7 @@ def main():
     ap.add_argument("--keydir", action="store_true", help="also time the device keydir (gck_ctx_keydir)")
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: skip the keydir merge across ranks that follows the timed replays")
-    ap.add_argument("--fused", action="store_true",
-                    help="experimental GCK_OPT_FUSED path (boundary discovery inside the streaming CRC pass)")
+    ap.add_argument("--spec-kib", type=int, default=0, help="speculation window per chunk (KiB, 0: default)")
     ap.add_argument("--merge", action="store_true",
                     help="N=1: time the keydir merge too (a one-rank RCCL group)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
@@ -243,8 +242,7 @@ def main():
 
     cfg = shard_config(args.config, rank)
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10,
-                          flags=g.core.OPT_FUSED if args.fused else 0)
+    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10, spec_window=args.spec_kib << 10)
     info = ctx.encode(**cfg)
     setup_s = time.perf_counter() - t_setup
 
@@ -297,10 +295,9 @@ def main():
         launches = 1
         achieved = my_bytes / (crc_avg * 1e-3) / 1e9
         traffic = None
-        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}{'_fused' if args.fused else ''}.json")
+        tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
         if os.path.exists(tf):
-            t = json.load(open(tf))
-            traffic = t.get("fuse_hbm_bytes_per_launch" if args.fused else "crc_rows_hbm_bytes_per_launch")
+            traffic = json.load(open(tf)).get("crc_rows_hbm_bytes_per_launch")
         out = {
             "metric": "device-resident data-file GiB/s CRC-verified+header-decoded, 1 GPU (+2/4/8)",
             "value": round(value, 2),
@@ -325,7 +322,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_fuse" if args.fused else "k_crc_rows",
+                "kernel": "k_crc_rows",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

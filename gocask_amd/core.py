@@ -79,16 +79,14 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-OPT_FUSED = 1  # GCK_OPT_FUSED (include/gocask_hip.h): experimental fused boundary + CRC pass
-
-
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, flags=0):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = flags
+    o.flags = 0
+    o.spec_window = spec_window
     return o
 
 
@@ -235,14 +233,14 @@ def host_unregister(arr):
     check(_lib.load().gck_host_unregister(arr.ctypes.data))
 
 
-def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0):
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap)),
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window)),
                       ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
@@ -268,11 +266,11 @@ def keydir(files, recs):
 class ReplayContext:
     """Device-resident replay (gck_ctx_*): load or encode once, run many times."""
 
-    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, flags=0):
+    def __init__(self, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
         self._L = _lib.load()
         self._h = ctypes.c_void_p()
         self._n_live = 0
-        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, flags)),
+        check(self._L.gck_ctx_create(ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window)),
                                      ctypes.byref(self._h)))
 
     def load(self, files, reset_after=None):

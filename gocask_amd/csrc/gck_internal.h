@@ -78,6 +78,8 @@ struct Ctx {
     uint32_t n_chunks = 0;
     DBuf d_fbase, d_flen, d_ffirst, d_fnch, d_fbad, d_fterm, d_ftpos, d_fnrec, d_ffirstrec, d_carry;
     DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
+    DBuf d_ch_wend;              // where each chunk's walk stopped (its bound, walk_bound)
+    uint32_t chunk_shift = 17;   // log2(opts.chunk_bytes)
     DBuf d_rec_base, d_bsum, d_scratch_off, d_scratch_hdr, d_counters;
     DBuf d_freset;                   // per file: 1 = lastOffset resets after it
     DBuf d_gbase;                    // record range of the run [0, n)
@@ -89,7 +91,6 @@ struct Ctx {
     // rows
     uint64_t n_rows = 0;
     DBuf d_row_first, d_rend, d_plan, d_queue;
-    DBuf d_fep, d_redo, d_flist;  // GCK_OPT_FUSED: (c, pre) stage per chunk; chunks to stream again (flags, list)
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xfw, d_xa, d_xb, d_zrow, d_zl;

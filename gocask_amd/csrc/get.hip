@@ -187,7 +187,9 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
                 if (!same) continue;
                 const gck_rec r = recs[cur];
                 if (!(r.flags & GCK_F_TOMBSTONE)) {
-                    if ((uint64_t)r.value_pos + r.value_size > flen[r.file]) {
+                    // os.File.ReadAt into an empty buffer returns (0, nil) at any
+                    // offset, so an empty value is never a short read
+                    if (r.value_size && (uint64_t)r.value_pos + r.value_size > flen[r.file]) {
                         st = GCK_EIO;  // Disk.ReadFileAt short read
                     } else {
                         st = GCK_OK;   // pending the CRC
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
                                                      uint32_t *__restrict__ expect) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const gck_rec r = live[i];
-        const bool ok = (uint64_t)r.value_pos + r.value_size <= flen[r.file];
+        const bool ok = !r.value_size || (uint64_t)r.value_pos + r.value_size <= flen[r.file];  // see k_get_lookup
         status[i] = ok ? GCK_OK : GCK_EIO;
         item[i] = ok ? fbase[r.file] + r.value_pos : 0;
         vsize[i] = ok ? r.value_size : 0;

@@ -73,6 +73,21 @@ __device__ __forceinline__ Hdr ld_hdr(const uint8_t *__restrict__ arena, uint64_
     return h;
 }
 
+// The same 16 bytes with two loads (16 B + 4 B, dword aligned) instead of five.
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ Hdr ld_hdr2(const uint8_t *__restrict__ arena, uint64_t o) {
+    const uint8_t *p = arena + (o & ~3ull);
+    const u32x4_a4 v = *reinterpret_cast<const u32x4_a4 *>(p);
+    const uint32_t w4 = *reinterpret_cast<const uint32_t *>(p + 16);
+    const uint32_t sh = (uint32_t)o & 3u;
+    Hdr h;
+    h.crc = ab(v.y, v.x, sh);
+    h.ts = ab(v.z, v.y, sh);
+    h.ks = ab(v.w, v.z, sh);
+    h.vs = ab(w4, v.w, sh);
+    return h;
+}
+
 // Follow the header chain from q for kHops+1 headers: key length in
 // [1, max_key] and every record inside the file.  A chain may only end exactly
 // at the file end.  (A record straddling the file end is rejected: that only
@@ -95,10 +110,11 @@ __device__ bool chain_ok(const uint8_t *__restrict__ arena, uint64_t base, uint6
 // The reference's readEntry loop (core/db.go:131-178) over one chunk: decode
 // headers from p while p < ce.  EOF classes follow Go's io.ReadFull /
 // bufio.Reader.Discard semantics.  emit(i, p, hdr) per record.
-template <class Emit>
+template <class Emit, bool H2 = false>
 __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uint64_t len, uint64_t ce,
                            uint64_t p, Emit emit, uint32_t &count, uint64_t &exit, uint32_t &term,
                            uint64_t &tpos) {
+    auto ld = [&](uint64_t o) { return H2 ? ld_hdr2(arena, o) : ld_hdr(arena, o); };
     uint32_t n = 0;
     term = T_NONE;
     tpos = 0;
@@ -108,7 +124,7 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
     // base / len are consumed here, before the loop, so no load issued
     // outside the loop is still pending inside it.
     const uint64_t a0 = base + (p < len ? p : 0);
-    Hdr h = ld_hdr(arena, a0);
+    Hdr h = ld(a0);
     emit.prime();  // the loop is entered with the back edge's queue shape
     while (p < ce) {
         const uint64_t rem = len - p;
@@ -126,7 +142,7 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
         }
         // the next header (the arena is padded: a read at the file end or
         // just past the chunk stays in bounds and is never used)
-        const Hdr hn = ld_hdr(arena, base + (next < len ? next : 0));
+        const Hdr hn = ld(base + (next < len ? next : 0));
         emit(n, p, h);
         ++n;
         p = next;
@@ -142,9 +158,15 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {
     return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
 }
 
-// One wavefront per chunk finds the first byte position >= chunk start whose
-// header and the next kHops headers are plausible (chunk 0 of a file starts at
-// 0).  Each pass covers 4 KiB of positions, 64 per lane.  Prefilter: a header
+// One wavefront per chunk finds the first byte position p in [chunk start,
+// chunk start + window) whose header and the next kHops headers are plausible
+// (chunk 0 of a file starts at 0); none (kNone) when no position in the window
+// qualifies: the walk of the chunk before then covers this chunk too.  Chunk
+// starts inside long values (most of the corpus bytes sit in values > 4 KiB)
+// would otherwise stream the rest of the value; a bounded window keeps the
+// search cost per chunk fixed, so chunks can be small (short walk chains)
+// where records are dense, and merge where they are sparse (few hops).  Each
+// pass covers 4 KiB of positions, 64 per lane.  Prefilter: a header
 // at p with KeySize <= 65535 (tombstones: KeySize 0) has bytes p+10 and p+11
 // zero, so the lane flags positions whose bytes 10, 11 are a zero pair (about
 // 2 VALU per position; in value bytes a zero pair is rare) and only flagged
@@ -159,7 +181,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                                                     const uint64_t *__restrict__ ch_start,
                                                     const uint64_t *__restrict__ ch_end,
                                                     uint64_t *__restrict__ ch_entry, uint32_t n_chunks,
-                                                    uint32_t max_key) {
+                                                    uint32_t max_key, uint64_t window) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
     if (c >= n_chunks) return;
@@ -204,8 +226,12 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
             }
             return cm;
         };
+        // positions searched: [cs, lim).  The windows are loaded up to two
+        // ahead unconditionally (the arena is padded past every file; a
+        // branch around a load would cost the prefetch its place).
+        const uint64_t lim = ce - cs > window ? cs + window : ce;
         uint64_t from = cs;
-        while (found == kNone && from < ce) {
+        while (found == kNone && from < lim) {
             uint64_t wb = kNone, cm = 0;
             {
                 u32x4 A[5], B[5], C[5];
@@ -215,15 +241,15 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                     load(b0 + 2 * 4096, C);
                     cm = cands(A);
                     if (__ballot(cm != 0)) { wb = b0; break; }
-                    if (b0 + 4096 >= ce) break;
+                    if (b0 + 4096 >= lim) break;
                     load(b0 + 3 * 4096, A);
                     cm = cands(B);
                     if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
-                    if (b0 + 2 * 4096 >= ce) break;
+                    if (b0 + 2 * 4096 >= lim) break;
                     load(b0 + 4 * 4096, B);
                     cm = cands(C);
                     if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
-                    if (b0 + 3 * 4096 >= ce) break;
+                    if (b0 + 3 * 4096 >= lim) break;
                 }
             }
             if (wb == kNone) break;
@@ -245,79 +271,131 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
             }
             from = wb + 4096;
         }
-        // shadows: a true header is preceded by plausible ones 1..3 bytes
-        // earlier (a tombstone's 2-byte shadow has KeySize = the timestamp's
-        // high half and can re-sync onto the true chain after one hop), so
-        // the latest chaining position within 3 bytes wins
+        // shadows: next to a true header at p, positions p-2, p-1 (KeySize =
+        // the timestamp's high bytes plus KeySize << 8) and p+3 (KeySize =
+        // ValueSize << 8) often decode as plausible headers too, and one long
+        // first hop can land such a shadow on the true chain, which then
+        // chains.  A shadow's fields are the true ones shifted by whole
+        // bytes, so its first hop is >= 256 times the true record's: of the
+        // chaining positions within 3 bytes of the first one, the one with
+        // the shortest first record wins (ties: the earliest).  (Preferring
+        // the latest mis-speculated ~5 chunks of C3's 65 K, the earliest ~15.)
         if (found != kNone) {
+            const Hdr h0 = ld_hdr(arena, base + found);
+            uint64_t best = 16ull + h0.ks + h0.vs, pick = found;
 #pragma unroll 1
-            for (uint32_t k = 3; k >= 1; --k)
-                if (found + k < ce && chain_ok(arena, base, len, found + k, mk)) {
-                    found += k;
-                    break;
+            for (uint32_t k = 1; k <= 3; ++k) {
+                if (found + k >= ce) break;
+                const Hdr hk = ld_hdr(arena, base + found + k);
+                const uint64_t hop = 16ull + hk.ks + hk.vs;
+                if (hop < best && chain_ok(arena, base, len, found + k, mk)) {
+                    best = hop;
+                    pick = found + k;
                 }
+            }
+            found = pick;
         }
     }
     if (lane == 0) ch_entry[c] = found;
 }
 
-// The stage of a chunk: cap slots + 1 scratch slot (records past cap land
-// there; k_compact re-walks such chunks).  Every hop stores, so the number of
-// stores per hop is fixed and the next header's load wait counts them.
+// The stage: per chunk, cap record slots + 1 scratch slot (records past cap
+// land there; k_compact re-walks such chunks), interleaved over groups of
+// kStageIl consecutive chunks: slot i of chunk c is element
+// ((c / kStageIl) * (cap + 1) + i) * kStageIl + c % kStageIl.  The lanes of a
+// k_walk wavefront walk consecutive chunks hop by hop, so a hop's stage store
+// writes 64 / kStageIl runs of kStageIl consecutive elements (whole lines)
+// instead of 64 scattered partial lines (measured: those cost half of the
+// walk), and k_compact still reads a chunk's slots at a short stride.
+#ifndef GCK_STAGE_IL
+#define GCK_STAGE_IL 8
+#endif
+constexpr uint32_t kStageIl = GCK_STAGE_IL;
+__host__ __device__ __forceinline__ uint64_t stage_slot(uint32_t c, uint32_t i, uint32_t cap) {
+    return ((uint64_t)(c / kStageIl) * (cap + 1) + (i < cap ? i : cap)) * kStageIl + (c % kStageIl);
+}
+// Every hop stores, so the number of stores per hop is fixed and the next
+// header's load wait counts them.
 struct ScratchEmit {
-    uint64_t *off;
+    uint64_t *off;  // the chunk's slot 0 (stride kStageIl elements)
     uint4 *hdr;
     uint32_t cap;
     __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
-        const uint32_t k = i < cap ? i : cap;
+        const uint64_t k = (uint64_t)(i < cap ? i : cap) * kStageIl;
         off[k] = p;
         hdr[k] = make_uint4(h.crc, h.ts, h.ks, h.vs);
     }
     // the stores of one hop, to the scratch slot
     __device__ void prime() const {
-        off[cap] = 0;
-        hdr[cap] = make_uint4(0, 0, 0, 0);
+        off[(uint64_t)cap * kStageIl] = 0;
+        hdr[(uint64_t)cap * kStageIl] = make_uint4(0, 0, 0, 0);
     }
 };
+
+// Where the walk of chunk c stops: the start of the next chunk of its file
+// that has an entry (its records are that chunk's), else the file end.  A
+// chunk without an entry is covered by the walk of the nearest earlier chunk
+// that has one.  Chunk starts are (index within the file) << chunk_shift.
+__device__ uint64_t walk_bound(const uint64_t *__restrict__ ch_entry, const uint32_t *__restrict__ f_first_chunk,
+                               const uint32_t *__restrict__ f_nchunks, const uint64_t *__restrict__ flen, uint32_t c,
+                               uint32_t f, uint32_t chunk_shift) {
+    const uint32_t fc = f_first_chunk[f], fe = fc + f_nchunks[f];
+    for (uint32_t d = c + 1; d < fe; d += 4) {
+        uint64_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = d + k < fe ? ch_entry[d + k] : kNone;  // 4 loads in flight
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (e[k] != kNone) return (uint64_t)(d + k - fc) << chunk_shift;
+    }
+    return flen[f];
+}
 
 __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_t *fbase,
                                 const uint64_t *flen, uint32_t c, uint32_t f, uint64_t ce, uint64_t entry,
                                 uint32_t cap, uint64_t *s_off, uint4 *s_hdr, uint32_t *ch_count,
-                                uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos) {
+                                uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *ch_wend) {
     uint32_t count = 0, term = T_NONE;
     uint64_t exit = kNone, tpos = 0;
     if (entry != kNone) {
-        ScratchEmit em{s_off + (uint64_t)c * (cap + 1), s_hdr + (uint64_t)c * (cap + 1), cap};
+        ScratchEmit em{s_off + stage_slot(c, 0, cap), s_hdr + stage_slot(c, 0, cap), cap};
         walk_chain(arena, fbase[f], flen[f], ce, entry, em, count, exit, term, tpos);
     }
     ch_count[c] = count;
     ch_exit[c] = exit;
     ch_term[c] = term;
     ch_tpos[c] = tpos;
+    ch_wend[c] = ce;
 }
 
-// One lane per chunk: latency-bound header chain from the speculative entry.
+// One lane per chunk: latency-bound header chain from the speculative entry
+// to the walk bound (walk_bound).
 __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint64_t *__restrict__ fbase,
                                               const uint64_t *__restrict__ flen,
                                               const uint32_t *__restrict__ ch_file,
-                                              const uint64_t *__restrict__ ch_end,
+                                              const uint32_t *__restrict__ f_first_chunk,
+                                              const uint32_t *__restrict__ f_nchunks,
                                               const uint64_t *__restrict__ ch_entry, uint32_t *ch_count,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
-                                              uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
-                                              uint32_t n_chunks) {
+                                              uint64_t *ch_wend, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
+                                              uint32_t chunk_shift, uint32_t n_chunks) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
-    walk_into_chunk(arena, fbase, flen, c, ch_file[c], ch_end[c], ch_entry[c], cap, s_off, s_hdr, ch_count,
-                    ch_exit, ch_term, ch_tpos);
+    const uint32_t f = ch_file[c];
+    const uint64_t entry = ch_entry[c];
+    const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
+    walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_off, s_hdr, ch_count, ch_exit, ch_term, ch_tpos,
+                    ch_wend);
 }
 
-// Chunk c is consistent iff its entry equals the record start that the chain
-// of the nearest earlier non-empty chunk reaches (none if that chain ended).
-// If every chunk is consistent, every chunk is correct (chunk 0 of each file
-// is true by construction): induction over the chunk order.
+// Consistency of chunk c against j, the nearest earlier chunk of its file with
+// an entry (chunk 0 of a file always has one, entry 0): if c has an entry, j's
+// walk must have ended exactly there (exit == entry, not at an EOF); if c has
+// none, j's walk must have covered c (exit past c's end, or an EOF: then no
+// later record exists).  If every chunk is consistent, every chunk is correct:
+// induction over the chunk order from each file's chunk 0.
 __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ ch_file,
-                                                  const uint64_t *__restrict__ ch_start,
                                                   const uint64_t *__restrict__ ch_end,
                                                   const uint64_t *__restrict__ ch_entry,
                                                   const uint64_t *__restrict__ ch_exit,
@@ -332,35 +410,33 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
     if (c != fc) {
         uint32_t j = c - 1;
         while (j > fc && ch_entry[j] == kNone) --j;
-        uint64_t expect = kNone;
-        if (ch_entry[j] == kNone) {
-            bad = true;
-        } else if (ch_term[j] == T_NONE) {
-            const uint64_t x = ch_exit[j];
-            if (x < ch_start[c]) bad = true;
-            else expect = x < ch_end[c] ? x : kNone;
-        }
-        if (!bad && ch_entry[c] != expect) bad = true;
+        const bool ended = ch_entry[j] == kNone || ch_term[j] != T_NONE;
+        const uint64_t x = ch_exit[j], e = ch_entry[c];
+        bad = e != kNone ? (ended || x != e) : (!ended && x < ch_end[c]);
     }
     ch_bad[c] = bad ? 1u : 0u;
     const uint64_t m = __ballot(bad);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (uint32_t)__popcll(m));
 }
 
-// One lane per inconsistent chunk: take the entry from the nearest earlier
-// non-empty chunk and re-walk.  Chunks whose look-back crosses another
-// inconsistent chunk wait for a later round (the next k_validate decides),
-// so no lane reads state another lane is rewriting.
+// One lane per inconsistent chunk: its entry becomes the exit of the nearest
+// earlier chunk with an entry (none if that walk ended at an EOF or went past
+// this chunk), then it walks to its bound.  Chunks whose look-back crosses
+// another inconsistent chunk wait for a later round (the next k_validate
+// decides), so no lane reads state another lane is rewriting: the chunks a
+// fixed chunk's walk_bound reads all look back to it and wait.
 __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena,
                                                const uint64_t *__restrict__ fbase,
                                                const uint64_t *__restrict__ flen,
                                                const uint32_t *__restrict__ ch_file,
                                                const uint64_t *__restrict__ ch_end,
                                                const uint32_t *__restrict__ f_first_chunk,
+                                               const uint32_t *__restrict__ f_nchunks,
                                                const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
                                                uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
-                                               uint64_t *ch_tpos, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
-                                               uint32_t c_begin, uint32_t c_end, uint32_t *counter) {
+                                               uint64_t *ch_tpos, uint64_t *ch_wend, uint64_t *s_off, uint4 *s_hdr,
+                                               uint32_t cap, uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end,
+                                               uint32_t *counter) {
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end || !ch_bad[c]) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
@@ -374,8 +450,9 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
     }
     ch_entry[c] = e_new;
     atomicAdd(counter, 1u);
-    walk_into_chunk(arena, fbase, flen, c, f, ch_end[c], e_new, cap, s_off, s_hdr, ch_count, ch_exit, ch_term,
-                    ch_tpos);
+    const uint64_t ce = e_new != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
+    walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_off, s_hdr, ch_count, ch_exit, ch_term, ch_tpos,
+                    ch_wend);
 }
 
 // Exclusive scan of per-chunk record counts -> rec_base[0..n], offset by a
@@ -539,20 +616,22 @@ struct DirectEmit {
 
 // Record table in walk order: one wavefront per chunk copies its staged
 // headers; chunks that overflowed the stage re-walk straight into the table.
-__global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ arena,
-                                                 const uint64_t *__restrict__ fbase,
-                                                 const uint64_t *__restrict__ flen,
-                                                 const uint32_t *__restrict__ ch_file,
-                                                 const uint64_t *__restrict__ ch_end,
-                                                 const uint64_t *__restrict__ ch_entry,
-                                                 const uint32_t *__restrict__ ch_count,
-                                                 const uint64_t *__restrict__ rec_base,
-                                                 const uint64_t *__restrict__ s_off,
-                                                 const uint4 *__restrict__ s_hdr, uint32_t cap,
-                                                 uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
-                                                 uint4 *rec_hdr, uint32_t *rec_file, uint32_t *counters) {
+// A workgroup takes 16 consecutive chunks, so the stage lines it reads (slot
+// i of kStageIl consecutive chunks, stage_slot) are fetched once per CU.
+__global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ arena,
+                                                  const uint64_t *__restrict__ fbase,
+                                                  const uint64_t *__restrict__ flen,
+                                                  const uint32_t *__restrict__ ch_file,
+                                                  const uint64_t *__restrict__ ch_wend,
+                                                  const uint64_t *__restrict__ ch_entry,
+                                                  const uint32_t *__restrict__ ch_count,
+                                                  const uint64_t *__restrict__ rec_base,
+                                                  const uint64_t *__restrict__ s_off,
+                                                  const uint4 *__restrict__ s_hdr, uint32_t cap,
+                                                  uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
+                                                  uint4 *rec_hdr, uint32_t *rec_file, uint32_t *counters) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
     if (c >= n_chunks) return;
     const uint64_t entry = ch_entry[c];
     const uint32_t cnt = ch_count[c];
@@ -564,7 +643,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ are
         for (uint32_t i = lane; i < cnt; i += 64) {
             const uint64_t r = rb + i;
             if (r >= n_total) break;
-            const uint64_t si = (uint64_t)c * (cap + 1) + i;
+            const uint64_t si = stage_slot(c, i, cap);
             rec_off[r] = base + s_off[si];
             rec_hdr[r] = s_hdr[si];
             rec_file[r] = f;
@@ -574,7 +653,7 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ are
         DirectEmit em{rec_off, rec_hdr, rec_file, rb, n_total, base, f};
         uint32_t count, term;
         uint64_t exit, tpos;
-        walk_chain(arena, base, flen[f], ch_end[c], entry, em, count, exit, term, tpos);
+        walk_chain(arena, base, flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
     }
 }
 
@@ -984,548 +1063,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     }
 }
 
-// ------------------------------------------------- fused pass (experimental) ---
-// GCK_OPT_FUSED: boundary discovery inside the streaming CRC pass.  A
-// wavefront takes a whole chunk from a queue, streams its rows in order (NR a
-// step, the next step's loads in flight) and follows the header chain from
-// the chunk's speculative entry through the words it already holds (a dynamic
-// register index + readlane per dword: tens of cycles a hop instead of an HBM
-// round trip).  This replaces k_walk, k_row_index and k_row_plan; the CRC
-// arithmetic per row is k_crc_rows'.
-//   stage: the k_walk stage (offset, header) per chunk-local record;
-//   ep stage, (cap + 2) slots per chunk: slot 1 + i = (c, pre) of local record
-//     i's last byte when it lies in the chunk; slot 0 ("incoming") = the end of
-//     a record that began in an earlier chunk: at entry - 1 when the entry is
-//     past the chunk start, or at the chunk's last byte when the chunk holds no
-//     header start and the next chunk's entry is its end (or the file ends).
-// k_compact_fused resolves every record's slot.  The cuts of a row are
-// consecutive slots in lane order (incoming, then records), as k_crc_rows
-// needs.  Records decoded per step are held two per lane and leave in a fixed
-// number of stores (more than 64 in a step, or than cap in a chunk:
-// the run is redone on the standard path).
-
-// (a & m) | (b & ~m) with a scalar mask, opaque to the compiler: a select
-// tree written with ?: is folded back into an indexed load from a stack copy
-// (scratch), which also makes every later vmcnt wait drain the row prefetch.
-// x as a wave-uniform (SGPR) value: the chain state is uniform by
-// construction, but the compiler's divergence analysis loses that through the
-// parse loop and would keep it (and every branch on it) in VGPRs/exec masks.
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint32_t vsel(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(a), "v"(b));
-    return r;
-}
-// v[k] for a wave-uniform k: a 4-level select tree (15 v_bfi_b32).
-__device__ __forceinline__ uint32_t pick16(const u32x16 &v, uint32_t k) {
-    const uint32_t m8 = (k & 8u) ? ~0u : 0u, m4 = (k & 4u) ? ~0u : 0u, m2 = (k & 2u) ? ~0u : 0u,
-                   m1 = (k & 1u) ? ~0u : 0u;
-    uint32_t l1[8], l2[4];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) l1[j] = vsel(m8, v[j + 8], v[j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) l2[j] = vsel(m4, l1[j + 4], l1[j]);
-    return vsel(m1, vsel(m2, l2[3], l2[1]), vsel(m2, l2[2], l2[0]));
-}
-
-// Words k, k+1, k+2 (mod 16) of v for a wave-uniform k: a barrel shift that
-// keeps only the needed outputs (23 v_bfi_b32).
-__device__ __forceinline__ void pick3(const u32x16 &v, uint32_t k, uint32_t &o0, uint32_t &o1, uint32_t &o2) {
-    const uint32_t m8 = (k & 8u) ? ~0u : 0u, m4 = (k & 4u) ? ~0u : 0u, m2 = (k & 2u) ? ~0u : 0u,
-                   m1 = (k & 1u) ? ~0u : 0u;
-    uint32_t x1[10], x2[6], x3[4];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) x1[j] = vsel(m8, v[(j + 8) & 15], v[j]);
-#pragma unroll
-    for (int j = 0; j < 6; ++j) x2[j] = vsel(m4, x1[j + 4], x1[j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x3[j] = vsel(m2, x2[j + 2], x2[j]);
-    o0 = vsel(m1, x3[1], x3[0]);
-    o1 = vsel(m1, x3[2], x3[1]);
-    o2 = vsel(m1, x3[3], x3[2]);
-}
-
-template <int NR>
-__global__ __launch_bounds__(1024) void k_fuse(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                               const uint64_t *__restrict__ fbase, const uint64_t *__restrict__ flen,
-                                               const uint32_t *__restrict__ ch_file,
-                                               const uint64_t *__restrict__ ch_start,
-                                               const uint64_t *__restrict__ ch_end,
-                                               const uint64_t *__restrict__ ch_entry,
-                                               const uint32_t *__restrict__ f_first_chunk,
-                                               const uint32_t *__restrict__ f_nchunks,
-                                               const uint32_t *__restrict__ list,
-                                               const uint32_t *__restrict__ list_n, uint32_t n_chunks,
-                                               uint32_t *__restrict__ ch_count, uint64_t *__restrict__ ch_exit,
-                                               uint32_t *__restrict__ ch_term, uint64_t *__restrict__ ch_tpos,
-                                               uint64_t *__restrict__ s_off, uint4 *__restrict__ s_hdr,
-                                               uint2 *__restrict__ s_ep, uint32_t cap,
-                                               const uint32_t *__restrict__ g_slice,
-                                               const uint32_t *__restrict__ g_nib, uint32_t *__restrict__ out_rend,
-                                               uint32_t *__restrict__ queue, uint32_t *__restrict__ counters) {
-    // list mode (validation rounds): the chunks to stream again; none: leave
-    // before filling the tables
-    const uint32_t n_list = list ? *list_n : 0u;
-    if (list && n_list == 0) return;
-    __shared__ uint32_t lds[40960];
-    fill_crc_lds(lds, g_slice, g_nib);
-    const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
-    const uint32_t nbyte = (kNibBase + (lane >> 5) * 4096 + l31) * 4;
-    const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
-    const uint32_t s_rel = lane * kSlab;
-    constexpr uint32_t kDrop = 0xFFFFFFF0u;
-
-    auto grab = [&]() -> uint32_t {
-        uint32_t v = 0;
-        if (lane == 0) {
-            v = atomicAdd(queue, 1u);
-            if (list) v = v < n_list ? list[v] : n_chunks;
-        }
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-    };
-    struct RowBuf {
-        u32x4 x[4];
-    };
-    auto issue = [&](uint64_t row0, RowBuf (&bs)[NR]) {
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            const uint64_t r = min(row0 + i, n_rows - 1);
-            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
-            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel, 0, 0);
-            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 16, 0, 0);
-            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 32, 0, 0);
-            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 48, 0, 0);
-        }
-    };
-
-    uint32_t c = grab();
-    if (c >= n_chunks) return;
-    RowBuf buf0[NR], buf1[NR];  // fixed registers: the steps alternate in pairs
-    {
-        const uint64_t b0 = fbase[ch_file[c]] + ch_start[c];
-        issue(b0 / kRow, buf0);
-    }
-    for (;;) {
-        const uint32_t f = ch_file[c];
-        const uint64_t base = fbase[f], len = flen[f], cs = ch_start[c], ce = ch_end[c];
-        const uint64_t entry = ch_entry[c];
-        const uint32_t fc = f_first_chunk[f], fn = f_nchunks[f];
-        const uint64_t R0 = (base + cs) / kRow, R1 = (base + ce + kRow - 1) / kRow;  // the chunk's rows
-        const bool next_at_end = c + 1 >= fc + fn || ch_entry[c + 1] == ce;
-        // the incoming cut (file-relative), kNone if the chunk has none
-        const uint64_t in_pos = entry != kNone ? (entry > cs ? entry - 1 : kNone) : (next_at_end ? ce - 1 : kNone);
-        const uint32_t cn = grab();  // the next chunk (its first rows load during this one's last step)
-        // parse state (wave-uniform)
-        uint64_t p = entry, tpos = 0, pend = kNone;
-        uint32_t nrec = 0, term = T_NONE, pend_slot = 0, over = 0;
-#ifdef GCK_XP_NOPARSE
-        bool done = true;
-#else
-        bool done = entry == kNone;
-#endif
-        uint32_t carry[4] = {0u, 0u, 0u, 0u};  // the 16 bytes before the window
-        uint32_t rend_buf = 0;
-        const uint64_t stage0 = (uint64_t)c * (cap + 1), ep0 = (uint64_t)c * (cap + 2);
-        const __amdgpu_buffer_rsrc_t ep_rsrc = make_rsrc(s_ep + ep0, (cap + 2) * 8);
-        const __amdgpu_buffer_rsrc_t off_rsrc = make_rsrc(s_off + stage0, cap * 8);
-        const __amdgpu_buffer_rsrc_t hdr_rsrc = make_rsrc(s_hdr + stage0, cap * 16);
-        auto step = [&](const RowBuf(&bs)[NR], RowBuf(&nb)[NR], uint64_t R) {
-            // the next step's rows: this chunk's, or the next chunk's first
-            uint64_t nrow = R + NR;
-            if (nrow >= R1) nrow = cn < n_chunks ? (fbase[ch_file[cn]] + ch_start[cn]) / kRow : R;
-            issue(nrow, nb);
-            // a row's 16 words as one vector value: a uniform dynamic index is a
-            // relative register move, not a private (scratch) array
-            u32x16 w[NR];
-#pragma unroll
-            for (int i = 0; i < NR; ++i)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    w[i][4 * k] = bs[i].x[k].x;
-                    w[i][4 * k + 1] = bs[i].x[k].y;
-                    w[i][4 * k + 2] = bs[i].x[k].z;
-                    w[i][4 * k + 3] = bs[i].x[k].w;
-                }
-            // ---- parse the window [W0, W0 + NR rows) (file-relative) ----
-            const uint64_t W0 = R * kRow - base, WE = W0 + (uint64_t)NR * kRow;
-            uint32_t m[NR], ra[NR];  // per row: this lane's cut blocks, the row's first cut slot
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                m[i] = 0;
-                ra[i] = kNone32;
-            }
-            auto cut = [&](uint64_t pos, uint32_t slot) {  // pos in [W0, WE)
-                const uint32_t o = (uint32_t)(pos - W0), row = o / kRow, ln = (o % kRow) / kSlab,
-                               blk = (o % kSlab) / kBlock;
-#pragma unroll
-                for (int i = 0; i < NR; ++i)
-                    if (row == (uint32_t)i) {
-                        if (lane == ln) m[i] |= 1u << blk;
-                        if (ra[i] == kNone32) ra[i] = slot;
-                    }
-            };
-            auto dword = [&](int64_t d) -> uint32_t {  // dword d of the window (d >= -4: the carry)
-                if (d < 0) {
-                    const uint32_t j = (uint32_t)(d + 4), m1 = (j & 1u) ? ~0u : 0u, m2 = (j & 2u) ? ~0u : 0u;
-                    return vsel(m2, vsel(m1, carry[3], carry[2]), vsel(m1, carry[1], carry[0]));
-                }
-                const uint32_t row = (uint32_t)(d >> 10), ln = (uint32_t)(d >> 4) & 63u, word = (uint32_t)d & 15u;
-                uint32_t v = 0;
-#pragma unroll
-                for (int i = 0; i < NR; ++i)
-                    if (row == (uint32_t)i) {
-                        const uint32_t x = pick16(w[i], word);
-                        v = (uint32_t)__builtin_amdgcn_readlane((int)x, (int)ln);
-                    }
-                return v;
-            };
-            if (in_pos != kNone && in_pos >= W0 && in_pos < WE) cut(in_pos, 0);
-            if (pend != kNone && pend < WE) {
-                cut(pend, pend_slot);
-                pend = kNone;
-            }
-            uint32_t srec = 0;             // records decoded in this step
-            constexpr int kSlots = 1;  // record slots per lane: 64 records a step (C3's records are >= 88 B)
-            constexpr uint32_t kStepRecs = 64 * kSlots;
-            uint64_t r_off[kSlots];  // lane l holds step records l, l + 64, ...
-            uint32_t r_h[kSlots][2];  // KeySize, ValueSize (CRC, Timestamp: k_finalize, from the arena)
-#pragma unroll
-            for (int q = 0; q < kSlots; ++q) {
-                r_off[q] = 0;
-                r_h[q][0] = r_h[q][1] = 0u;
-            }
-            while (!done) {
-                p = uni64(p);
-                if (p >= ce) { done = true; break; }
-                const uint64_t rem = len - p;
-                if (rem < 16) { term = T_ERR; tpos = p; done = true; break; }  // ErrUnexpectedEOF
-                if (p + 16 > WE) break;                                         // the header continues in the next step
-                // KeySize / ValueSize: bytes p+8 .. p+15, in window dwords d8 .. d8+2
-                const int64_t d8 = (int64_t)uni64((uint64_t)(((int64_t)p + 8 - (int64_t)W0) >> 2));
-                const uint32_t sh = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(p & 3));
-                uint32_t a2, a3, a4;
-                if (d8 >= 0 && (d8 >> 10) == ((d8 + 2) >> 10) && (d8 >> 10) < NR) {
-                    // one row: words k .. k+2 of every slab, then the lane (the next one past word 15)
-                    const uint32_t row = (uint32_t)(d8 >> 10), ln = (uint32_t)(d8 >> 4) & 63u, k = (uint32_t)d8 & 15u;
-#ifndef GCK_PICK_TREE
-                    // a uniform branch on (row, k): three readlanes from fixed
-                    // registers (no select tree)
-                    a2 = a3 = a4 = 0;
-#define GCK_H3(K)                                                                              \
-    case K:                                                                                    \
-        a2 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][K], (int)ln);                       \
-        a3 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][(K + 1) & 15], (int)(ln + ((K + 1) >> 4))); \
-        a4 = (uint32_t)__builtin_amdgcn_readlane((int)w[i][(K + 2) & 15], (int)(ln + ((K + 2) >> 4))); \
-        break;
-#pragma unroll
-                    for (int i = 0; i < NR; ++i)
-                        if (row == (uint32_t)i) {
-                            switch (k) {
-                                GCK_H3(0) GCK_H3(1) GCK_H3(2) GCK_H3(3) GCK_H3(4) GCK_H3(5) GCK_H3(6) GCK_H3(7)
-                                GCK_H3(8) GCK_H3(9) GCK_H3(10) GCK_H3(11) GCK_H3(12) GCK_H3(13) GCK_H3(14) GCK_H3(15)
-                            }
-                        }
-#undef GCK_H3
-#else
-                    uint32_t o0 = 0, o1 = 0, o2 = 0;
-#pragma unroll
-                    for (int i = 0; i < NR; ++i)
-                        if (row == (uint32_t)i) pick3(w[i], k, o0, o1, o2);
-                    a2 = (uint32_t)__builtin_amdgcn_readlane((int)o0, (int)(ln + ((k + 0) >> 4)));
-                    a3 = (uint32_t)__builtin_amdgcn_readlane((int)o1, (int)(ln + ((k + 1) >> 4)));
-                    a4 = (uint32_t)__builtin_amdgcn_readlane((int)o2, (int)(ln + ((k + 2) >> 4)));
-#endif
-                } else {
-                    // the carry (d < 0), the end of a row (lane 63, words 14-15)
-                    // or the start of the next (lane 0, words 0-2): constant
-                    // register indices, no select tree
-                    auto edge = [&](int64_t d) -> uint32_t {
-                        if (d < 0) {  // readfirstlane: an asm result counts as divergent
-                            const uint32_t j = (uint32_t)(d + 4), m1 = (j & 1u) ? ~0u : 0u, m2 = (j & 2u) ? ~0u : 0u;
-                            return (uint32_t)__builtin_amdgcn_readfirstlane(
-                                (int)vsel(m2, vsel(m1, carry[3], carry[2]), vsel(m1, carry[1], carry[0])));
-                        }
-                        const uint32_t row = (uint32_t)(d >> 10), wd = (uint32_t)d & 1023u;
-                        uint32_t v = 0;
-#pragma unroll
-                        for (int i = 0; i < NR; ++i)
-                            if (row == (uint32_t)i) {
-                                if (wd >= 1008u) {  // lane 63
-                                    const uint32_t m = (wd & 1u) ? ~0u : 0u;
-                                    v = (uint32_t)__builtin_amdgcn_readlane((int)vsel(m, w[i][15], w[i][14]), 63);
-                                } else {  // lane 0
-                                    const uint32_t m1 = (wd & 1u) ? ~0u : 0u, m2 = (wd & 2u) ? ~0u : 0u;
-                                    v = (uint32_t)__builtin_amdgcn_readlane(
-                                        (int)vsel(m2, w[i][2], vsel(m1, w[i][1], w[i][0])), 0);
-                                }
-                            }
-                        return v;
-                    };
-                    a2 = edge(d8);
-                    a3 = edge(d8 + 1);
-                    a4 = (d8 + 2) < (int64_t)NR * 1024 ? edge(d8 + 2) : 0u;
-                }
-                const uint32_t ks = ab(a3, a2, sh), vs = ab(a4, a3, sh);
-                const uint32_t klen = ks ? ks : vs;  // db.go:151-155
-                const uint64_t rem2 = rem - 16;
-                if (klen > 0 && rem2 == 0) { term = T_SILENT; tpos = p; done = true; break; }  // ReadFull io.EOF
-                if (rem2 < klen) { term = T_ERR; tpos = p; done = true; break; }               // partial key
-                uint64_t next;
-                if (ks == 0) {
-                    next = p + 16 + klen;  // tombstone
-                } else {
-                    if (rem2 - klen < vs) { term = T_SILENT; tpos = p; done = true; break; }  // Discard io.EOF
-                    next = p + 16 + (uint64_t)ks + vs;
-                }
-                if (srec < kStepRecs) {
-                    const uint32_t hl = srec & 63, hs = srec >> 6;
-#pragma unroll
-                    for (int q = 0; q < kSlots; ++q)
-                        if (hs == (uint32_t)q && lane == hl) {
-                            r_off[q] = p;
-                            r_h[q][0] = ks;
-                            r_h[q][1] = vs;
-                        }
-                } else {
-                    over = 1;
-                }
-                ++srec;
-                const uint32_t slot = 1 + nrec;
-                ++nrec;
-                if (next - 1 < WE) cut(next - 1, slot);
-                else { pend = next - 1; pend_slot = slot; }
-                p = next;
-            }
-            // the step's records leave in a fixed number of stores (out of range: dropped)
-            {
-                const uint32_t first = nrec - srec;  // local index of the step's first record
-#pragma unroll
-                for (int q = 0; q < kSlots; ++q) {
-                    const uint32_t k = lane + 64u * q, li = first + k;
-                    const bool st = k < srec && k < kStepRecs && li < cap;
-                    u32x2 ov;
-                    ov.x = (uint32_t)r_off[q];
-                    ov.y = (uint32_t)(r_off[q] >> 32);
-                    __builtin_amdgcn_raw_buffer_store_b64(ov, off_rsrc, (int)(st ? li * 8u : kDrop), 0, 0);
-                    u32x4 hv;
-                    hv.x = 0u;
-                    hv.y = 0u;
-                    hv.z = r_h[q][0];
-                    hv.w = r_h[q][1];
-                    __builtin_amdgcn_raw_buffer_store_b128(hv, hdr_rsrc, (int)(st ? li * 16u : kDrop), 0, 0);
-                }
-            }
-            // ---- the rows' CRC arithmetic (k_crc_rows' process) ----
-            uint32_t a[NR], c1[NR], c2[NR], c3[NR], G[NR];
-#pragma unroll
-            for (int i = 0; i < NR; ++i) a[i] = w[i][0];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-#pragma unroll
-                for (int i = 0; i < NR; ++i) {
-                    const uint32_t nx = j < 15 ? w[i][j < 15 ? j + 1 : 15] : 0u;
-                    if (j == 15) {
-                        G[i] = slice4x(lds, lb0, lb1, a[i], 0u);
-                    } else if ((j & 3) == 3) {
-                        const uint32_t cc = slice4x(lds, lb0, lb1, a[i], 0u);
-                        if (j == 3) c1[i] = cc;
-                        if (j == 7) c2[i] = cc;
-                        if (j == 11) c3[i] = cc;
-                        a[i] = cc ^ nx;
-                    } else {
-                        a[i] = slice4x(lds, lb0, lb1, a[i], nx);
-                    }
-                }
-            }
-            uint32_t P[NR], pre[NR];
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                uint32_t t[8];
-#pragma unroll
-                for (int qn = 0; qn < 8; ++qn) {
-                    const uint32_t s4 = 4 * qn;
-                    const uint32_t x = s4 >= 7 ? G[i] >> (s4 - 7) : G[i] << (7 - s4);
-                    t[qn] = lds_at(lds, (x & 0x780u) | (nbyte + qn * 2048));
-                }
-                P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
-            }
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                const bool in_chunk = R + i < R1;
-                const uint32_t mi = in_chunk ? m[i] : 0u;
-                auto capr = [&](uint32_t b) {
-                    uint32_t v = b == 3 ? c3[i] : c2[i];
-                    v = b == 1 ? c1[i] : v;
-                    return b == 0 ? 0u : v;
-                };
-                if (__ballot(mi & (mi - 1)) == 0) {
-                    const uint64_t C = __ballot(mi != 0);
-                    const uint32_t idx =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-                    u32x2 v;
-                    v.x = capr((uint32_t)__builtin_ctz(mi | 16u));
-                    v.y = pre[i];
-                    __builtin_amdgcn_raw_buffer_store_b64(v, ep_rsrc, (int)(mi ? (ra[i] + idx) * 8u : kDrop), 0, 0);
-                } else {
-                    const uint32_t n = __builtin_popcount(mi);
-                    const uint32_t ex = wave_incl_sum(n) - n;
-                    uint32_t mm = mi;
-#pragma unroll
-                    for (uint32_t q = 0; q < 4; ++q) {
-                        u32x2 v;
-                        v.x = capr((uint32_t)__builtin_ctz(mm | 16u));
-                        v.y = pre[i];
-                        __builtin_amdgcn_raw_buffer_store_b64(v, ep_rsrc, (int)(q < n ? (ra[i] + ex + q) * 8u : kDrop),
-                                                              0, 0);
-                        mm &= mm - 1;
-                    }
-                }
-                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P[i], 63);
-                const uint32_t rr = (uint32_t)(R + i - R0);  // row within the chunk
-                rend_buf = (lane == (rr & 63)) ? total : rend_buf;
-                if ((rr & 63) == 63 || R + i + 1 == R1) {  // 64 rows (or the chunk) done: one coalesced store
-                    const uint64_t rb = R + i - (rr & 63);
-                    if (lane <= (rr & 63) && in_chunk) out_rend[rb + lane] = rend_buf;
-                }
-            }
-            // the 16 bytes before the next window
-#pragma unroll
-            for (int k = 0; k < 4; ++k) carry[k] = (uint32_t)__builtin_amdgcn_readlane((int)w[NR - 1][12 + k], 63);
-        };
-        const uint64_t steps = (R1 - R0 + NR - 1) / NR;
-        for (uint64_t st = 0; st < steps; st += 2) {
-            step(buf0, buf1, R0 + st * NR);
-            if (st + 1 < steps) step(buf1, buf0, R0 + (st + 1) * NR);
-        }
-        if (steps & 1) {  // the next chunk's first rows went to buf1 (rare: a file's last chunk)
-#pragma unroll
-            for (int i = 0; i < NR; ++i) buf0[i] = buf1[i];
-        }
-        // a header that starts in the chunk but ends past its rows: read it directly
-        while (!done) {
-            if (p >= ce) { done = true; break; }
-            const uint64_t rem = len - p;
-            if (rem < 16) { term = T_ERR; tpos = p; done = true; break; }
-            const Hdr h = ld_hdr(arena, base + p);
-            const uint32_t klen = h.ks ? h.ks : h.vs;
-            const uint64_t rem2 = rem - 16;
-            if (klen > 0 && rem2 == 0) { term = T_SILENT; tpos = p; done = true; break; }
-            if (rem2 < klen) { term = T_ERR; tpos = p; done = true; break; }
-            uint64_t next;
-            if (h.ks == 0) {
-                next = p + 16 + klen;
-            } else {
-                if (rem2 - klen < h.vs) { term = T_SILENT; tpos = p; done = true; break; }
-                next = p + 16 + (uint64_t)h.ks + h.vs;
-            }
-            if (lane == 0 && nrec < cap) {
-                s_off[stage0 + nrec] = p;
-                s_hdr[stage0 + nrec] = make_uint4(h.crc, h.ts, h.ks, h.vs);
-            }
-            ++nrec;
-            p = next;
-        }
-        if (nrec > cap) over = 1;
-        if (lane == 0) {
-            ch_count[c] = nrec;
-            ch_exit[c] = p;
-            ch_term[c] = term;
-            ch_tpos[c] = tpos;
-            if (over) atomicAdd(&counters[2], 1u);
-        }
-        if (cn >= n_chunks) return;
-        c = cn;
-    }
-}
-
-// Record table of the fused pass: one wavefront per chunk copies its staged
-// records and resolves each record's (c, pre) slot: its own when its last byte
-// lies in the chunk, else the incoming slot of the chunk that holds it.
-__global__ __launch_bounds__(256) void k_compact_fused(const uint64_t *__restrict__ fbase,
-                                                       const uint32_t *__restrict__ ch_file,
-                                                       const uint64_t *__restrict__ ch_end,
-                                                       const uint32_t *__restrict__ ch_count,
-                                                       const uint64_t *__restrict__ rec_base,
-                                                       const uint32_t *__restrict__ f_first_chunk,
-                                                       const uint64_t *__restrict__ s_off,
-                                                       const uint4 *__restrict__ s_hdr,
-                                                       const uint2 *__restrict__ s_ep, uint32_t cap,
-                                                       uint32_t chunk_shift, uint32_t n_chunks, uint64_t n_total,
-                                                       uint64_t *__restrict__ rec_off, uint4 *__restrict__ rec_hdr,
-                                                       uint32_t *__restrict__ rec_file, uint2 *__restrict__ ep) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
-    const uint32_t cnt = min(ch_count[c], cap);
-    const uint64_t rb = rec_base[c];
-    const uint32_t f = ch_file[c];
-    const uint64_t base = fbase[f], ce = ch_end[c];
-    for (uint32_t i = lane; i < cnt; i += 64) {
-        const uint64_t r = rb + i;
-        if (r >= n_total) break;
-        const uint64_t si = (uint64_t)c * (cap + 1) + i;
-        const uint64_t p = s_off[si];
-        const uint4 h = s_hdr[si];
-        rec_off[r] = base + p;
-        rec_hdr[r] = h;
-        rec_file[r] = f;
-        const uint64_t last = p + 16 + (uint64_t)h.z + h.w - 1;  // tombstone: KeySize 0, the key is the "value"
-        const uint64_t slot = last < ce ? (uint64_t)c * (cap + 2) + 1 + i
-                                        : (uint64_t)(f_first_chunk[f] + (uint32_t)(last >> chunk_shift)) * (cap + 2);
-        ep[r] = s_ep[slot];
-    }
-}
-
-// After k_validate: the inconsistent chunks take the entry from the nearest
-// earlier non-empty chunk (as k_fixup) and are marked to be streamed again,
-// with the chunk before them when it holds no header start (its incoming cut
-// depends on this chunk's entry).
-__global__ __launch_bounds__(256) void k_fuse_fix(const uint32_t *__restrict__ ch_file,
-                                                  const uint64_t *__restrict__ ch_end,
-                                                  const uint32_t *__restrict__ f_first_chunk,
-                                                  const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
-                                                  const uint64_t *__restrict__ ch_exit,
-                                                  const uint32_t *__restrict__ ch_term, uint32_t *redo,
-                                                  uint32_t *list, uint32_t *list_n, uint32_t n_chunks,
-                                                  uint32_t *counter) {
-    auto add = [&](uint32_t x) {  // once per chunk
-        if (atomicExch(redo + x, 1u) == 0u) list[atomicAdd(list_n, 1u)] = x;
-    };
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks || !ch_bad[c]) return;
-    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
-    uint32_t j = c - 1;
-    while (j > fc && ch_entry[j] == kNone && !ch_bad[j]) --j;
-    if (ch_bad[j] || ch_entry[j] == kNone) return;
-    uint64_t e_new = kNone;
-    if (ch_term[j] == T_NONE) {
-        const uint64_t x = ch_exit[j];
-        if (x < ch_end[c]) e_new = x;
-    }
-    ch_entry[c] = e_new;
-    add(c);
-    if (c > fc && ch_entry[c - 1] == kNone) add(c - 1);
-    atomicAdd(counter, 1u);
-}
-
 // ---------------------------------------------------------------- finalize ---
 // Per record r = [rs, ve) (core/db.go:311 applied to every record).  Notation
 // as in gck_math.h; for a position p inside row R (row end E_R):
@@ -1596,7 +1133,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                                                   const uint32_t *__restrict__ zrow,
                                                   const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
-                                                  uint32_t *counters, uint32_t hdr_from_arena) {
+                                                  uint32_t *counters) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
@@ -1669,10 +1206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         uint32_t pw[11];
 #pragma unroll
         for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
-        // the fused pass stages KeySize / ValueSize only: CRC and Timestamp
-        // come from these words
-        const uint32_t hcrc = hdr_from_arena ? ab(pw[1], pw[0], lead) : h.x;
-        const uint32_t hts = hdr_from_arena ? ab(pw[2], pw[1], lead) : h.y;
+        const uint32_t hcrc = h.x, hts = h.y;
         pw[0] &= ~0u << (8 * lead);
         // unrolled over the words in registers (no indexed register array),
         // then the words of long keys from memory
@@ -1716,6 +1250,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
     if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&blk_rej, wsum);
     __syncthreads();
     if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[3], blk_rej);
+}
+
+// Measurement variants of k_walk (gck_diag_walk_variant): MODE bit 1 = header
+// by two loads (ld_hdr2), 2 = stage only (KeySize, ValueSize) (8 B a hop),
+// 4 = no stage stores.  Same chains, counts and exits as k_walk.
+struct Stage8Emit {
+    uint2 *kv;
+    uint32_t cap;
+    __device__ void operator()(uint32_t i, uint64_t, const Hdr &h) const { kv[i < cap ? i : cap] = make_uint2(h.ks, h.vs); }
+    __device__ void prime() const { kv[cap] = make_uint2(0, 0); }
+};
+struct NoEmit {
+    __device__ void operator()(uint32_t, uint64_t, const Hdr &) const {}
+    __device__ void prime() const {}
+};
+template <int MODE>
+__global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
+                                                 const uint64_t *__restrict__ flen,
+                                                 const uint32_t *__restrict__ ch_file,
+                                                 const uint64_t *__restrict__ ch_entry,
+                                                 const uint64_t *__restrict__ ch_wend, uint32_t *ch_count,
+                                                 uint64_t *ch_exit, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
+                                                 uint32_t n_chunks) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_chunks) return;
+    const uint64_t entry = ch_entry[c];
+    if (entry == kNone) return;
+    const uint32_t f = ch_file[c];
+    uint32_t count = 0, term;
+    uint64_t exit = 0, tpos;
+    constexpr bool H2 = (MODE & 1) != 0;
+    if constexpr ((MODE & 4) != 0) {
+        walk_chain<NoEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, NoEmit{}, count, exit, term, tpos);
+    } else if constexpr ((MODE & 2) != 0) {
+        Stage8Emit em{reinterpret_cast<uint2 *>(s_hdr) + stage_slot(c, 0, cap), cap};
+        walk_chain<Stage8Emit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
+    } else {
+        ScratchEmit em{s_off + stage_slot(c, 0, cap), s_hdr + stage_slot(c, 0, cap), cap};
+        walk_chain<ScratchEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
+    }
+    ch_count[c] = count;
+    ch_exit[c] = exit;
 }
 
 // ------------------------------------------------------------- host side ---
@@ -1771,16 +1347,20 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     d.chunk_bytes = 512 << 10;
     d.max_key = 65536;
     d.chunk_cap = 1024;
+    d.spec_window = 0;  // the whole chunk
     if (o) {
         d.device = o->device;
         if (o->chunk_bytes) d.chunk_bytes = o->chunk_bytes;
-        else if (o->flags & GCK_OPT_FUSED) d.chunk_bytes = 256 << 10;  // shorter serial re-streams (§10d)
         if (o->max_key) d.max_key = o->max_key;
         if (o->chunk_cap) d.chunk_cap = o->chunk_cap;
+        if (o->spec_window) d.spec_window = o->spec_window;
         d.flags = o->flags;
     }
     if (d.chunk_bytes < 4096 || (d.chunk_bytes & (d.chunk_bytes - 1))) return GCK_EINVAL;
+    if (d.spec_window == 0 || d.spec_window > d.chunk_bytes) d.spec_window = d.chunk_bytes;
+    d.spec_window = (d.spec_window + 4095u) & ~4095u;  // whole 4 KiB search windows
     c->opts = d;
+    c->chunk_shift = (uint32_t)__builtin_ctz(d.chunk_bytes);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= d.device || d.device < 0) {
         set_error("hipGetDeviceCount", hipErrorNoDevice, __FILE__, __LINE__);
@@ -1823,7 +1403,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
 static void ctx_free(Ctx *c) {
     DBuf *all[] = {&c->arena, &c->d_fbase, &c->d_flen, &c->d_ffirst, &c->d_fnch, &c->d_fbad, &c->d_fterm,
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
-                   &c->d_ch_end, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
+                   &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_hdr, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
@@ -1831,7 +1411,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
-                   &c->d_gvoff, &c->d_gvals, &c->d_fep, &c->d_redo, &c->d_flist};
+                   &c->d_gvoff, &c->d_gvals};
     for (DBuf *b : all) b->release();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
@@ -1885,11 +1465,12 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ffirstrec.ensure(nf * 8)) || (rc = c->d_carry.ensure(nf * 4)) ||
         (rc = c->d_ch_file.ensure((nc + 1) * 4)) || (rc = c->d_ch_start.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_end.ensure((nc + 1) * 8)) || (rc = c->d_ch_entry.ensure((nc + 1) * 8)) ||
+        (rc = c->d_ch_wend.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 1) * (cap + 1) * 8)) ||
-        (rc = c->d_scratch_hdr.ensure((nc + 1) * (cap + 1) * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 64) / 64 * 64 * (cap + 1) * 8)) ||
+        (rc = c->d_scratch_hdr.ensure((nc + 64) / 64 * 64 * (cap + 1) * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_plan.ensure((c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
         return rc;
@@ -1917,6 +1498,16 @@ static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + p
 enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
 constexpr int kRounds = 2;             // device validation/fixup rounds
 
+static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1) {
+    k_fixup<<<nblk(c1 - c0, 256), 256, 0, s>>>(
+        c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
+        c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
+        c->d_ch_entry.as<uint64_t>(), c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
+        c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(),
+        c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
+        c->d_counters.as<uint32_t>() + CNT_FIXUP);
+}
+
 // Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
 // kRounds validate/fixup rounds and a final validation counted at val_cnt[kRounds].
 static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt) {
@@ -1925,29 +1516,21 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
     k_spec_entry<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_start.as<uint64_t>() + c0,
                                             c->d_ch_end.as<uint64_t>() + c0, c->d_ch_entry.as<uint64_t>() + c0, n,
-                                            c->opts.max_key);
+                                            c->opts.max_key, c->opts.spec_window);
     k_walk<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-                                        c->d_ch_file.as<uint32_t>() + c0, c->d_ch_end.as<uint64_t>() + c0,
-                                        c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
-                                        c->d_ch_exit.as<uint64_t>() + c0, c->d_ch_term.as<uint32_t>() + c0,
-                                        c->d_ch_tpos.as<uint64_t>() + c0,
-                                        c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * (cap + 1),
-                                        c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * (cap + 1), cap, n);
+                                        c->d_ch_file.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
+                                        c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
+                                        c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
+                                        c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
+                                        c->d_ch_wend.as<uint64_t>(), c->d_scratch_off.as<uint64_t>(),
+                                        c->d_scratch_hdr.as<uint4>(), cap, c->chunk_shift, c1);
     for (int r = 0; r <= kRounds; ++r) {
-        k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
-                                                c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-                                                c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(), val_cnt + r, c0,
-                                                c1);
+        k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
+                                                c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
+                                                c->d_ch_term.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
+                                                c->d_ch_bad.as<uint32_t>(), val_cnt + r, c0, c1);
         if (r == kRounds) break;
-        k_fixup<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
-                                             c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                             c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
-                                             c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
-                                             c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
-                                             c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                             c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), cap, c0, c1,
-                                             c->d_counters.as<uint32_t>() + CNT_FIXUP);
+        launch_fixup(c, s, c0, c1);
     }
 }
 
@@ -1976,12 +1559,11 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                            const uint64_t *rng, uint64_t cap) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
     if (n)
-        k_compact<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_end.as<uint64_t>() + c0,
+        k_compact<<<nblk(n, 16), 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
                                              c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
                                              c->d_rec_base.as<uint64_t>() + c0,
-                                             c->d_scratch_off.as<uint64_t>() + (uint64_t)c0 * (ccap + 1),
-                                             c->d_scratch_hdr.as<uint4>() + (uint64_t)c0 * (ccap + 1), ccap, n, cap,
+                                             c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), ccap, n, cap,
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
                                              c->d_rec_file.as<uint32_t>(), c->d_counters.as<uint32_t>());
     const uint32_t grid = (uint32_t)c->n_cu * 4;
@@ -2010,7 +1592,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     return GCK_OK;
 }
 
-static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs, bool hdr_from_arena = false) {
+static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
     if (!max_recs) return;
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
@@ -2022,7 +1604,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_xfw.as<uint32_t>(),
                                     c->d_zrow.as<uint32_t>(),
                                     c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
-                                    c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>(), hdr_from_arena ? 1u : 0u);
+                                    c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
 }
 
 static int ensure_records(Ctx *c, uint64_t nr) {
@@ -2111,20 +1693,12 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipStreamSynchronize(s));
     // rare: inconsistencies left after the device rounds (cascading mis-speculation)
     for (uint32_t left = hcnt[CNT_VAL + kRounds]; left;) {
-        k_fixup<<<nblk(nc, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
-                                              c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-                                              c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
-                                              c->d_ch_bad.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
-                                              c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
-                                              c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                              c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(),
-                                              c->opts.chunk_cap, 0u, nc, cnt + CNT_FIXUP);
+        launch_fixup(c, s, 0u, nc);
         GCK_HIP(hipMemsetAsync(cnt + CNT_HOSTVAL, 0, 4, s));
-        k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
-                                                 c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                 c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-                                                 c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
-                                                 cnt + CNT_HOSTVAL, 0u, nc);
+        k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
+                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
+                                                 c->d_ch_term.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
+                                                 c->d_ch_bad.as<uint32_t>(), cnt + CNT_HOSTVAL, 0u, nc);
         uint32_t v = 0;
         GCK_HIP(hipMemcpyAsync(&v, cnt + CNT_HOSTVAL, 4, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipStreamSynchronize(s));
@@ -2238,114 +1812,12 @@ static int ctx_run_device(Ctx *c) {
     return c->status;
 }
 
-// GCK_OPT_FUSED (experimental): speculation, then k_fuse (boundaries + CRC in
-// one streaming pass), validation rounds that stream the fixed chunks again,
-// scans, accounting, k_compact_fused, finalize.  Stage overflow or unsettled
-// speculation: redone on the host path.
-static int ctx_run_fused(Ctx *c) {
-    const auto t0 = std::chrono::steady_clock::now();
-    GCK_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint32_t nc = c->n_chunks, nf = c->nfiles, ccap = c->opts.chunk_cap;
-    const uint64_t cap = c->rec_cap;
-    int rc;
-    if ((rc = c->d_fep.ensure((uint64_t)(nc + 1) * (ccap + 2) * 8)) || (rc = c->d_redo.ensure((nc + 2) * 4)) ||
-        (rc = c->d_flist.ensure((nc + 2) * 4)))
-        return rc;
-    uint32_t *redo = c->d_redo.as<uint32_t>(), *list_n = redo + nc, *list = c->d_flist.as<uint32_t>();
-    uint32_t *cnt = c->d_counters.as<uint32_t>();
-    uint64_t *gbase = c->d_gbase.as<uint64_t>();
-    uint64_t *res = c->d_counters.as<uint64_t>() + 8;
-    uint32_t *queue = c->d_queue.as<uint32_t>();
-    k_run_init<<<1, 64, 0, s>>>(cnt, gbase, c->d_row_first.as<uint32_t>(), queue);
-    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
-    k_spec_entry<<<nblk(nc, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-                                             c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
-                                             c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(), nc,
-                                             c->opts.max_key);
-    // phases of this path: boundary = speculation, crc = the fused pass with
-    // its validation rounds, final = scans, accounting, record table, finalize
-    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
-    GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
-    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nc, (uint64_t)c->n_cu);
-    auto fuse = [&](bool listed) {  // all chunks, or the listed ones on a few workgroups
-        k_fuse<2><<<listed ? std::min<uint32_t>(grid, 16u) : grid, 1024, 0, s>>>(
-            c->arena.as<uint8_t>(), c->n_rows, c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-            c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(), c->d_ch_end.as<uint64_t>(),
-            c->d_ch_entry.as<uint64_t>(), c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(),
-            listed ? list : nullptr, list_n, nc,
-            c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-            c->d_ch_tpos.as<uint64_t>(), c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(),
-            c->d_fep.as<uint2>(), ccap, c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_rend.as<uint32_t>(),
-            queue, cnt);
-    };
-    fuse(false);
-    for (int r = 0; r <= kRounds; ++r) {
-        k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_start.as<uint64_t>(),
-                                                c->d_ch_end.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(),
-                                                c->d_ch_exit.as<uint64_t>(), c->d_ch_term.as<uint32_t>(),
-                                                c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
-                                                cnt + CNT_VAL + r, 0, nc);
-        if (r == kRounds) break;
-        GCK_HIP(hipMemsetAsync(redo, 0, (uint64_t)(nc + 1) * 4, s));  // flags and the list count
-        k_fuse_fix<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
-                                                 c->d_ffirst.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
-                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
-                                                 c->d_ch_term.as<uint32_t>(), redo, list, list_n, nc,
-                                                 cnt + CNT_FIXUP);
-        GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-        fuse(true);
-    }
-    GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
-    launch_scan(c, s, 0, nc, 0, nf, gbase, cap);
-    k_account<<<1, 1, 0, s>>>(nf, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(), c->d_fterm.as<uint32_t>(),
-                              c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
-                              c->d_carry.as<uint32_t>(), gbase, cap, res);
-    k_compact_fused<<<nblk(nc, 4), 256, 0, s>>>(
-        c->d_fbase.as<uint64_t>(), c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
-        c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), c->d_ffirst.as<uint32_t>(),
-        c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), c->d_fep.as<uint2>(), ccap,
-        (uint32_t)__builtin_ctz(c->opts.chunk_bytes), nc, cap, c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
-        c->d_rec_file.as<uint32_t>(), c->d_ep.as<uint2>());
-    launch_finalize(c, s, gbase, cap, true);
-    GCK_HIP(hipEventRecord(c->ev[PH_END], s));
-    uint32_t h[32] = {};
-    GCK_HIP(hipMemcpyAsync(h, cnt, 128, hipMemcpyDeviceToHost, s));
-    GCK_HIP(hipStreamSynchronize(s));
-    GCK_HIP(hipGetLastError());
-    const uint64_t *hr = reinterpret_cast<const uint64_t *>(h + 16);
-    if (h[CNT_VAL + kRounds] != 0 || h[CNT_CAP] != 0 || h[CNT_STAGE] != 0 || hr[5] > cap) return GCK_ERERUN;
-    c->status = (int32_t)hr[0];
-    c->err_file = (uint32_t)hr[1];
-    c->err_off = hr[2];
-    c->files_walked = (uint32_t)hr[3];
-    c->final_last_offset = (uint32_t)hr[4];
-    c->n_recs = hr[5];
-    c->n_fixups = h[CNT_FIXUP];
-    c->n_overflow = 0;
-    c->n_crc_fail = h[CNT_REJECT];
-    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
-    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
-        c->ms_phase[p] = ms;
-    }
-    float span = 0;
-    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
-    c->ms_phase[PH_PIPE] = span;
-    c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    c->device_path = true;
-    return c->status;
-}
-
 static int ctx_run(Ctx *c) {
     c->n_live = 0;  // the keydir (and its pack) belong to the previous run
     c->kd_nparts = 0;
     c->kd_valid = false;
     if (c->rec_cap > 0 && c->nfiles > 0) {
-        const int rc = (c->opts.flags & GCK_OPT_FUSED) ? ctx_run_fused(c) : ctx_run_device(c);
+        const int rc = ctx_run_device(c);
         if (rc != GCK_ERERUN) return rc;
         ++c->n_reruns;
     }
@@ -2523,6 +1995,72 @@ int gck_device_count(void) {
 const char *gck_version(void) { return "gocask_hip 0.1 (gfx950)"; }
 
 const char *gck_last_error(void) { return gck::last_error(); }
+
+// Diagnostic: the speculative entry of every chunk (k_spec_entry again, into
+// a scratch array) next to the final entry of the last run, both copied to
+// host arrays of n_chunks; *n = chunks.
+int gck_diag_spec_entries(gck_ctx *ctx, uint64_t *spec, uint64_t *final_, uint64_t cap, uint64_t *n) {
+    if (!ctx || !n) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    *n = c->n_chunks;
+    if (!spec || !final_ || cap < c->n_chunks) return GCK_EINVAL;
+    if (!c->n_chunks) return GCK_OK;
+    GCK_HIP(hipSetDevice(c->device));
+    DBuf tmp;
+    if (tmp.ensure((uint64_t)c->n_chunks * 8)) return GCK_ENOMEM;
+    k_spec_entry<<<nblk(c->n_chunks, 4), 256, 0, c->stream>>>(
+        c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
+        c->d_ch_start.as<uint64_t>(), c->d_ch_end.as<uint64_t>(), tmp.as<uint64_t>(), c->n_chunks, c->opts.max_key,
+        c->opts.spec_window);
+    GCK_HIP(hipMemcpyAsync(spec, tmp.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost, c->stream));
+    GCK_HIP(hipMemcpyAsync(final_, c->d_ch_entry.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost, c->stream));
+    GCK_HIP(hipStreamSynchronize(c->stream));
+    tmp.release();
+    return GCK_OK;
+}
+
+// Measurement helper: time k_walk variants (k_walk_xp MODE) on the chunk
+// entries of the last run; the stage is clobbered (rerun before fetching).
+int gck_diag_walk_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
+    if (!ctx || iters <= 0 || mode < 0 || mode > 7) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    if (!c->n_chunks) return GCK_EINVAL;
+    GCK_HIP(hipSetDevice(c->device));
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    const uint32_t nc = c->n_chunks;
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) {
+#define GCK_WALK_XP(M)                                                                                             \
+    case M:                                                                                                        \
+        k_walk_xp<M><<<nblk(nc, 256), 256, 0, c->stream>>>(                                                        \
+            c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(), \
+            c->d_ch_entry.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(), c->d_ch_count.as<uint32_t>(),              \
+            c->d_ch_exit.as<uint64_t>(), c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(),          \
+            c->opts.chunk_cap, nc);                                                                                \
+        break;
+        switch (mode) {
+            GCK_WALK_XP(0)
+            GCK_WALK_XP(1)
+            GCK_WALK_XP(2)
+            GCK_WALK_XP(3)
+            GCK_WALK_XP(4)
+            GCK_WALK_XP(5)
+            GCK_WALK_XP(6)
+            GCK_WALK_XP(7)
+        }
+#undef GCK_WALK_XP
+    }
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms_per_iter = ms / iters;
+    return GCK_OK;
+}
 
 // Measurement helper: time ablated variants of k_crc_rows on the state left by
 // the last gck_ctx_run (outputs are clobbered; rerun before fetching).

@@ -75,19 +75,18 @@ typedef struct gck_rec {
     uint32_t crc_calc;   /* CRC-32/IEEE of the record's last ValueSize bytes               */
 } gck_rec;
 
+/* Tuning knobs; zero fields take the defaults.  Results never depend on them. */
 typedef struct gck_opts {
     int32_t device;        /* HIP device ordinal (default 0)                               */
-    uint32_t chunk_bytes;  /* boundary-speculation chunk (0: 512 KiB, 256 KiB fused; pow2) */
+    uint32_t chunk_bytes;  /* boundary-speculation chunk (pow2 >= 4 KiB; default 512 KiB)  */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
-    uint32_t chunk_cap;    /* records staged per chunk before re-walk (default 256)       */
-    uint32_t flags;        /* GCK_OPT_*                                                     */
+    uint32_t chunk_cap;    /* records staged per chunk before a re-walk (default 1024)    */
+    uint32_t flags;        /* reserved, 0                                                  */
+    uint32_t spec_window;  /* bytes from a chunk's start searched for its first record    */
+                           /* (rounded up to 4 KiB; default 0 = the whole chunk).  A      */
+                           /* chunk whose first record lies further in is covered by the  */
+                           /* walk of the chunk before it.                                 */
 } gck_opts;
-
-
-/* Experimental: boundary discovery fused into the streaming CRC pass (one
- * wavefront per chunk follows the header chain through the words it streams);
- * results are identical, runs it cannot settle are redone on the standard path. */
-#define GCK_OPT_FUSED 1u
 
 typedef struct gck_result {
     gck_rec *recs;              /* library-owned pinned host array; free with gck_result_free */
@@ -218,6 +217,14 @@ int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per
  * state (mode bits 1 = no record intervals, 2 = no LDS table chain, 4 = no
  * tail shift / segmented scan).  Clobbers the last run's outputs. */
 int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter);
+/* Measurement helper: time variants of the chain walk on the last run's chunk
+ * entries (mode bits 1 = header in two loads, 2 = 8-byte stage, 4 = no stage
+ * stores).  Clobbers the last run's stage. */
+int gck_diag_walk_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter);
+/* Diagnostic: every chunk's speculative entry (recomputed) and its final entry
+ * after validation in the last run (host arrays of cap >= chunks; *n = chunks;
+ * UINT64_MAX = none). */
+int gck_diag_spec_entries(gck_ctx *ctx, uint64_t *spec, uint64_t *final_, uint64_t cap, uint64_t *n);
 /* Copy `len` bytes of file `file` (as resident in the arena) back to host. */
 int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, uint64_t len);
 

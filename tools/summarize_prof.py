@@ -66,16 +66,7 @@ def main():
         "algorithmic_bytes_per_launch": (bench["config"]["bytes_per_gpu"] / bench["roofline"].get("launches_per_step", 1))
         if bench else None,
     }
-    fuse_key = next((k for k in summary if k.startswith("k_fuse<")), None)
-    if crc_key is None and fuse_key is not None:
-        # a fused-path run: its own traffic file (the default path's stays)
-        fz = pmc[fuse_key]  # the full launches: the largest dispatches (listed re-streams are small)
-        out["kernel"] = "k_fuse"
-        out["fuse_hbm_bytes_per_launch"] = max(fz.get("FETCH_SIZE", [0])) * 2048 or None
-        out["fuse_write_bytes_per_launch"] = max(fz.get("WRITE_SIZE", [0])) * 1024 or None
-        json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}_fused.json"), "w"), indent=1)
-    else:
-        json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"traffic_{cfg}.json"), "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
