@@ -80,14 +80,14 @@ struct Ctx {
     DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
     DBuf d_ch_wend;              // where each chunk's walk stopped (its bound, walk_bound)
     uint32_t chunk_shift = 17;   // log2(opts.chunk_bytes)
-    DBuf d_rec_base, d_bsum, d_scratch_off, d_scratch_hdr, d_counters;
+    DBuf d_rec_base, d_bsum, d_stage, d_counters;  // d_stage: (KeySize, ValueSize) per walked record (stage_slot)
     DBuf d_freset;                   // per file: 1 = lastOffset resets after it
     DBuf d_gbase;                    // record range of the run [0, n)
 
     // records
     uint64_t n_recs = 0;
     uint64_t rec_cap = 0;  // record-table capacity of the current run
-    DBuf d_rec_off, d_rec_hdr, d_rec_file, d_ep, d_out;
+    DBuf d_rec_off, d_rec_kv, d_rec_file, d_ep, d_out;  // record table: arena offset, (KeySize, ValueSize), file
     // rows
     uint64_t n_rows = 0;
     DBuf d_row_first, d_rend, d_plan, d_queue;

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
                                                     const unsigned long long *__restrict__ table, uint64_t slots,
                                                     const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ rec_off,
-                                                    const uint4 *__restrict__ rec_hdr,
+                                                    const uint2 *__restrict__ rec_kv,
                                                     const gck_rec *__restrict__ recs,
                                                     const uint64_t *__restrict__ fbase,
                                                     const uint64_t *__restrict__ flen, int32_t *__restrict__ status,
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
                 const unsigned long long v = table[s];
                 if (v == kEmptySlot) break;
                 const uint32_t cur = (uint32_t)v;
-                if ((uint32_t)(v >> 32) != tag || key_len(rec_hdr[cur]) != len) continue;
+                if ((uint32_t)(v >> 32) != tag || key_len(rec_kv[cur]) != len) continue;
                 const KeyWords a(arena, rec_off[cur] + 16, len);
                 bool same = true;
                 for (uint32_t i = 0; same && 4 * i < len; ++i) same = a[i] == k[i];
@@ -320,7 +320,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     GCK_HIP(hipMemcpyAsync(c->d_gkoff.p, key_off, (n + 1) * 8ull, hipMemcpyHostToDevice, s));
     k_get_lookup<<<(n + 255) / 256, 256, 0, s>>>(
         c->d_gkeys.as<uint8_t>(), c->d_gkoff.as<uint64_t>(), n, c->d_ktab.as<unsigned long long>(), c->kd_slots,
-        c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+        c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
         c->d_out.as<gck_rec>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
         c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>());
     uint8_t *dvals = nullptr;

@@ -10,7 +10,7 @@ constexpr int kKdTile = 1024;  // records per compaction tile (one workgroup)
 
 // Key of a record: KeySize bytes after the header, or ValueSize bytes for a
 // tombstone (KeySize 0; core/db.go:151-155).
-__device__ __forceinline__ uint32_t key_len(const uint4 &h) { return h.z ? h.z : h.w; }
+__device__ __forceinline__ uint32_t key_len(const uint2 &kv) { return kv.x ? kv.x : kv.y; }  // (KeySize, ValueSize)
 
 __device__ __forceinline__ uint64_t mix64d(uint64_t x) {
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

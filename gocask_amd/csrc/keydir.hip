@@ -28,11 +28,11 @@ __device__ bool same_key(const uint8_t *__restrict__ arena, const uint64_t *__re
 // removed, so a probe sequence never skips a key's slot.
 __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ arena,
                                                    const uint64_t *__restrict__ rec_off,
-                                                   const uint4 *__restrict__ rec_hdr, uint64_t n,
+                                                   const uint2 *__restrict__ rec_kv, uint64_t n,
                                                    uint64_t *__restrict__ khash,
                                                    unsigned long long *__restrict__ table, uint64_t mask) {
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t len = key_len(rec_hdr[r]);
+        const uint32_t len = key_len(rec_kv[r]);
         const uint64_t h = key_hash(KeyWords(arena, rec_off[r] + 16, len), len);
         khash[r] = h;
         const uint32_t tag = slot_tag(h);
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
             }
             if ((uint32_t)(cur >> 32) != tag) continue;
             const uint32_t ci = (uint32_t)cur;
-            if (key_len(rec_hdr[ci]) == len && same_key(arena, rec_off, ci, r, len)) {
+            if (key_len(rec_kv[ci]) == len && same_key(arena, rec_off, ci, r, len)) {
                 if (ci < r) atomicMax(table + s, mine);  // same key: the later record wins
                 break;
             }
@@ -61,13 +61,13 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
 // Put (or, for a merge across shards, always: tombstones then stay as delete
 // markers).
 __global__ __launch_bounds__(256) void k_kd_mark(const unsigned long long *__restrict__ table, uint64_t slots,
-                                                 const uint4 *__restrict__ rec_hdr, uint32_t keep_tombstones,
+                                                 const uint2 *__restrict__ rec_kv, uint32_t keep_tombstones,
                                                  uint32_t *__restrict__ live) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long v = table[s];
         if (v == kEmptySlot) continue;
         const uint32_t r = (uint32_t)v;
-        if (keep_tombstones || rec_hdr[r].z != 0) live[r] = 1;
+        if (keep_tombstones || rec_kv[r].x != 0) live[r] = 1;
     }
 }
 
@@ -360,9 +360,9 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8, s));
     GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
     const uint32_t grid = (uint32_t)c->n_cu * 8;
-    k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), n,
+    k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), n,
                                      c->d_khash.as<uint64_t>(), c->d_ktab.as<unsigned long long>(), slots - 1);
-    k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_hdr.as<uint4>(),
+    k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_kv.as<uint2>(),
                                    (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>());
     k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
     k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);

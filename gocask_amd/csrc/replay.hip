@@ -315,21 +315,17 @@ __host__ __device__ __forceinline__ uint64_t stage_slot(uint32_t c, uint32_t i, 
     return ((uint64_t)(c / kStageIl) * (cap + 1) + (i < cap ? i : cap)) * kStageIl + (c % kStageIl);
 }
 // Every hop stores, so the number of stores per hop is fixed and the next
-// header's load wait counts them.
+// header's load wait counts them.  A slot holds (KeySize, ValueSize): the
+// record offsets follow from the chunk's entry and the entry sizes (a scan in
+// k_compact), CRC and Timestamp from the header bytes (k_finalize reads them).
 struct ScratchEmit {
-    uint64_t *off;  // the chunk's slot 0 (stride kStageIl elements)
-    uint4 *hdr;
+    uint2 *kv;  // the chunk's slot 0 (stride kStageIl elements)
     uint32_t cap;
-    __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
-        const uint64_t k = (uint64_t)(i < cap ? i : cap) * kStageIl;
-        off[k] = p;
-        hdr[k] = make_uint4(h.crc, h.ts, h.ks, h.vs);
+    __device__ void operator()(uint32_t i, uint64_t, const Hdr &h) const {
+        kv[(uint64_t)(i < cap ? i : cap) * kStageIl] = make_uint2(h.ks, h.vs);
     }
-    // the stores of one hop, to the scratch slot
-    __device__ void prime() const {
-        off[(uint64_t)cap * kStageIl] = 0;
-        hdr[(uint64_t)cap * kStageIl] = make_uint4(0, 0, 0, 0);
-    }
+    // the store of one hop, to the scratch slot
+    __device__ void prime() const { kv[(uint64_t)cap * kStageIl] = make_uint2(0, 0); }
 };
 
 // Where the walk of chunk c stops: the start of the next chunk of its file
@@ -353,12 +349,12 @@ __device__ uint64_t walk_bound(const uint64_t *__restrict__ ch_entry, const uint
 
 __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_t *fbase,
                                 const uint64_t *flen, uint32_t c, uint32_t f, uint64_t ce, uint64_t entry,
-                                uint32_t cap, uint64_t *s_off, uint4 *s_hdr, uint32_t *ch_count,
+                                uint32_t cap, uint2 *s_kv, uint32_t *ch_count,
                                 uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *ch_wend) {
     uint32_t count = 0, term = T_NONE;
     uint64_t exit = kNone, tpos = 0;
     if (entry != kNone) {
-        ScratchEmit em{s_off + stage_slot(c, 0, cap), s_hdr + stage_slot(c, 0, cap), cap};
+        ScratchEmit em{s_kv + stage_slot(c, 0, cap), cap};
         walk_chain(arena, fbase[f], flen[f], ce, entry, em, count, exit, term, tpos);
     }
     ch_count[c] = count;
@@ -378,14 +374,14 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint32_t *__restrict__ f_nchunks,
                                               const uint64_t *__restrict__ ch_entry, uint32_t *ch_count,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
-                                              uint64_t *ch_wend, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
+                                              uint64_t *ch_wend, uint2 *s_kv, uint32_t cap,
                                               uint32_t chunk_shift, uint32_t n_chunks) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
     const uint32_t f = ch_file[c];
     const uint64_t entry = ch_entry[c];
     const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
-    walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_off, s_hdr, ch_count, ch_exit, ch_term, ch_tpos,
+    walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
                     ch_wend);
 }
 
@@ -434,7 +430,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                                                const uint32_t *__restrict__ f_nchunks,
                                                const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
                                                uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
-                                               uint64_t *ch_tpos, uint64_t *ch_wend, uint64_t *s_off, uint4 *s_hdr,
+                                               uint64_t *ch_tpos, uint64_t *ch_wend, uint2 *s_kv,
                                                uint32_t cap, uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end,
                                                uint32_t *counter) {
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
@@ -451,7 +447,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
     ch_entry[c] = e_new;
     atomicAdd(counter, 1u);
     const uint64_t ce = e_new != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
-    walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_off, s_hdr, ch_count, ch_exit, ch_term, ch_tpos,
+    walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
                     ch_wend);
 }
 
@@ -599,7 +595,7 @@ __global__ void k_account(uint32_t nf, const uint64_t *__restrict__ flen, const 
 
 struct DirectEmit {
     uint64_t *rec_off;
-    uint4 *rec_hdr;
+    uint2 *rec_kv;
     uint32_t *rec_file;
     uint64_t rb, n_total, base;
     uint32_t f;
@@ -607,7 +603,7 @@ struct DirectEmit {
         const uint64_t r = rb + i;
         if (r < n_total) {
             rec_off[r] = base + p;
-            rec_hdr[r] = make_uint4(h.crc, h.ts, h.ks, h.vs);
+            rec_kv[r] = make_uint2(h.ks, h.vs);
             rec_file[r] = f;
         }
     }
@@ -615,9 +611,11 @@ struct DirectEmit {
 };
 
 // Record table in walk order: one wavefront per chunk copies its staged
-// headers; chunks that overflowed the stage re-walk straight into the table.
-// A workgroup takes 16 consecutive chunks, so the stage lines it reads (slot
-// i of kStageIl consecutive chunks, stage_slot) are fetched once per CU.
+// (KeySize, ValueSize) pairs and rebuilds the record offsets from the chunk's
+// entry by a scan of the entry sizes; chunks that overflowed the stage re-walk
+// straight into the table.  A workgroup takes 16 consecutive chunks, so the
+// stage lines it reads (slot i of kStageIl consecutive chunks, stage_slot)
+// are fetched once per CU.
 __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint64_t *__restrict__ flen,
@@ -626,10 +624,9 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   const uint64_t *__restrict__ ch_entry,
                                                   const uint32_t *__restrict__ ch_count,
                                                   const uint64_t *__restrict__ rec_base,
-                                                  const uint64_t *__restrict__ s_off,
-                                                  const uint4 *__restrict__ s_hdr, uint32_t cap,
+                                                  const uint2 *__restrict__ s_kv, uint32_t cap,
                                                   uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
-                                                  uint4 *rec_hdr, uint32_t *rec_file, uint32_t *counters) {
+                                                  uint2 *rec_kv, uint32_t *rec_file, uint32_t *counters) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
     if (c >= n_chunks) return;
@@ -640,26 +637,36 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
     const uint32_t f = ch_file[c];
     const uint64_t base = fbase[f];
     if (cnt <= cap) {
-        for (uint32_t i = lane; i < cnt; i += 64) {
+        uint64_t run = base + entry;  // arena offset of the next record
+        for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool in = i < cnt;
+            const uint2 kv = in ? s_kv[stage_slot(c, i, cap)] : make_uint2(0u, 0u);
+            // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
+            // inclusive scan is exact in 24-bit halves (entries < 2^33)
+            const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
+            const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
             const uint64_t r = rb + i;
-            if (r >= n_total) break;
-            const uint64_t si = stage_slot(c, i, cap);
-            rec_off[r] = base + s_off[si];
-            rec_hdr[r] = s_hdr[si];
-            rec_file[r] = f;
+            if (in && r < n_total) {
+                rec_off[r] = run + (((uint64_t)hi << 24) + lo) - e;
+                rec_kv[r] = kv;
+                rec_file[r] = f;
+            }
+            run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
+                   (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
         }
     } else if (lane == 0) {
         atomicAdd(&counters[2], 1u);
-        DirectEmit em{rec_off, rec_hdr, rec_file, rb, n_total, base, f};
+        DirectEmit em{rec_off, rec_kv, rec_file, rb, n_total, base, f};
         uint32_t count, term;
         uint64_t exit, tpos;
         walk_chain(arena, base, flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
     }
 }
 
-__device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uint4 *rec_hdr, uint64_t r) {
-    const uint4 h = rec_hdr[r];
-    return rec_off[r] + 16 + (uint64_t)h.z + h.w;  // tombstone: KeySize 0, the key is the "value"
+__device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uint2 *rec_kv, uint64_t r) {
+    const uint2 kv = rec_kv[r];
+    return rec_off[r] + 16 + (uint64_t)kv.x + kv.y;  // tombstone: KeySize 0, the key is the "value"
 }
 
 // Record range [rng[0], rng[1]) of the run (device-resident).
@@ -676,13 +683,13 @@ __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64
         row_first[row] = v;
 }
 
-__global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint4 *__restrict__ rec_hdr,
+__global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint2 *__restrict__ rec_kv,
                             const uint64_t *__restrict__ rng, uint64_t r0, uint32_t *__restrict__ row_first) {
     const uint64_t rb = rng[0], re = rng[1];
     for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
          r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ve_r = value_end(rec_off, rec_hdr, r);
-        const uint64_t lo = r == rb ? r0 : (value_end(rec_off, rec_hdr, r - 1) + kRow - 1) / kRow;
+        const uint64_t ve_r = value_end(rec_off, rec_kv, r);
+        const uint64_t lo = r == rb ? r0 : (value_end(rec_off, rec_kv, r - 1) + kRow - 1) / kRow;
         const uint64_t hi = (ve_r + kRow - 1) / kRow;
         for (uint64_t row = lo; row < hi; ++row) row_first[row] = (uint32_t)r;
     }
@@ -715,7 +722,7 @@ constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the re
 constexpr int kPlanWaves = 4;
 
 __global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__restrict__ rec_off,
-                                                              const uint4 *__restrict__ rec_hdr,
+                                                              const uint2 *__restrict__ rec_kv,
                                                               uint64_t r0, uint64_t nr,
                                                               const uint32_t *__restrict__ row_first,
                                                               uint4 *__restrict__ plan) {
@@ -730,7 +737,7 @@ __global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__
     for (uint64_t b = lo; b < hi; b += 64) {
         const uint64_t r = b + lane;
         if (r < hi) {
-            const uint64_t last = value_end(rec_off, rec_hdr, r) - 1;  // the record's last byte
+            const uint64_t last = value_end(rec_off, rec_kv, r) - 1;  // the record's last byte
             const uint32_t rl = (uint32_t)(last / kRow - R0);          // 0..63
             const uint32_t o = (uint32_t)(last % kRow), slab = o / kSlab, blk = (o % kSlab) / kBlock;
             atomicOr(cw + slab * 9 + rl / 8, (1u << blk) << (4 * (rl % 8)));
@@ -1123,7 +1130,7 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, con
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
-                                                  const uint4 *__restrict__ rec_hdr,
+                                                  const uint2 *__restrict__ rec_kv,
                                                   const uint32_t *__restrict__ rec_file,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint32_t *__restrict__ carry, const uint64_t *__restrict__ rng,
@@ -1150,10 +1157,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const bool valid = r_ < re;
         const uint64_t r = valid ? r_ : re - 1;
         const uint64_t rs = rec_off[r];
-        const uint4 h = rec_hdr[r];
+        const uint2 kv = rec_kv[r];  // (KeySize, ValueSize)
         const uint32_t f = rec_file[r];
-        const uint32_t V = h.w;
-        const uint64_t vs = rs + 16 + h.z, ve = vs + V;
+        const uint32_t V = kv.y;
+        const uint64_t vs = rs + 16 + kv.x, ve = vs + V;
         // ft of the previous record (same file: its end is rs), from the 16 B
         // block holding byte rs - 1
         const bool prev_same = rs != fbase[f];
@@ -1206,7 +1213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         uint32_t pw[11];
 #pragma unroll
         for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
-        const uint32_t hcrc = h.x, hts = h.y;
+        const uint32_t hcrc = ab(pw[1], pw[0], lead), hts = ab(pw[2], pw[1], lead);  // header CRC, Timestamp
         pw[0] &= ~0u << (8 * lead);
         // unrolled over the words in registers (no indexed register array),
         // then the words of long keys from memory
@@ -1226,13 +1233,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint32_t calc = raw0 ^ z;
         if (valid) {
             const uint64_t fo = rs - fbase[f];
-            const bool tomb = h.z == 0;
+            const bool tomb = kv.x == 0;
             gck_rec o;
             o.rec_off = fo;
             o.file = f;
-            o.key_len = tomb ? h.w : h.z;
-            o.value_pos = carry[f] + (uint32_t)fo + 16u + h.z;
-            o.value_size = h.w;
+            o.key_len = tomb ? kv.y : kv.x;
+            o.value_pos = carry[f] + (uint32_t)fo + 16u + kv.x;
+            o.value_size = kv.y;
             o.crc = hcrc;
             o.ts = hts;
             o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == hcrc ? GCK_F_CRC_OK : 0u);
@@ -1253,14 +1260,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
 }
 
 // Measurement variants of k_walk (gck_diag_walk_variant): MODE bit 1 = header
-// by two loads (ld_hdr2), 2 = stage only (KeySize, ValueSize) (8 B a hop),
-// 4 = no stage stores.  Same chains, counts and exits as k_walk.
-struct Stage8Emit {
-    uint2 *kv;
-    uint32_t cap;
-    __device__ void operator()(uint32_t i, uint64_t, const Hdr &h) const { kv[i < cap ? i : cap] = make_uint2(h.ks, h.vs); }
-    __device__ void prime() const { kv[cap] = make_uint2(0, 0); }
-};
+// by two loads (ld_hdr2; the compiler already merges ld_hdr's), 4 = no stage
+// stores.  Same chains, counts and exits as k_walk.
 struct NoEmit {
     __device__ void operator()(uint32_t, uint64_t, const Hdr &) const {}
     __device__ void prime() const {}
@@ -1271,7 +1272,7 @@ __global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ are
                                                  const uint32_t *__restrict__ ch_file,
                                                  const uint64_t *__restrict__ ch_entry,
                                                  const uint64_t *__restrict__ ch_wend, uint32_t *ch_count,
-                                                 uint64_t *ch_exit, uint64_t *s_off, uint4 *s_hdr, uint32_t cap,
+                                                 uint64_t *ch_exit, uint2 *s_kv, uint32_t cap,
                                                  uint32_t n_chunks) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_chunks) return;
@@ -1283,11 +1284,8 @@ __global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ are
     constexpr bool H2 = (MODE & 1) != 0;
     if constexpr ((MODE & 4) != 0) {
         walk_chain<NoEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, NoEmit{}, count, exit, term, tpos);
-    } else if constexpr ((MODE & 2) != 0) {
-        Stage8Emit em{reinterpret_cast<uint2 *>(s_hdr) + stage_slot(c, 0, cap), cap};
-        walk_chain<Stage8Emit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
     } else {
-        ScratchEmit em{s_off + stage_slot(c, 0, cap), s_hdr + stage_slot(c, 0, cap), cap};
+        ScratchEmit em{s_kv + stage_slot(c, 0, cap), cap};
         walk_chain<ScratchEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
     }
     ch_count[c] = count;
@@ -1404,8 +1402,8 @@ static void ctx_free(Ctx *c) {
     DBuf *all[] = {&c->arena, &c->d_fbase, &c->d_flen, &c->d_ffirst, &c->d_fnch, &c->d_fbad, &c->d_fterm,
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
-                   &c->d_rec_base, &c->d_bsum, &c->d_scratch_off, &c->d_scratch_hdr, &c->d_counters, &c->d_rec_off,
-                   &c->d_rec_hdr, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
+                   &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
+                   &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
@@ -1469,8 +1467,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure(16)) || (rc = c->d_scratch_off.ensure((nc + 64) / 64 * 64 * (cap + 1) * 8)) ||
-        (rc = c->d_scratch_hdr.ensure((nc + 64) / 64 * 64 * (cap + 1) * 16)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure(16)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_plan.ensure((c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
         return rc;
@@ -1504,7 +1501,7 @@ static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1) {
         c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
         c->d_ch_entry.as<uint64_t>(), c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(),
-        c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
+        c->d_stage.as<uint2>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
         c->d_counters.as<uint32_t>() + CNT_FIXUP);
 }
 
@@ -1522,8 +1519,7 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
                                         c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
                                         c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
                                         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                        c->d_ch_wend.as<uint64_t>(), c->d_scratch_off.as<uint64_t>(),
-                                        c->d_scratch_hdr.as<uint4>(), cap, c->chunk_shift, c1);
+                                        c->d_ch_wend.as<uint64_t>(), c->d_stage.as<uint2>(), cap, c->chunk_shift, c1);
     for (int r = 0; r <= kRounds; ++r) {
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
@@ -1563,16 +1559,16 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
                                              c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
                                              c->d_rec_base.as<uint64_t>() + c0,
-                                             c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(), ccap, n, cap,
-                                             c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+                                             c->d_stage.as<uint2>(), ccap, n, cap,
+                                             c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                              c->d_rec_file.as<uint32_t>(), c->d_counters.as<uint32_t>());
     const uint32_t grid = (uint32_t)c->n_cu * 4;
     k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
-    k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), rng, r0,
+    k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), rng, r0,
                                      c->d_row_first.as<uint32_t>());
     if (r1 > r0)
         k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
-            c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
+            c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
             c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16);
 }
 
@@ -1598,7 +1594,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
     // round of workgroups would double the kernel's latency-bound time)
     const uint64_t want = nblk(max_recs, 256), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
     const uint32_t grid = (uint32_t)(want < res ? want : res);
-    k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_hdr.as<uint4>(),
+    k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_xfw.as<uint32_t>(),
@@ -1610,7 +1606,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
 static int ensure_records(Ctx *c, uint64_t nr) {
     nr = nr ? nr : 1;
     int rc;
-    if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_hdr.ensure(nr * 16)) ||
+    if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_kv.ensure(nr * 8)) ||
         (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_ep.ensure((nr + kEpScratch) * 8)) ||
         (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
         return rc;
@@ -2037,8 +2033,7 @@ int gck_diag_walk_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter
         k_walk_xp<M><<<nblk(nc, 256), 256, 0, c->stream>>>(                                                        \
             c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(), \
             c->d_ch_entry.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(), c->d_ch_count.as<uint32_t>(),              \
-            c->d_ch_exit.as<uint64_t>(), c->d_scratch_off.as<uint64_t>(), c->d_scratch_hdr.as<uint4>(),          \
-            c->opts.chunk_cap, nc);                                                                                \
+            c->d_ch_exit.as<uint64_t>(), c->d_stage.as<uint2>(), c->opts.chunk_cap, nc);                         \
         break;
         switch (mode) {
             GCK_WALK_XP(0)
