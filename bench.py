@@ -53,6 +53,30 @@ def _cpu_model():
     return None
 
 
+def usable_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU
+    quota (cpu.max) and by OMP_NUM_THREADS when set (the GPU box gives each
+    job a share of a larger machine).  Returns (usable, dict of the sources)."""
+    src = {"nproc": os.cpu_count() or 1}
+    try:
+        src["affinity"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        src["affinity"] = src["nproc"]
+    n = src["affinity"]
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            src["cgroup_quota"] = max(1, int(int(quota) / int(period)))
+            n = min(n, src["cgroup_quota"])
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        src["omp_num_threads"] = int(omp)
+        n = min(n, int(omp))
+    return max(1, n), src
+
+
 def _timed(fn, min_s=4.0):
     reps, t = 0, 0.0
     while t < min_s or reps < 1:
@@ -63,14 +87,17 @@ def _timed(fn, min_s=4.0):
     return out, reps, t
 
 
-def cpu_baseline(cfg_name, sample_bytes, max_threads=16, min_s=4.0, mt_file_bytes=256 << 20):
+def cpu_baseline(cfg_name, sample_bytes, min_s=4.0, mt_file_bytes=256 << 20):
     """Oracle (C port of the reference replay) on host cores, on bounded samples
     of the same workload (SURVEY.md §8d's three variants):
       ref_faithful  1 thread: header decode, every byte through a 4 KiB buffer (bufio), key,
                     hash-map keydir, no CRC (core/db.go:125-178);
       ref_crc       1 thread: the same plus the CRC verdict per record (the primary value);
-      all_cores     one thread per file (up to max_threads, the box's CPU share), + CRC,
-                    a keydir per file (no cross-file merge)."""
+      all_cores     one thread per file on every usable CPU (usable_cpus()), + CRC,
+                    a keydir per file (no cross-file merge).
+    The oracle is a C port: Go's reflective binary.Read and per-record
+    allocations (core/db.go:145-178) are not in it, so ref_faithful likely
+    overstates the Go reference's speed (kind "port")."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from concurrent.futures import ThreadPoolExecutor
@@ -89,8 +116,8 @@ def cpu_baseline(cfg_name, sample_bytes, max_threads=16, min_s=4.0, mt_file_byte
                           sample=what + ", bytes through a 4 KiB buffer, no CRC (the reference's replay)"),
         ref_crc=dict(value=round(nbytes * reps / t / GiB, 3), cores=1, sample=what + ", + CRC verdict"),
     )
-    nproc = os.cpu_count() or 1
-    nt = max(1, min(nproc, max_threads, 16))
+    nt, cpus = usable_cpus()
+    nproc = cpus["nproc"]
     kw_mt = dict(CONFIGS[cfg_name])
     kw_mt["n_files"] = nt
     kw_mt["max_file_size"] = min(kw_mt["max_file_size"], mt_file_bytes)
@@ -105,7 +132,7 @@ def cpu_baseline(cfg_name, sample_bytes, max_threads=16, min_s=4.0, mt_file_byte
                                         f"one thread per file, + CRC verdict, a keydir per file")
     return dict(value=variants["ref_crc"]["value"], unit="GiB/s", cores=1, kind="port",
                 sample=what + f", single-thread oracle replay + CRC verdict + hash-map keydir, {reps} pass(es)",
-                variants=variants, nproc=nproc, cpu_model=_cpu_model())
+                variants=variants, nproc=nproc, usable_cpus=nt, cpu_sources=cpus, cpu_model=_cpu_model())
 
 
 def host_inclusive(g, ctx, info, steps):

@@ -393,6 +393,7 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
     for (uint64_t i = 0; i < n; ++i) {
         if (ko[i + 1] < ko[i] || vo[i + 1] < vo[i]) return GCK_EINVAL;
         const uint64_t kl = ko[i + 1] - ko[i], vl = tb[i] ? 0 : vo[i + 1] - vo[i];
+        if (kl == 0) return GCK_EINVALID_KEY;  // Put / Delete of an empty key (core/db.go:186, :294)
         if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) return GCK_EINVAL;  // u32 header fields
         off[i + 1] = off[i] + 16 + kl + vl;
     }

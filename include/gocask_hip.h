@@ -264,7 +264,9 @@ void gck_encode_zipf_table(uint32_t *thr);
  * in order.  keys/vals are concatenated bytes with n+1 offsets
  * (key_off/val_off); every pointer except total is DEVICE memory; out_off
  * (n+1) receives each record's offset in out; *total = bytes written (or
- * needed: GCK_EINVAL with nothing written when out_cap < *total).  stream:
+ * needed: GCK_EINVAL with nothing written when out_cap < *total; GCK_EINVALID_KEY
+ * and nothing written when a key is empty, as DB.Put / DB.Delete refuse it,
+ * core/db.go:186-188, :294-297).  stream:
  * a hipStream_t, NULL for the default stream; returns after the bytes are
  * written. */
 int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint8_t *vals,

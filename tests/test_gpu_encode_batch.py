@@ -45,10 +45,21 @@ def test_encode_batch_empty_and_zero_length():
 
     out, off = core.encode_batch([])
     assert out.numel() == 0 and off.cpu().numpy().tolist() == [0]
-    ops = [(5, b"k", b""), (6, b"", b"v"), (7, b"gone", None), (2**32 + 9, b"x" * 64, b"y" * 4096),
-           (8, bytes(range(256)) * 20, None), (9, b"q" * 3000, bytes(range(7)) * 300), (10, b"", b"")]
+    ops = [(5, b"k", b""), (7, b"gone", None), (2**32 + 9, b"x" * 64, b"y" * 4096),
+           (8, bytes(range(256)) * 20, None), (9, b"q" * 3000, bytes(range(7)) * 300), (10, b"z", b"")]
     out, _ = core.encode_batch(ops)
     assert bytes(out.cpu().numpy()) == _expected(ops)
+
+
+@pytest.mark.parametrize("bad", [(6, b"", b"v"), (6, b"", b""), (6, b"", None)])
+def test_encode_batch_rejects_empty_key(bad):
+    # DB.Put and DB.Delete reject an empty key with ErrInvalidKey
+    # (core/db.go:186-188; Delete through get, :238-241, :294-297)
+    from gocask_amd import _lib, core
+
+    with pytest.raises(_lib.GckError) as e:
+        core.encode_batch([(1, b"a", b"b"), bad])
+    assert e.value.code == _lib.GCK_EINVALID_KEY
 
 
 def test_encode_batch_replays():
