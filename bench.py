@@ -87,7 +87,7 @@ def _timed(fn, min_s=4.0):
     return out, reps, t
 
 
-def cpu_baseline(cfg_name, sample_bytes, min_s=4.0, mt_file_bytes=256 << 20):
+def cpu_baseline(cfg_name, sample_bytes, max_threads=None, min_s=4.0, mt_file_bytes=256 << 20):
     """Oracle (C port of the reference replay) on host cores, on bounded samples
     of the same workload (SURVEY.md §8d's three variants):
       ref_faithful  1 thread: header decode, every byte through a 4 KiB buffer (bufio), key,
@@ -117,6 +117,7 @@ def cpu_baseline(cfg_name, sample_bytes, min_s=4.0, mt_file_bytes=256 << 20):
         ref_crc=dict(value=round(nbytes * reps / t / GiB, 3), cores=1, sample=what + ", + CRC verdict"),
     )
     nt, cpus = usable_cpus()
+    nt = min(nt, max_threads) if max_threads else nt  # (tests: a small sample)
     nproc = cpus["nproc"]
     kw_mt = dict(CONFIGS[cfg_name])
     kw_mt["n_files"] = nt
