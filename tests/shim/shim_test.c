@@ -1,0 +1,205 @@
+/*
+ * shim_test.c — TEST PROGRAM.  Does in C exactly what the cgo shim of
+ * INTEGRATION.md §2 does inside core.NewDB, so the calling pattern a Go
+ * maintainer would ship is exercised against the real library:
+ *
+ *   1. walk the db directory like Disk.Walk (internal/fs/disk.go:122-145):
+ *      filepath.Walk order (names sorted bytewise, recursive, Lstat), only
+ *      *.csk; each file is opened read-only, and INSIDE the walk callback,
+ *      while it is open, stat'ed, mmap'ed read-only and page-locked
+ *      (gck_host_register) -- Disk.Walk closes it when the callback returns
+ *      (disk.go:143), the mapping stays valid;
+ *   2. reset_after = Name() != activeFile.Name() (core/db.go:117);
+ *   3. no .csk file at all: nothing to replay, an empty keydir (the shim
+ *      must not index files[0]);
+ *   4. gck_replay through include/gocask_hip.h;
+ *   5. apply the records in walk order to a map (keyDir.set / unset,
+ *      core/keydir.go:22-49) and lastOffset = final_last_offset.
+ *
+ * Usage: shim_test <db dir> [active Name()]   (default: Disk.Open's choice,
+ * the lexically last directory entry without its extension).
+ * Prints "status <rc> last_offset <n> keys <n>" then one line per live key:
+ * "<key hex> <crc> <ts> <value_pos> <value_size> <file Name()>", sorted.
+ */
+#define _GNU_SOURCE
+#include <dirent.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include "gocask_hip.h"
+
+typedef struct {
+    char name[256]; /* DiskFile.Name(): base name without the extension */
+    const uint8_t *map;
+    uint64_t len;
+} mapped;
+
+static mapped *g_files;
+static size_t g_n, g_cap;
+
+static int cmp_str(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
+
+static const char *ext_of(const char *p) {
+    const char *d = strrchr(p, '.'), *s = strrchr(p, '/');
+    return d && (!s || d > s) ? d : "";
+}
+
+/* The Walk callback: the file is open here and only here. */
+static int on_file(const char *path) {
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return -1;
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        return -1;
+    }
+    if (g_n == g_cap) {
+        g_cap = g_cap ? 2 * g_cap : 16;
+        g_files = realloc(g_files, g_cap * sizeof(mapped));
+    }
+    mapped *m = &g_files[g_n++];
+    memset(m, 0, sizeof *m);
+    const char *b = strrchr(path, '/');
+    b = b ? b + 1 : path;
+    snprintf(m->name, sizeof m->name, "%.*s", (int)(ext_of(b) - b), b);
+    m->len = (uint64_t)st.st_size;
+    if (m->len) {
+        void *a = mmap(NULL, m->len, PROT_READ, MAP_SHARED, fd, 0);
+        if (a == MAP_FAILED) {
+            close(fd);
+            return -1;
+        }
+        m->map = a;
+        if (gck_host_register(m->map, m->len) != GCK_OK) m->map = a; /* pinning is an optimisation only */
+    }
+    close(fd); /* Disk.Walk: return file.Close() */
+    return 0;
+}
+
+static int walk(const char *path) { /* filepath.Walk with Disk.Walk's filter */
+    struct stat st;
+    if (lstat(path, &st) != 0) return -1;
+    if (!S_ISDIR(st.st_mode)) return strcmp(ext_of(path), ".csk") == 0 ? on_file(path) : 0;
+    DIR *d = opendir(path);
+    if (!d) return -1;
+    char **names = NULL;
+    size_t n = 0, cap = 0;
+    for (struct dirent *e; (e = readdir(d));) {
+        if (!strcmp(e->d_name, ".") || !strcmp(e->d_name, "..")) continue;
+        if (n == cap) names = realloc(names, (cap = cap ? 2 * cap : 16) * sizeof(char *));
+        names[n++] = strdup(e->d_name);
+    }
+    closedir(d);
+    qsort(names, n, sizeof(char *), cmp_str);
+    int rc = 0;
+    for (size_t i = 0; i < n; ++i) {
+        char *p = NULL;
+        if (!rc && asprintf(&p, "%s/%s", path, names[i]) > 0) rc = walk(p);
+        free(p);
+        free(names[i]);
+    }
+    free(names);
+    return rc;
+}
+
+typedef struct {
+    const uint8_t *key;
+    uint32_t klen;
+    gck_rec rec;
+    int live;
+} kd_entry;
+
+static int cmp_kd(const void *a, const void *b) {
+    const kd_entry *x = a, *y = b;
+    const uint32_t n = x->klen < y->klen ? x->klen : y->klen;
+    const int c = memcmp(x->key, y->key, n);
+    return c ? c : (x->klen > y->klen) - (x->klen < y->klen);
+}
+
+int main(int argc, char **argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s <db dir> [active name]\n", argv[0]);
+        return 2;
+    }
+    char active[256] = "";
+    if (argc > 2) {
+        snprintf(active, sizeof active, "%s", argv[2]);
+    } else { /* Disk.Open: the lexically last entry of any kind */
+        struct dirent **ents;
+        int n = scandir(argv[1], &ents, NULL, alphasort);
+        for (int i = 0; i < n; ++i) {
+            if (strcmp(ents[i]->d_name, ".") && strcmp(ents[i]->d_name, "..")) {
+                const char *e = ext_of(ents[i]->d_name);
+                snprintf(active, sizeof active, "%.*s", (int)(e - ents[i]->d_name), ents[i]->d_name);
+            }
+            free(ents[i]);
+        }
+        if (n >= 0) free(ents);
+    }
+    if (walk(argv[1]) != 0) {
+        fprintf(stderr, "walk failed\n");
+        return 3;
+    }
+    int rc = GCK_OK;
+    gck_result res;
+    memset(&res, 0, sizeof res);
+    if (g_n) { /* zero files: no replay, no files[0] */
+        gck_file *gf = calloc(g_n, sizeof(gck_file));
+        for (size_t i = 0; i < g_n; ++i) {
+            gf[i].data = g_files[i].map;
+            gf[i].len = g_files[i].len;
+            gf[i].reset_after = strcmp(g_files[i].name, active) != 0;
+        }
+        rc = gck_replay(gf, (uint32_t)g_n, NULL, &res);
+        free(gf);
+        if (rc != GCK_OK && rc != GCK_EUNEXPECTED_EOF) {
+            fprintf(stderr, "gck_replay: %d %s\n", rc, gck_last_error());
+            return 4;
+        }
+    }
+    /* keyDir.set / unset in walk order: a sorted array, last writer wins */
+    kd_entry *kd = calloc(res.n ? res.n : 1, sizeof(kd_entry));
+    size_t nk = 0;
+    for (uint64_t i = 0; i < res.n; ++i) {
+        const gck_rec *r = &res.recs[i];
+        kd[nk].key = g_files[r->file].map + r->rec_off + 16;
+        kd[nk].klen = r->key_len;
+        kd[nk].rec = *r;
+        kd[nk].live = !(r->flags & GCK_F_TOMBSTONE);
+        ++nk;
+    }
+    /* stable: equal keys keep walk order, the last one wins */
+    for (size_t i = 1; i < nk; ++i) { /* insertion sort by key (test sizes) */
+        kd_entry t = kd[i];
+        size_t j = i;
+        while (j > 0 && cmp_kd(&kd[j - 1], &t) > 0) {
+            kd[j] = kd[j - 1];
+            --j;
+        }
+        kd[j] = t;
+    }
+    size_t live = 0;
+    for (size_t i = 0; i < nk; ++i)
+        if ((i + 1 == nk || cmp_kd(&kd[i], &kd[i + 1]) != 0) && kd[i].live) ++live;
+    printf("status %d last_offset %u keys %zu\n", rc, res.final_last_offset, live);
+    for (size_t i = 0; i < nk; ++i) {
+        if (!((i + 1 == nk || cmp_kd(&kd[i], &kd[i + 1]) != 0) && kd[i].live)) continue;
+        for (uint32_t b = 0; b < kd[i].klen; ++b) printf("%02x", kd[i].key[b]);
+        const gck_rec *r = &kd[i].rec;
+        printf(" %u %u %u %u %s\n", r->crc, r->ts, r->value_pos, r->value_size, g_files[r->file].name);
+    }
+    free(kd);
+    if (g_n) gck_result_free(&res);
+    for (size_t i = 0; i < g_n; ++i)
+        if (g_files[i].len) {
+            gck_host_unregister(g_files[i].map);
+            munmap((void *)g_files[i].map, g_files[i].len);
+        }
+    free(g_files);
+    return 0;
+}

@@ -1,0 +1,101 @@
+"""The cgo shim's calling pattern, in C, against the real
+library (tests/shim/shim_test.c): files mmap'ed and pinned inside the Walk
+callback while Disk.Walk still has them open (internal/fs/disk.go:128-144),
+no files[0] when the walk finds no .csk file, gck_replay through
+include/gocask_hip.h, records applied to a map in walk order.  Its keydir must
+equal the reference tests' known answers (tests/golden/) and the oracle's."""
+import os
+import subprocess
+
+import pytest
+
+from golden_cases import load_case
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SHIM = os.path.join(HERE, "shim", "build", "shim_test")
+
+
+@pytest.fixture(scope="module")
+def shim():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    subprocess.run(["make", "-s", "-C", os.path.join(HERE, "shim")], check=True)
+    return SHIM
+
+
+def run(shim, d, active=None):
+    p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.splitlines()
+    head = lines[0].split()
+    st = dict(status=int(head[1]), last_offset=int(head[3]), keys=int(head[5]))
+    kd = {}
+    for ln in lines[1:]:
+        k, crc, ts, pos, size, f = ln.split()
+        kd[bytes.fromhex(k)] = dict(crc=int(crc), ts=int(ts), value_pos=int(pos), value_size=int(size), file=f)
+    assert len(kd) == st["keys"]
+    return st, kd
+
+
+@pytest.mark.parametrize("name", ["existing_after_startup", "keys_in_order", "updated_values_across_files",
+                                  "deleted_after_startup", "removed_keys", "datatxt_1000_puts", "crc_fail",
+                                  "partial_write_desync"])
+def test_shim_golden(shim, orc, tmp_path, name):
+    meta, files, reset = load_case(name)
+    assert sorted(meta["walk"]) == meta["walk"]  # a directory walks in this order too
+    for w, f in zip(meta["walk"], files):
+        (tmp_path / (w + ".csk")).write_bytes(f.tobytes())
+    st, kd = run(shim, tmp_path, meta["active"])
+    want, wst = orc.replay(files, reset)
+    okd = orc.keydir(files, want, reset)
+    assert st["status"] == wst["status"] and st["last_offset"] == wst["final_last_offset"]
+    assert set(kd) == set(okd)
+    for k, r in okd.items():
+        e = kd[k]
+        assert (e["crc"], e["ts"], e["value_pos"], e["value_size"]) == (
+            int(r["crc"]), int(r["ts"]), int(r["value_pos"]), int(r["value_size"]))
+        assert e["file"] == meta["walk"][int(r["file"])]
+    if meta["status"] != "unexpected_eof":  # the reference tests' own answers
+        assert set(kd) == {k.encode() for k in meta["expect"]}
+        for k, x in meta["expect"].items():
+            if "file" in x:
+                assert kd[k.encode()]["file"] == x["file"]
+        for k, x in meta.get("derived", {}).items():
+            if isinstance(x, dict) and not k.startswith("_") and "value_pos" in x:
+                assert kd[k.encode()]["value_pos"] == x["value_pos"], k
+
+
+def test_shim_no_data_files(shim, tmp_path):
+    # only a non-.csk entry: Disk.Open picks it as the active file, the walk
+    # finds nothing; the shim must not index files[0]
+    (tmp_path / "foo.txt").write_bytes(b"not a data file")
+    st, kd = run(shim, tmp_path)
+    assert st == dict(status=0, last_offset=0, keys=0) and kd == {}
+
+
+def test_shim_disk_layout(shim, orc, tmp_path):
+    # rotated data_<n>_<unix>.csk files, foo.txt, a nested directory; Disk.Open's
+    # active file (the lexically last entry, "foo") never matches, so every
+    # file resets lastOffset
+    files, names = orc.gen_corpus(seed=23, val_fixed=0, key_min=8, key_max=16, key_universe=300, tomb_permille=40,
+                                  flip_permille=20, max_file_size=1 << 16, n_files=10)
+    (tmp_path / "a_sub").mkdir()
+    nested = orc.entry(5, b"nested", b"v1") + orc.tombstone(6, b"k0000001")
+    (tmp_path / "a_sub" / "data_9_1.csk").write_bytes(nested)
+    for f, n in zip(files, names):
+        (tmp_path / (n + ".csk")).write_bytes(f.tobytes())
+    (tmp_path / "foo.txt").write_bytes(b"x")
+    st, kd = run(shim, tmp_path)
+    import numpy as np
+
+    walk = ["data_9_1"] + sorted(names)
+    wf = [np.frombuffer(nested, np.uint8)] + [files[names.index(n)] for n in sorted(names)]
+    want, wst = orc.replay(wf, [True] * len(wf))
+    okd = orc.keydir(wf, want, [True] * len(wf))
+    assert st["status"] == 0 and st["last_offset"] == wst["final_last_offset"] == 0
+    assert set(kd) == set(okd)
+    for k, r in okd.items():
+        assert kd[k]["value_pos"] == int(r["value_pos"]) and kd[k]["file"] == walk[int(r["file"])]
