@@ -9,8 +9,10 @@ into HBM by the device encoder before timing starts.
   python bench.py [--gpus N --steps K --warmup W --config c3]
   N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Each rank replays its own C3-shaped shard (16 x 2 GiB files, seed 3+rank):
-weak scaling, no data-path collective (files are independent).
+N = 1 times C3 (BASELINE's metric config).  N > 1 times C4: one corpus of
+16 x N files of 2 GiB (per-file seed 4 + n), cut into N contiguous walk-order
+shards, one per rank (weak scaling; no data-path collective: the files are
+independent).
 After the timed replays, N>1 runs also time the keydir merge across ranks (the
 path's one exchange step, RCCL all-to-all; reported as "keydir_merge", not
 part of value).  Rank 0 prints one JSON line.
@@ -33,12 +35,19 @@ CONFIGS = {
                max_file_size=2 << 30, n_files=16),
     "c5": dict(seed=3, val_fixed=0, key_min=8, key_max=24, key_universe=5_000_000, tomb_permille=10,
                flip_permille=10, max_file_size=2 << 30, n_files=16),
+    # C4: one corpus of 16 x N files (8 GPUs: 128 x 2 GiB = 256 GiB), file n a
+    # one-file C3-spec corpus with seed 4 + n, cut into N
+    # contiguous walk-order shards (gocask_amd.shard.c4_file_ids)
+    "c4": dict(seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=312_500, tomb_permille=10,
+               max_file_size=2 << 30, n_files=1),
 }
+C4_FILES_PER_GPU = 16
 DESCR = {
     "c1": "C1: 1 x 64 MiB file, 16 B keys, 1 KiB values",
     "c2": "C2: 1 x 8 GiB file, 16 B keys, 4 KiB values",
     "c3": "C3: 32 GiB = 16 x 2 GiB rotated files, 8-24 B keys, Zipf(1.1) 64 B-64 KiB values, 1% tombstones",
     "c5": "C5: C3 + 1% single-bit flips in values",
+    "c4": "C4: {n} x 2 GiB files (per-file seed 4+n, C3 spec), one corpus cut into {g} contiguous walk-order shards",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -201,18 +210,30 @@ def keydir_merge(g, ctx, dist, n_files, reps=2):
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     w, lo, ex, mg = (round(x * 1e3, 3) for x in v.tolist())
     return dict(ms=w, local_ms=lo, exchange_ms=ex, merge_ms=mg, live_entries=int(c[0].item()),
-                exchanged_bytes=int(c[1].item()),
+                exchanged_bytes=int(c[1].item()), global_status=ph["status"],
                 note="global keydir over all ranks' files: keydir with tombstones per rank, key-hash partition, "
                      "RCCL all-to-all of entries + keys, per-owner last-shard-wins merge; max over ranks; "
                      "not part of value")
 
 
 def shard_config(cfg_name, rank):
-    """The corpus rank `rank` replays: its own C3-shaped shard of independent
-    files (seed + rank), so no data-path collective is needed."""
+    """A per-rank corpus for the configs that are not sharded (C1-C3, C5 at
+    N > 1: rank r replays its own copy of the spec with seed + r)."""
     cfg = dict(CONFIGS[cfg_name])
     cfg["seed"] = cfg["seed"] + rank
     return cfg
+
+
+def encode_workload(ctx, cfg_name, world, rank):
+    """Encode this rank's files into its context.  C4: the rank's contiguous
+    walk-order range of the one global corpus (no data-path collective: the
+    files are independent)."""
+    if cfg_name == "c4":
+        from gocask_amd import shard
+
+        ids, last_active = shard.c4_file_ids(world, rank, C4_FILES_PER_GPU)
+        return ctx.encode_files(ids, last_is_active=last_active, **CONFIGS["c4"])
+    return ctx.encode(**shard_config(cfg_name, rank))
 
 
 def reduce_over_ranks(dist, elapsed, nbytes, device):
@@ -233,7 +254,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="workload (default: c3 at one GPU, c4 -- one corpus sharded over the GPUs -- at N > 1)")
     ap.add_argument("--chunk-kib", type=int, default=0)
     ap.add_argument("--cpu-sample-gib", type=float, default=2.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -268,10 +290,11 @@ def main():
 
     import gocask_amd as g
 
-    cfg = shard_config(args.config, rank)
+    if args.config is None:
+        args.config = "c3" if world == 1 else "c4"
     t_setup = time.perf_counter()
     ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10, spec_window=args.spec_kib << 10)
-    info = ctx.encode(**cfg)
+    info = encode_workload(ctx, args.config, world, rank)
     setup_s = time.perf_counter() - t_setup
 
     def barrier():
@@ -340,12 +363,13 @@ def main():
             "dtype": "u8",
             "data": "synthetic (device-encoded GoCask records, DESIGN.md Corpus)",
             "config": {
-                "workload": DESCR[args.config] + (" per GPU" if world > 1 else ""),
+                "workload": DESCR[args.config].format(n=C4_FILES_PER_GPU * world, g=world)
+                + (" per GPU" if world > 1 and args.config != "c4" else ""),
                 "bytes_per_gpu": my_bytes,
                 "records_per_gpu": st["n_recs"],
                 "files_per_gpu": info["n_files"],
                 "crc_rejects": st["n_crc_fail"],
-                "parallelism": f"files sharded over {world} GPU(s), no data-path collective"
+                "parallelism": f"files sharded over {world} GPU(s) in contiguous walk-order ranges, no data-path collective"
                                + ("; keydir merge over RCCL all-to-all after the timed replays" if world > 1 else ""),
             },
             "roofline": {

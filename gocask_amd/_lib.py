@@ -53,7 +53,7 @@ assert KD_ENTRY_DTYPE.itemsize == 64
 EXPORTED = [
     "gck_replay", "gck_result_free", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
     "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
-    "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_stream_pattern", "gck_diag_crc_variant", "gck_diag_walk_variant", "gck_diag_spec_entries", "gck_encode_corpus", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
+    "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_stream_pattern", "gck_diag_crc_variant", "gck_diag_walk_variant", "gck_diag_spec_entries", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
     "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count", "gck_host_register", "gck_host_unregister",
     "gck_version", "gck_last_error",
@@ -100,6 +100,13 @@ class GckStats(ctypes.Structure):
         ("ms_kernel", ctypes.c_double * 12),
         ("device_path", ctypes.c_uint32),
         ("n_reruns", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("err_file", ctypes.c_uint32),
+        ("err_off", ctypes.c_uint64),
+        ("files_walked", ctypes.c_uint32),
+        ("final_last_offset", ctypes.c_uint32),
+        ("n_files", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
     ]
 
 
@@ -189,6 +196,7 @@ def load():
         "gck_diag_spec_entries": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
         "gck_encode_corpus": (ctypes.c_int, [vp, P(GckCorpusCfg), P(ctypes.c_uint32), P(ctypes.c_uint64), vp,
                                              ctypes.c_uint32]),
+        "gck_encode_files": (ctypes.c_int, [vp, P(GckCorpusCfg), vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]),
         "gck_encode_walk_order": (ctypes.c_int, [vp, vp, ctypes.c_uint32]),
         "gck_encode_zipf_table": (None, [vp]),
         "gck_encode_batch": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_uint64, vp,

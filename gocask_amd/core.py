@@ -296,6 +296,23 @@ class ReplayContext:
         self._L.gck_encode_walk_order(self._h, order.ctypes.data, nf.value)
         return dict(n_files=nf.value, n_ops=nops.value, sizes=sizes[:nf.value].copy(), walk_order=order)
 
+    def encode_files(self, file_ids, last_is_active=False, **kw):
+        """One-file corpora data_<id>_... (seed = seed + id), in the given
+        (walk) order, into the arena (gck_encode_files): BASELINE C4's shards."""
+        c = GckCorpusCfg()
+        d = dict(seed=1, max_file_size=64 * MB, n_ops=0, n_files=1, key_min=16, key_max=16, key_universe=0,
+                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000)
+        d.update(kw)
+        for k, v in d.items():
+            setattr(c, k, v)
+        ids = np.ascontiguousarray(file_ids, dtype=np.uint32)
+        sizes = np.zeros(max(len(ids), 1), dtype=np.uint64)
+        nops = ctypes.c_uint64()
+        check(self._L.gck_encode_files(self._h, ctypes.byref(c), ids.ctypes.data, len(ids), 1 if last_is_active else 0,
+                                       ctypes.byref(nops), sizes.ctypes.data))
+        return dict(n_files=len(ids), n_ops=nops.value, sizes=sizes[:len(ids)].copy(),
+                    walk_order=np.arange(len(ids), dtype=np.uint32), file_ids=ids.copy())
+
     def run(self):
         return check(self._L.gck_ctx_run(self._h), (GCK_OK, GCK_EUNEXPECTED_EOF))
 
@@ -416,7 +433,9 @@ class ReplayContext:
             phases[name] = s.ms_kernel[i]
         return dict(bytes=s.bytes, n_recs=s.n_recs, n_crc_fail=s.n_crc_fail, n_chunks=s.n_chunks,
                     n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
-                    device_path=bool(s.device_path), n_reruns=s.n_reruns)
+                    device_path=bool(s.device_path), n_reruns=s.n_reruns, status=s.status, err_file=s.err_file,
+                    err_off=s.err_off, files_walked=s.files_walked, final_last_offset=s.final_last_offset,
+                    n_files=s.n_files)
 
     def stream_read_ceiling(self, iters=10):
         """Plain streaming read of the resident arena: (ms per pass, GB/s)."""

@@ -207,6 +207,50 @@ int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files
     return GCK_OK;
 }
 
+int gck_encode_files(gck_ctx *ctx, const gck_corpus_cfg *cfg, const uint32_t *file_ids, uint32_t n,
+                     uint32_t last_is_active, uint64_t *n_ops_out, uint64_t *file_sizes) {
+    if (!ctx || !cfg || (n && !file_ids)) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    std::vector<std::vector<OpDesc>> ops(n);
+    std::vector<uint64_t> lens(n);
+    std::vector<uint8_t> reset(n);
+    for (uint32_t k = 0; k < n; ++k) {
+        gck_corpus_cfg one = *cfg;
+        one.seed = cfg->seed + file_ids[k];
+        one.n_files = 1;
+        one.n_ops = 0;
+        std::vector<uint32_t> op_file;
+        std::vector<uint64_t> sizes;
+        const int rc = plan(&one, ops[k], op_file, sizes);
+        if (rc) return rc;
+        lens[k] = sizes[0];
+        reset[k] = (last_is_active && k + 1 == n) ? 0 : 1;
+    }
+    int rc = ctx_layout(c, lens.data(), n, reset.data());
+    if (rc) return rc;
+    c->walk_to_creation.assign(file_ids, file_ids + n);
+    DBuf d_ops;
+    for (uint32_t k = 0; k < n; ++k) {
+        for (auto &o : ops[k]) o.dst += c->f_base[k];
+        if (ops[k].empty()) continue;
+        if ((rc = d_ops.ensure(ops[k].size() * sizeof(OpDesc) + 16))) return rc;
+        GCK_HIP(hipMemcpy(d_ops.p, ops[k].data(), ops[k].size() * sizeof(OpDesc), hipMemcpyHostToDevice));
+        const uint32_t grid = (uint32_t)((ops[k].size() + 255) / 256);
+        k_encode<<<grid, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), d_ops.as<OpDesc>(), ops[k].size(),
+                                             cfg->seed + file_ids[k], cfg->ts_base, cfg->flip_permille);
+        GCK_HIP(hipGetLastError());
+        GCK_HIP(hipStreamSynchronize(c->stream));  // d_ops is reused by the next file
+    }
+    d_ops.release();
+    uint64_t tot = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        tot += ops[k].size();
+        if (file_sizes) file_sizes[k] = lens[k];
+    }
+    if (n_ops_out) *n_ops_out = tot;
+    return GCK_OK;
+}
+
 int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n) {
     if (!ctx || !creation_index) return GCK_EINVAL;
     const auto &o = ctx->c.walk_to_creation;

@@ -1921,6 +1921,12 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->n_reruns = c->n_reruns;
     out->ms_total = c->ms_total;
     for (int p = 0; p < PH_NPHASE && p < 12; ++p) out->ms_kernel[p] = c->ms_phase[p];
+    out->status = c->status;
+    out->err_file = c->err_file;
+    out->err_off = c->err_off;
+    out->files_walked = c->files_walked;
+    out->final_last_offset = c->final_last_offset;
+    out->n_files = c->nfiles;
     return GCK_OK;
 }
 

@@ -117,6 +117,14 @@ typedef struct gck_stats {
     double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
     uint32_t device_path;   /* 1: the last run had no host round trip (record table sized by an earlier run) */
     uint32_t n_reruns;      /* device-only runs redone on the host path (capacity / unsettled speculation)  */
+    /* the last run's outcome, as gck_result reports it (no records copied):   */
+    int32_t status;              /* GCK_OK or GCK_EUNEXPECTED_EOF                 */
+    uint32_t err_file;           /* file index of the startup error               */
+    uint64_t err_off;            /* header offset of the record that hit it       */
+    uint32_t files_walked;       /* files the reference would have walked         */
+    uint32_t final_last_offset;  /* keyDir.lastOffset after replay                */
+    uint32_t n_files;            /* files in the arena                            */
+    uint32_t reserved;
 } gck_stats;
 
 int gck_ctx_create(const gck_opts *opts, gck_ctx **out);
@@ -251,6 +259,14 @@ typedef struct gck_corpus_cfg {
  * order, may be NULL) report the layout. */
 int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files_out,
                       uint64_t *n_ops_out, uint64_t *file_sizes, uint32_t max_files);
+/* Encode n independent one-file corpora into the context's arena, in the given
+ * order (the caller's walk order): slot k is file data_<id>_<ts_base+id> with
+ * file_ids[k] = id, generated by the spec of cfg with seed cfg->seed + id and
+ * n_files = 1 (BASELINE C4: per-file seed 4 + n).  Every file resets lastOffset
+ * except the last when last_is_active.  n_ops_out / file_sizes (n entries,
+ * optional) report the ops and bytes per slot. */
+int gck_encode_files(gck_ctx *ctx, const gck_corpus_cfg *cfg, const uint32_t *file_ids, uint32_t n,
+                     uint32_t last_is_active, uint64_t *n_ops_out, uint64_t *file_sizes);
 /* Walk-order index -> creation index n of file data_<n>_... in the last encoded corpus. */
 int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n);
 /* The encoder's Zipf threshold table (65472 u32), for cross-checks. */

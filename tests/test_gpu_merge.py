@@ -295,3 +295,97 @@ def test_merge_keydir_two_ranks(g, orc):
     _check_merged(wf, owners, _global_keydir(wf, want), 2, [0, 0, 1, 1, 1])
     for p in procs:
         assert p.exitcode == 0
+
+
+# ---------------------- exact sharding: planned cuts, startup error propagation ---
+def _sharded_owners(g, torch, wf, reset, world, nparts):
+    """plan_shards + one context per shard + resolve_status; only the shards
+    up to the first startup error are packed (later ones send nothing)."""
+    from gocask_amd import shard
+
+    ranges = shard.plan_shards([len(f) for f in wf], reset, world)
+    per = []
+    for a, b in ranges:
+        with g.ReplayContext() as ctx:
+            if b > a:
+                ctx.load(wf[a:b], reset[a:b])
+                ctx.run()
+                per.append(ctx.stats())
+            else:
+                per.append(dict(status=0, err_file=0, err_off=0, files_walked=0, final_last_offset=0, n_files=0))
+    glob, contrib = shard.resolve_status(per)
+    shards = [(wf[a:b], reset[a:b]) for (a, b), c in zip(ranges, contrib) if c]
+    packed = _pack_shards(g, torch, shards, nparts)
+    try:
+        owners = [_merge_owner(torch, packed, p, packed[p % len(packed)][0]) for p in range(nparts)]
+    finally:
+        for c, *_ in packed:
+            c.close()
+    shard_of_file = [s for s, (a, b) in enumerate(ranges) for _ in range(a, b)]
+    return glob, owners, shard_of_file
+
+
+@pytest.mark.parametrize("world,nparts", [(2, 2), (3, 1), (4, 3)])
+def test_sharded_startup_error_propagates(g, orc, world, nparts):
+    import torch
+
+    from golden_cases import load_case
+
+    files, names = orc.gen_corpus(seed=77, val_fixed=0, key_min=8, key_max=16, key_universe=400,
+                                  tomb_permille=150, max_file_size=1 << 17, n_files=5)
+    wf, _ = _walk(files, names)
+    _, bad, _ = load_case("partial_write_desync")  # "unexpected EOF" on a key read at offset 74
+    wf = wf[:2] + [bad[0]] + wf[2:]
+    reset = [True] * (len(wf) - 1) + [False]
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] == 1 and wst["err_file"] == 2
+    glob, owners, shard_of_file = _sharded_owners(g, torch, wf, reset, world, nparts)
+    assert (glob["status"], glob["err_file"], glob["err_off"], glob["files_walked"]) == (
+        wst["status"], wst["err_file"], wst["err_off"], wst["files_walked"])
+    _check_merged(wf, owners, _global_keydir(wf, want), nparts, shard_of_file)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_keys_in_order_never_cuts_after_the_active_file(g, orc, world):
+    # core/db_test.go:428-471: the active "data" is walked first and does not
+    # reset lastOffset, so foobar in data01 has ValuePos 66; a cut right after
+    # "data" would give 22
+    import torch
+
+    from golden_cases import load_case
+
+    from gocask_amd import shard
+
+    meta, files, reset = load_case("keys_in_order")
+    assert reset[0] is False
+    ranges = shard.plan_shards([len(f) for f in files], reset, world)
+    assert all(a != 1 for a, _ in ranges)
+    want, wst = orc.replay(files, reset)
+    glob, owners, shard_of_file = _sharded_owners(g, torch, files, reset, world, 2)
+    assert glob["status"] == 0 and glob["final_last_offset"] == wst["final_last_offset"] == meta["final_last_offset"]
+    kd = _global_keydir(files, want)
+    _check_merged(files, owners, kd, 2, shard_of_file)
+    assert int(kd[b"foobar"]["value_pos"]) == 66
+
+
+def test_encode_files_matches_oracle_one_file_corpora(g, orc):
+    # BASELINE C4's generator: file n is a one-file corpus with seed + n
+    kw = dict(seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=2000, tomb_permille=10, flip_permille=10,
+              max_file_size=1 << 20, n_files=1)
+    ids = [3, 0, 11]
+    with g.ReplayContext() as ctx:
+        info = ctx.encode_files(ids, last_is_active=True, **kw)
+        files = []
+        for k, n in enumerate(ids):
+            want_f, want_names = orc.gen_corpus(**{**kw, "seed": 4 + n})
+            assert len(want_f) == 1 and int(info["sizes"][k]) == len(want_f[0])
+            got = ctx.read_file(k, 0, len(want_f[0]))
+            assert np.array_equal(got, want_f[0]), n
+            files.append(want_f[0])
+        ctx.run()
+        recs, st = ctx.fetch()
+    want, wst = orc.replay(files, [True, True, False])
+    assert st["status"] == 0 and len(recs) == len(want) == info["n_ops"]
+    for f in FIELDS:
+        assert np.array_equal(recs[f], want[f]), f
+    assert st["final_last_offset"] == wst["final_last_offset"] == len(files[-1])

@@ -110,3 +110,148 @@ def test_sharded_merge_rule_equals_global_keydir(orc, cuts, nparts):
             if not int(r["flags"]) & 1:
                 merged[key] = (f, int(r["rec_off"]))
     assert merged == glob
+
+
+# ------------------------------------------------ shard planning (exact cuts) ---
+def test_plan_shards_cuts_only_after_resetting_files():
+    import random
+
+    from gocask_amd import shard
+
+    rng = random.Random(5)
+    for _ in range(300):
+        n = rng.randint(0, 12)
+        sizes = [rng.randint(0, 100) for _ in range(n)]
+        reset = [rng.random() < 0.7 for _ in range(n)]
+        world = rng.randint(1, 6)
+        ranges = shard.plan_shards(sizes, reset, world)
+        assert len(ranges) == world and ranges[0][0] == 0 and ranges[-1][1] == n
+        for (a, b), (c, _) in zip(ranges, ranges[1:]):
+            assert a <= b == c  # contiguous, in walk order
+        for a, b in ranges[1:]:
+            assert a == n or a == 0 or reset[a - 1], (sizes, reset, ranges)
+
+
+def test_plan_shards_balances_bytes():
+    from gocask_amd import shard
+
+    assert shard.plan_shards([10] * 16, [True] * 15 + [False], 4) == [(0, 4), (4, 8), (8, 12), (12, 16)]
+    # the active file walked first (core/db_test.go:428-471): no cut right after it
+    assert shard.plan_shards([41, 25, 25], [False, True, True], 3) == [(0, 2), (2, 2), (2, 3)]
+    assert shard.plan_shards([5, 5], [True, False], 1) == [(0, 2)]
+
+
+def _status(st, n_files):
+    return dict(status=st["status"], err_file=st["err_file"], err_off=st["err_off"],
+                files_walked=st["files_walked"], final_last_offset=st["final_last_offset"], n_files=n_files)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_replay_with_startup_error_equals_global(orc, world):
+    """A startup error in one shard aborts the walk for every later shard
+    (core/db.go:134-138, disk.go:134-141): resolve_status + the merge rule on
+    the oracle's per-shard records == the oracle's global replay."""
+    from golden_cases import load_case
+
+    from gocask_amd import shard
+
+    files, names = orc.gen_corpus(seed=83, val_fixed=0, key_min=8, key_max=16, key_universe=300,
+                                  tomb_permille=150, max_file_size=1 << 15, n_files=6)
+    wf = [files[i] for i in sorted(range(len(files)), key=lambda i: names[i])]
+    _, bad, _ = load_case("partial_write_desync")
+    wf = wf[:3] + [bad[0]] + wf[3:]
+    reset = [True] * (len(wf) - 1) + [False]
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] == 1 and wst["err_file"] == 3
+    ranges = shard.plan_shards([len(f) for f in wf], reset, world)
+    per, recs_of = [], []
+    for a, b in ranges:
+        recs, st = orc.replay(wf[a:b], reset[a:b]) if b > a else (want[:0], dict(
+            status=0, err_file=0, err_off=0, files_walked=0, final_last_offset=0))
+        per.append(_status(st, b - a))
+        recs_of.append((a, recs))
+    glob, contrib = shard.resolve_status(per)
+    assert glob["status"] == wst["status"] and glob["err_file"] == wst["err_file"]
+    assert glob["err_off"] == wst["err_off"] and glob["files_walked"] == wst["files_walked"]
+    merged = {}
+    for (a, recs), c in zip(recs_of, contrib):
+        if not c:
+            continue
+        for key, (f, r) in _keydir_with_tombstones(wf[a:], recs, a).items():
+            if int(r["flags"]) & 1:
+                merged.pop(key, None)
+            else:
+                merged[key] = (f, int(r["rec_off"]), int(r["value_pos"]))
+    glob_kd = {}
+    for r in want:
+        o = int(r["rec_off"]) + 16
+        key = bytes(wf[int(r["file"])][o:o + int(r["key_len"])])
+        if int(r["flags"]) & 1:
+            glob_kd.pop(key, None)
+        else:
+            glob_kd[key] = (int(r["file"]), int(r["rec_off"]), int(r["value_pos"]))
+    assert merged == glob_kd
+
+
+def test_resolve_status_without_errors():
+    from gocask_amd import shard
+
+    ok = lambda n, last: dict(status=0, err_file=0, err_off=0, files_walked=n, final_last_offset=last, n_files=n)
+    g, c = shard.resolve_status([ok(2, 0), ok(0, 0), ok(3, 77), ok(0, 0)])
+    assert g == dict(status=0, err_file=0, err_off=0, files_walked=5, final_last_offset=77) and all(c)
+
+
+def test_c4_shards_cover_the_corpus_in_walk_order():
+    from gocask_amd import shard
+
+    for world in (1, 2, 4, 8):
+        total = 16 * world
+        names = sorted(f"data_{n}_{1700000000 + n}.csk" for n in range(total))
+        got, actives = [], []
+        for r in range(world):
+            ids, last_active = shard.c4_file_ids(world, r)
+            assert len(ids) == 16
+            got += ids
+            actives.append(last_active)
+        assert [f"data_{n}_{1700000000 + n}.csk" for n in got] == names
+        assert actives == [False] * (world - 1) + [True]
+
+
+class _FakeCtx:
+    def __init__(self, st):
+        self._st = st
+
+    def stats(self):
+        return self._st
+
+
+def _status_worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    from gocask_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        st = [dict(status=0, err_file=0, err_off=0, files_walked=2, final_last_offset=0, n_files=2),
+              dict(status=1, err_file=1, err_off=74, files_walked=2, final_last_offset=9, n_files=3)][rank]
+        out.put((rank,) + shard.gather_status(_FakeCtx(st), dist))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_status_two_ranks_gloo():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_status_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, g, c in res:
+        assert g == dict(status=1, err_file=3, err_off=74, files_walked=4, final_last_offset=9) and c == [True, True]
