@@ -249,6 +249,23 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
+def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0):
+    """gck_replay_into: host-in/host-out replay (pipelined over file groups)
+    with the tuples written into recs (a REC_DTYPE array; register it with
+    host_register for DMA rate).  Returns the status dict; recs[:n] hold the
+    records."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    res = GckResult()
+    rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes)),
+                           recs.ctypes.data if recs.size else None, recs.size, ctypes.byref(res))
+    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+    return dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=res.n,
+                n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset, files_walked=res.files_walked)
+
+
 def keydir(files, recs):
     """Apply the tuples in walk order (core/keydir.go:22-49): {key: record row}."""
     kd = {}

@@ -1379,8 +1379,14 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
-    std::vector<uint32_t> slice, nib, xinv, xfw, xa, xb, zrow, zl;
-    make_tables(slice, nib, xinv, xfw, xa, xb, zrow, zl);
+    // the constant tables are the same for every context: built once per process
+    struct Tables {
+        std::vector<uint32_t> slice, nib, xinv, xfw, xa, xb, zrow, zl;
+        Tables() { make_tables(slice, nib, xinv, xfw, xa, xb, zrow, zl); }
+    };
+    static const Tables tabs;
+    const std::vector<uint32_t> &slice = tabs.slice, &nib = tabs.nib, &xinv = tabs.xinv, &xfw = tabs.xfw,
+                                &xa = tabs.xa, &xb = tabs.xb, &zrow = tabs.zrow, &zl = tabs.zl;
     int rc;
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xfw.ensure(xfw.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
@@ -1951,22 +1957,156 @@ int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, u
     return GCK_OK;
 }
 
+// Host-in/host-out replay, pipelined over file groups: the files are cut into
+// contiguous walk-order groups of >= kGroupBytes, each cut after a file that
+// resets lastOffset (so every group replays exactly as the whole walk would,
+// as shards do, gocask_amd/shard.py), one context per group.  All H2D copies
+// are queued at once on a copy stream; group g's replay waits only for its own
+// files, so it runs while later groups are still crossing PCIe.  The first
+// group with a startup error ends the walk (core/db.go:134-138): later groups
+// contribute nothing.  The tuples of the contributing groups (their file
+// indices rebased) are gathered into one array: into the caller's dst (cap
+// records) when dst != NULL, else into library-owned pinned memory.
+constexpr uint64_t kGroupBytes = 1ull << 30;
+
+__global__ void k_rebase_file(gck_rec *recs, uint64_t n, uint32_t base) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        recs[i].file += base;
+}
+
+static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
+                          uint64_t cap, gck_result *out) {
+    memset(out, 0, sizeof(*out));
+    for (uint32_t f = 0; f < nfiles; ++f)
+        if (files[f].len && !files[f].data) return GCK_EINVAL;
+    std::vector<uint32_t> cut{0};  // group g = files [cut[g], cut[g+1])
+    uint64_t acc = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        acc += files[f].len;
+        if (acc >= kGroupBytes && files[f].reset_after && f + 1 < nfiles) {
+            cut.push_back(f + 1);
+            acc = 0;
+        }
+    }
+    cut.push_back(nfiles);
+    const uint32_t G = (uint32_t)cut.size() - 1;
+    std::vector<gck_ctx *> cs(G, nullptr);
+    std::vector<hipEvent_t> ev(G, nullptr);
+    hipStream_t copy = nullptr;
+    int rc = GCK_OK;
+    auto cleanup = [&]() {
+        if (copy) (void)hipStreamSynchronize(copy);
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (copy) (void)hipStreamDestroy(copy);
+        for (auto *c : cs) gck_ctx_destroy(c);
+    };
+    for (uint32_t g = 0; g < G && !rc; ++g) rc = gck_ctx_create(opts, &cs[g]);
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    const int dev = cs[0]->c.device;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) != hipSuccess) {
+        cleanup();
+        return GCK_EDEVICE;
+    }
+    for (uint32_t g = 0; g < G && !rc; ++g) {  // layouts, then every H2D queued on the copy stream
+        Ctx *c = &cs[g]->c;
+        const uint32_t f0 = cut[g], n = cut[g + 1] - f0;
+        std::vector<uint64_t> lens(n);
+        std::vector<uint8_t> reset(n);
+        for (uint32_t k = 0; k < n; ++k) {
+            lens[k] = files[f0 + k].len;
+            reset[k] = files[f0 + k].reset_after ? 1 : 0;
+        }
+        if ((rc = ctx_layout(c, lens.data(), n, reset.data()))) break;
+        for (uint32_t k = 0; k < n; ++k)
+            if (lens[k] && hipMemcpyAsync(c->arena.as<uint8_t>() + c->f_base[k], files[f0 + k].data, lens[k],
+                                          hipMemcpyHostToDevice, copy) != hipSuccess)
+                rc = GCK_EDEVICE;
+        if (hipEventCreateWithFlags(&ev[g], hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(ev[g], copy) != hipSuccess)
+            rc = GCK_EDEVICE;
+    }
+    uint32_t last = G;  // groups [0, last) contribute
+    for (uint32_t g = 0; g < G && !rc; ++g) {
+        Ctx *c = &cs[g]->c;
+        if (hipStreamWaitEvent(c->stream, ev[g], 0) != hipSuccess) {
+            rc = GCK_EDEVICE;
+            break;
+        }
+        const int r = ctx_run(c);
+        if (r != GCK_OK && r != GCK_EUNEXPECTED_EOF) {
+            rc = r;
+            break;
+        }
+        if (r == GCK_EUNEXPECTED_EOF) {
+            last = g + 1;
+            break;
+        }
+    }
+    if (rc) {
+        cleanup();
+        return rc;
+    }
+    uint64_t n_total = 0;
+    for (uint32_t g = 0; g < last; ++g) n_total += cs[g]->c.n_recs;
+    const Ctx *lc = &cs[last - 1]->c;
+    out->n = n_total;
+    out->status = lc->status;
+    out->err_file = cut[last - 1] + lc->err_file;
+    out->err_off = lc->err_off;
+    out->files_walked = cut[last - 1] + lc->files_walked;
+    // cuts follow resetting files: the last contributing group's lastOffset
+    out->final_last_offset = lc->final_last_offset;
+    for (uint32_t g = 0; g < last; ++g) out->n_crc_fail += cs[g]->c.n_crc_fail;
+    if (into && cap < n_total) {
+        cleanup();
+        return GCK_EINVAL;  // out->n says how many records to make room for
+    }
+    gck_rec *h = into ? dst : nullptr;
+    if (!into && n_total) {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, n_total * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) {
+            cleanup();
+            return GCK_ENOMEM;
+        }
+        h = static_cast<gck_rec *>(p);
+    }
+    uint64_t off = 0;
+    for (uint32_t g = 0; g < last && !rc; ++g) {
+        Ctx *c = &cs[g]->c;
+        if (!c->n_recs) continue;
+        if (cut[g]) k_rebase_file<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<gck_rec>(), c->n_recs, cut[g]);
+        if (hipMemcpyAsync(h + off, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess)
+            rc = GCK_EDEVICE;
+        off += c->n_recs;
+    }
+    for (uint32_t g = 0; g < last; ++g)
+        if (hipStreamSynchronize(cs[g]->c.stream) != hipSuccess) rc = GCK_EDEVICE;
+    if (rc) {
+        if (!into && h) (void)hipHostFree(h);
+        cleanup();
+        return rc;
+    }
+    out->recs = into ? nullptr : h;  // caller memory: nothing for gck_result_free
+    cleanup();
+    return out->status;
+}
+
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
-    gck_ctx *ctx = nullptr;
-    int rc = gck_ctx_create(opts, &ctx);
-    if (rc) return rc;
-    rc = gck_ctx_load(ctx, files, nfiles);
-    if (!rc) {
-        rc = gck_ctx_run(ctx);
-        if (rc == GCK_OK || rc == GCK_EUNEXPECTED_EOF) {
-            const int frc = gck_ctx_fetch(ctx, out);
-            if (frc) rc = frc;
-        }
-    }
-    gck_ctx_destroy(ctx);
-    return rc;
+    if (nfiles && !files) return GCK_EINVAL;
+    return replay_grouped(files, nfiles, opts, false, nullptr, 0, out);
+}
+
+int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_rec *dst, uint64_t cap,
+                    gck_result *out) {
+    if (!out || (cap && !dst) || (nfiles && !files)) return GCK_EINVAL;
+    return replay_grouped(files, nfiles, opts, true, dst, cap, out);
 }
 
 void gck_result_free(gck_result *res) {

@@ -99,8 +99,18 @@ typedef struct gck_result {
     uint64_t err_off;           /* header offset of the record that hit the error       */
 } gck_result;
 
-/* One-shot host-in/host-out replay (H2D, device pipeline, D2H). */
+/* One-shot host-in/host-out replay: H2D, device pipeline, D2H.  Pipelined over
+ * groups of files (>= 1 GiB, cut after files that reset lastOffset): every H2D
+ * copy is queued at once and each group replays as soon as its own files are
+ * resident, while later groups still cross PCIe (register the files with
+ * gck_host_register for asynchronous DMA).  Results are those of one replay
+ * of all files in walk order. */
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
+/* The same, tuples into caller memory dst (cap records; pin it for DMA rate);
+ * out->recs = NULL.  GCK_EINVAL (out->n = records needed, nothing copied)
+ * when cap < out->n. */
+int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_rec *dst, uint64_t cap,
+                    gck_result *out);
 void gck_result_free(gck_result *res);
 
 /* ---- device-resident context (benchmarks, repeated replays) ---------------- */

@@ -513,3 +513,39 @@ def test_keys_longer_than_speculation_bound(g, orc):
         st, vs, cc, vals = ctx.get_batch(keys)
     assert len(live) == 50 and all(s == 0 for s in st)
     assert max(len(k) for k in keys) > 65535
+
+
+# ------------------------------------- pipelined host-in/host-out replay ---
+def test_replay_grouped_equals_oracle(g, orc, monkeypatch):
+    # gck_replay / gck_replay_into cut the files into >= 1 GiB groups after
+    # files that reset lastOffset; with 12 x ~200 MiB files and the active
+    # file in the middle, groups must neither split a carry nor reorder
+    kw = dict(seed=46, val_fixed=0, key_min=8, key_max=24, key_universe=200000, tomb_permille=10,
+              flip_permille=10, max_file_size=200 << 20, n_files=12)
+    files, names = orc.gen_corpus(**kw)
+    wf, _ = walk_sorted(files, names)
+    reset = [True] * len(wf)
+    reset[5] = False  # the active file walked mid-way: lastOffset carries into file 6
+    want, wst = orc.replay(wf, reset)
+    got, gst = g.replay(wf, reset)
+    assert_same(got, gst, want, wst)
+    recs = np.zeros(len(want) + 3, dtype=g.REC_DTYPE)
+    st = g.replay_into(wf, recs, reset)
+    assert_same(recs[:st["n_recs"]], st, want, wst)
+    small = np.zeros(10, dtype=g.REC_DTYPE)
+    with pytest.raises(Exception):
+        g.replay_into(wf, small, reset)
+
+
+def test_replay_grouped_startup_error(g, orc):
+    # a startup error in a later group: the records before it, nothing after
+    big = [orc.gen_corpus(seed=47 + i, val_fixed=4096, key_min=16, key_max=16, max_file_size=600 << 20,
+                          n_files=1)[0][0] for i in range(3)]
+    bad = np.frombuffer(orc_mod.entry(1, b"user", b"x" * 10) + orc_mod.entry(2, b"key", b"yy")[:-4], np.uint8)
+    wf = [big[0], big[1], bad, big[2]]
+    reset = [True, True, True, False]
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] == 1 and wst["err_file"] == 2
+    got, gst = g.replay(wf, reset)
+    assert_same(got, gst, want, wst)
+    assert gst["files_walked"] == wst["files_walked"] == 3
