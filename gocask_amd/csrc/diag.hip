@@ -9,14 +9,24 @@
 
 namespace gck {
 
+template <bool NT = false>
+__device__ __forceinline__ uint4 ld16(const uint4 *p) {
+    if constexpr (NT) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else
+        return *p;
+}
+template <bool NT = false>
 __global__ __launch_bounds__(256) void k_stream_read(const uint4 *__restrict__ p, uint64_t n16, uint32_t *sink) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
     uint32_t acc = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; i < n16; i += stride) {
-        uint4 a = p[i];
-        uint4 b = i + 256 < n16 ? p[i + 256] : make_uint4(0, 0, 0, 0);
-        uint4 c = i + 512 < n16 ? p[i + 512] : make_uint4(0, 0, 0, 0);
-        uint4 d = i + 768 < n16 ? p[i + 768] : make_uint4(0, 0, 0, 0);
+        uint4 a = ld16<NT>(p + i);
+        uint4 b = i + 256 < n16 ? ld16<NT>(p + i + 256) : make_uint4(0, 0, 0, 0);
+        uint4 c = i + 512 < n16 ? ld16<NT>(p + i + 512) : make_uint4(0, 0, 0, 0);
+        uint4 d = i + 768 < n16 ? ld16<NT>(p + i + 768) : make_uint4(0, 0, 0, 0);
         acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
     }
     if (acc == 0x9E3779B9u) sink[0] = acc;  // practically never: keeps the loads live
@@ -87,27 +97,29 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t *__restrict__ arena
 
 using namespace gck;
 
-// pattern 0: k_stream_read; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>;
+// pattern 0: k_stream_read; 15: the same with non-temporal loads; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>;
 // 3..8: k_chase<dependent> with 8 Ki << (pattern-3) lanes; 9..14: the same
 // lane counts, independent loads.  The chase patterns make 10,240,000 hops in
 // all (C3's record count); *gbs reports hops per ns (G hops/s) for them.
 extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs) {
-    if (!ctx || iters <= 0 || pattern < 0 || pattern > 14) return GCK_EINVAL;
+    if (!ctx || iters <= 0 || pattern < 0 || pattern > 15) return GCK_EINVAL;
     Ctx *c = &ctx->c;
     GCK_HIP(hipSetDevice(c->device));
     if (!c->n_rows) return GCK_EINVAL;
     uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
-    const uint32_t lanes = pattern >= 3 ? 8192u << ((pattern - 3) % 6) : 0u;
+    const uint32_t lanes = pattern >= 3 && pattern <= 14 ? 8192u << ((pattern - 3) % 6) : 0u;
     const uint32_t hops = lanes ? ((10240000u / lanes + 7) & ~7u) : 0u;
     auto launch = [&]() {
-        if (pattern >= 9)
+        if (pattern == 15)
+            k_stream_read<true><<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
+        else if (pattern >= 9)
             k_chase<false><<<(lanes + 255) / 256, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), c->arena_len, lanes, hops,
                                                                       sink);
         else if (pattern >= 3)
             k_chase<true><<<(lanes + 255) / 256, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), c->arena_len, lanes, hops,
                                                                      sink);
         else if (pattern == 0)
-            k_stream_read<<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
+            k_stream_read<false><<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
         else if (pattern == 1)
             k_stream_rows<true><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
         else
@@ -142,9 +154,9 @@ extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
-    k_stream_read<<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);  // warm-up
+    k_stream_read<false><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);  // warm-up
     GCK_HIP(hipEventRecord(a, c->stream));
-    for (int i = 0; i < iters; ++i) k_stream_read<<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
+    for (int i = 0; i < iters; ++i) k_stream_read<false><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
     GCK_HIP(hipEventRecord(b, c->stream));
     GCK_HIP(hipEventSynchronize(b));
     float ms = 0;

@@ -697,6 +697,10 @@ __global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint2 *_
 
 constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
 constexpr int kBlockRows = 64;   // rows per plan block = per k_crc_rows work item
+// cache policy of k_crc_rows' arena loads (buffer aux bits: 1 sc0, 2 nt, 16 sc1)
+#ifndef GCK_ARENA_AUX
+#define GCK_ARENA_AUX 0
+#endif
 #ifndef GCK_CLAIM
 #define GCK_CLAIM 2
 #endif
@@ -892,10 +896,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         for (int i = 0; i < NR; ++i) {
             const uint64_t r = min(row0 + i, n_rows - 1);
             const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
-            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel, 0, 0);
-            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 16, 0, 0);
-            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 32, 0, 0);
-            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 48, 0, 0);
+            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel, 0, GCK_ARENA_AUX);
+            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 16, 0, GCK_ARENA_AUX);
+            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 32, 0, GCK_ARENA_AUX);
+            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 48, 0, GCK_ARENA_AUX);
         }
     };
     // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
@@ -1102,6 +1106,35 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
     }
     return p;
 }
+// a * b mod P for a per-lane b and any a, by a 4-bit window over a:
+// M[v] = b * (v3 + v2 x + v1 x^2 + v0 x^3) (v = a nibble, its bit 3 the lower
+// power) in a wave-private LDS table, entry-major (entry v of lane l at
+// byte mw + 256 v + 4 l: each lane of a 32-lane group on its own bank), then
+// Horner from the highest-degree nibble with y * x^4 = (y >> 4) ^ R[y & 15].
+// About 60 VALU + 15 LDS writes + 15 LDS reads, against 160 VALU for gf_mul.
+// M[0] must be zero (written once per kernel); mw = the wave's region + 4 lane.
+__device__ __forceinline__ uint32_t mulx(uint32_t v) {
+    return (v >> 1) ^ (kPoly & (uint32_t)(-(int32_t)(v & 1u)));
+}
+__device__ __forceinline__ uint32_t gf_mul_lds(char *lds, uint32_t mw, uint32_t rb, uint32_t a, uint32_t b) {
+    const uint32_t m8 = b, m4 = mulx(m8), m2 = mulx(m4), m1 = mulx(m2);
+    const uint32_t m[16] = {0u, m1, m2, m1 ^ m2, m4, m4 ^ m1, m4 ^ m2, m4 ^ m2 ^ m1,
+                            m8, m8 ^ m1, m8 ^ m2, m8 ^ m2 ^ m1, m8 ^ m4, m8 ^ m4 ^ m1, m8 ^ m4 ^ m2, m8 ^ m4 ^ m2 ^ m1};
+#pragma unroll
+    for (int v = 1; v < 16; ++v) *reinterpret_cast<uint32_t *>(lds + mw + 256 * v) = m[v];
+    auto ent = [&](int t) {  // M[nibble t of a] (t = 7: bits 3..0, the highest powers)
+        const int sh = 20 - 4 * t;
+        const uint32_t x = sh >= 0 ? a >> sh : a << -sh;
+        return *reinterpret_cast<const uint32_t *>(lds + ((x & 0xF00u) | mw));
+    };
+    uint32_t y = ent(7);
+#pragma unroll
+    for (int t = 6; t >= 0; --t) {
+        const uint32_t r = *reinterpret_cast<const uint32_t *>(lds + (rb | ((y << 2) & 0x3Cu)));
+        y = xor3(y >> 4, r, ent(t));
+    }
+    return y;
+}
 __device__ __forceinline__ uint32_t z4096(const uint32_t *Tz, uint32_t a) {
     return Tz[a & 0xFF] ^ Tz[256 + ((a >> 8) & 0xFF)] ^ Tz[512 + ((a >> 16) & 0xFF)] ^ Tz[768 + (a >> 24)];
 }
@@ -1136,109 +1169,150 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                                                   const uint32_t *__restrict__ carry, const uint64_t *__restrict__ rng,
                                                   const uint2 *__restrict__ ep, const uint32_t *__restrict__ rend,
                                                   const uint32_t *__restrict__ g_slice,
-                                                  const uint32_t *__restrict__ xinv, const uint32_t *__restrict__ xfw,
+                                                  const uint32_t *__restrict__ xinv,
                                                   const uint32_t *__restrict__ zrow,
                                                   const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
+    // gf_mul_lds: one 4 KiB table region per wave, then y * x^4 = (y >> 4) ^ R[y & 15]
+    __shared__ uint32_t Gm[4 * 1024 + 16];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
         Tz[i] = zrow[i];
         T[i] = g_slice[i];
     }
+    if (threadIdx.x < 16) Gm[4096 + threadIdx.x] = mulx(mulx(mulx(mulx(threadIdx.x))));
+    Gm[(threadIdx.x >> 6) * 1024 + (threadIdx.x & 63)] = 0;  // entry 0 of every lane
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
+    char *const ldsb = reinterpret_cast<char *>(Gm);  // byte offsets into Gm
+    const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = 4096 * 4;
     const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
     uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
-    // wave-uniform loop: the 64 lanes hold 64 consecutive records
-    for (uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < re; base += G) {
+    // wave-uniform loop: the 64 lanes hold 64 consecutive records.  Loads in
+    // three waves per iteration: the record table of this iteration (issued
+    // one iteration ahead), then every load that depends on it at once (header
+    // and key bytes, the end block where no neighbour provides ft, row sums,
+    // shift tables), then the next iteration's record table, so the compute
+    // below waits for one memory round trip per iteration.
+    struct Rec {
+        uint64_t rs;
+        uint2 kv;       // (KeySize, ValueSize)
+        uint32_t f;
+        uint2 ep;       // (c, pre) of the record's end block
+        uint32_t f0;    // rec_file / ep of the record before the wave's first
+        uint2 ep0;
+    };
+    auto load_rec = [&](uint64_t base, Rec &o) {
+        const uint64_t r = min(base + lane, re - 1), r0 = base ? base - 1 : 0;
+        o.rs = rec_off[r];
+        o.kv = rec_kv[r];
+        o.f = rec_file[r];
+        o.ep = ep[r];
+        o.f0 = base ? rec_file[r0] : 0xFFFFFFFFu;
+        o.ep0 = ep[r0];
+    };
+    uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    Rec cur;
+    if (base < re) load_rec(base, cur);
+    for (; base < re; base += G) {
         const uint64_t r_ = base + lane;
         const bool valid = r_ < re;
         const uint64_t r = valid ? r_ : re - 1;
-        const uint64_t rs = rec_off[r];
-        const uint2 kv = rec_kv[r];  // (KeySize, ValueSize)
-        const uint32_t f = rec_file[r];
-        const uint32_t V = kv.y;
+        const uint64_t rs = cur.rs;
+        const uint2 kv = cur.kv;
+        const uint32_t f = cur.f, V = kv.y;
         const uint64_t vs = rs + 16 + kv.x, ve = vs + V;
-        // ft of the previous record (same file: its end is rs), from the 16 B
-        // block holding byte rs - 1
-        const bool prev_same = rs != fbase[f];
-        const uint64_t bsp = prev_same ? (rs - 1) & ~15ull : rs;
-        const uint4 vp = *reinterpret_cast<const uint4 *>(arena + bsp);
-        const uint2 ep_prev = prev_same ? ep[r - 1] : make_uint2(0u, 0u);
-        const uint32_t e_prev = ep_prev.x, pre_prev = ep_prev.y;
-        const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
-        // A(rs) (0 when rs starts a row)
-        const uint32_t dp = (uint32_t)(((rs + kRow - 1) & ~(uint64_t)(kRow - 1)) - rs);
-        const uint32_t a_rs = (prev_same && dp) ? pre_prev ^ gf_mul(xfw[dp], ft_prev) : 0u;
-        // ft of this record: from lane + 1 if that lane holds record r + 1 of the same file
+        // the previous record (r - 1): lane - 1's, or the wave's extra one
+        const uint32_t f_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.f0, (int)f, 0x138, 0xF, 0xF, false);
+        const uint32_t e_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.ep0.x, (int)cur.ep.x, 0x138, 0xF, 0xF, false);
+        const uint32_t pre_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.ep0.y, (int)cur.ep.y, 0x138, 0xF, 0xF, false);
+        // records of a file are contiguous in walk order; lanes past the range
+        // repeat the last record and have no predecessor
+        const bool prev_same = valid && f_prev == f;
+        // ft of this record comes from lane + 1 if that lane holds record r + 1 of the same file
         const uint64_t nb_same = __ballot(valid && prev_same);
-        const uint32_t ft_next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ft_prev, 0x130, 0xF, 0xF, false);  // wave_shl:1
         const bool have = lane < 63 && ((nb_same >> (lane + 1)) & 1);
-        const uint2 ep_own = ep[r];
-        uint32_t ft = ft_next;
-        if (!have) {
-            const uint64_t bse = (ve - 1) & ~15ull;
-            ft = crc_block(T, ep_own.x, *reinterpret_cast<const uint4 *>(arena + bse), (uint32_t)(ve - bse));
-        }
-        const uint32_t e_pre = ep_own.y;
-        // Horner over the rows the record crosses
+        const uint64_t bsp = prev_same ? (rs - 1) & ~15ull : rs, bse = (ve - 1) & ~15ull;
         const uint64_t fr = rs / kRow, lr = (ve - 1) / kRow;
         const uint32_t d = (uint32_t)((lr + 1) * kRow - ve);
-        // acc = the record's bytes of its rows, referenced to the end row's
-        // end, without the last block's ft (added back unshifted below)
-        uint32_t acc = e_pre;
-        if (fr == lr) {
-            acc ^= a_rs;
-        } else {
-            uint32_t h_acc = rend[fr] ^ a_rs;
-            for (uint64_t row = fr + 1; row < lr; row += 8) {
-                uint32_t v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = row + j < lr ? rend[row + j] : 0u;
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (row + j < lr) h_acc = z4096(Tz, h_acc) ^ v[j];
-            }
-            acc ^= z4096(Tz, h_acc);
-        }
-        // F(0, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
-        const uint32_t chain = ft ^ gf_mul(xinv[d], acc);
-        // F(0, prefix): header + key bytes [rs, vs) as aligned words from
-        // rs & ~3, the bytes before rs masked to zero (F ignores leading zeros)
         const uint64_t w0 = rs & ~3ull;
-        const uint32_t lead = (uint32_t)(rs & 3), L = (uint32_t)(vs - w0);
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
+        // ---- every dependent load of this iteration
+        const uint4 vp = *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
         uint32_t pw[11];
 #pragma unroll
         for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
+        uint4 vend = make_uint4(0, 0, 0, 0);
+        if (!have) vend = *reinterpret_cast<const uint4 *>(arena + bse);
+        uint32_t rr[9];  // row sums rend[fr .. fr + 8] the record crosses
+#pragma unroll
+        for (int j = 0; j < 9; ++j) rr[j] = fr + j < lr ? rend[fr + j] : 0u;
+        const uint32_t xi = xinv[d], xv0 = xb[V & 0xFFFF], xhi = xa[V >> 16];
+        const uint32_t zlv = zl[min(V, (1u << 17) - 1)];
+        const uint32_t cf = carry[f];
+        const uint64_t fb = fbase[f];
+        // ---- the next iteration's record table
+        Rec nxt;
+        if (base + G < re) load_rec(base + G, nxt);
+        // ---- compute
+        const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
+        // A(rs) = pre_prev ^ Z_{E-rs}(ft_prev) (0 when rs starts a row).  Only
+        // pre_prev enters the row sums: they then give F(s, [rs, ve)) with
+        // s = ft_prev, and the header + key CRC below starts from s too, so
+        // F(0, value) = F(s, [rs, ve)) ^ Z_V(F(s, [rs, vs))) needs no shift of s.
+        const bool mid = prev_same && (rs & (kRow - 1)) != 0;
+        const uint32_t a_rs = mid ? pre_prev : 0u, s0 = mid ? ft_prev : 0u;
+        const uint32_t ft_next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ft_prev, 0x130, 0xF, 0xF, false);  // wave_shl:1
+        const uint32_t ft = have ? ft_next : crc_block(T, cur.ep.x, vend, (uint32_t)(ve - bse));
+        // acc = the record's bytes of its rows, referenced to the end row's
+        // end, without the last block's ft (added back unshifted below)
+        uint32_t acc = cur.ep.y;
+        if (fr == lr) {
+            acc ^= a_rs;
+        } else {
+            uint32_t h_acc = rr[0] ^ a_rs;
+#pragma unroll
+            for (int j = 1; j < 9; ++j)
+                if (fr + j < lr) h_acc = z4096(Tz, h_acc) ^ rr[j];
+            for (uint64_t row = fr + 9; row < lr; ++row) h_acc = z4096(Tz, h_acc) ^ rend[row];  // records over 36 KiB
+            acc ^= z4096(Tz, h_acc);
+        }
+        // F(s, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
+        const uint32_t chain = ft ^ gf_mul_lds(ldsb, mw, rxb, xi, acc);
+        // F(s, prefix): header + key bytes [rs, vs) as aligned words from
+        // rs & ~3; the first word's bytes before rs are shifted out
+        // (partial_word over its last 4 - lead bytes)
+        const uint32_t lead = (uint32_t)(rs & 3), L = (uint32_t)(vs - w0);
         const uint32_t hcrc = ab(pw[1], pw[0], lead), hts = ab(pw[2], pw[1], lead);  // header CRC, Timestamp
-        pw[0] &= ~0u << (8 * lead);
+        // word 0: F(s0, its bytes lead..3) = (s0 >> 8nb) ^ slice4((s0 ^ w >> 8 lead) << 8 lead), nb = 4 - lead
+        uint32_t p = slice4t(T, (s0 ^ (pw[0] >> (8 * lead))) << (8 * lead)) ^ (lead ? s0 >> (32 - 8 * lead) : 0u);
         // unrolled over the words in registers (no indexed register array),
         // then the words of long keys from memory
         const uint32_t nw = L / 4;
-        uint32_t p = 0, y = 0;
+        uint32_t y = 0;
 #pragma unroll
-        for (uint32_t i = 0; i < 11; ++i) {
+        for (uint32_t i = 1; i < 11; ++i) {
             if (i < nw) p = slice4t(T, p ^ pw[i]);
             y = i == nw ? pw[i] : y;
         }
         for (uint32_t i = 11; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
         if (nw >= 11) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
-        const uint32_t xv = V < 65536 ? xb[V] : gf_mul(xa[V >> 16], xb[V & 0xFFFF]);
-        const uint32_t raw0 = chain ^ gf_mul(xv, p);
-        const uint32_t z = V < (1u << 17) ? zl[V] : gf_mul(xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        // x^(8V) = xa[V >> 16] * xb[V & 0xFFFF]; crc32(0^V) from zl below 2^17
+        const uint32_t xv = V < 65536 ? xv0 : gf_mul_lds(ldsb, mw, rxb, xhi, xv0);
+        const uint32_t raw0 = chain ^ gf_mul_lds(ldsb, mw, rxb, xv, p);
+        const uint32_t z = V < (1u << 17) ? zlv : gf_mul_lds(ldsb, mw, rxb, xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         const uint32_t calc = raw0 ^ z;
         if (valid) {
-            const uint64_t fo = rs - fbase[f];
+            const uint64_t fo = rs - fb;
             const bool tomb = kv.x == 0;
             gck_rec o;
             o.rec_off = fo;
             o.file = f;
             o.key_len = tomb ? kv.y : kv.x;
-            o.value_pos = carry[f] + (uint32_t)fo + 16u + kv.x;
+            o.value_pos = cf + (uint32_t)fo + 16u + kv.x;
             o.value_size = kv.y;
             o.crc = hcrc;
             o.ts = hts;
@@ -1247,6 +1321,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
             out[r] = o;
             n_rej += calc != hcrc;
         }
+        cur = nxt;
     }
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
@@ -1603,7 +1678,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
     k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
-                                    c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(), c->d_xfw.as<uint32_t>(),
+                                    c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
                                     c->d_zrow.as<uint32_t>(),
                                     c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
