@@ -10,7 +10,7 @@
 //   k_scan_chunks  record slot per chunk (exclusive scan), per-file summary
 //   (host)         EOF classification, lastOffset carries (core/db.go:117)
 //   k_compact      record table (arena offset + header), walk order
-//   k_row_index    first record touching each 4 KiB row
+//   k_row_tail     first record touching each 4 KiB row (with k_compact)
 //   k_crc_rows     HBM-bound: every byte once, CRC partials of every value
 //   k_finalize     CRC verdict, ValuePos (u32 wrap), gck_rec tuples
 #include <chrono>
@@ -593,10 +593,18 @@ __global__ void k_account(uint32_t nf, const uint64_t *__restrict__ flen, const 
     res[5] = n_total;
 }
 
+// row_first[row] = the first record whose value ends after the row's first
+// byte.  Record r sets the rows from its start to its end, [ceil(rs / 4 KiB),
+// ceil(ve / 4 KiB)); k_row_tail sets the rows after a file's last record.
+__device__ __forceinline__ void set_row_first(uint32_t *row_first, uint64_t r, uint64_t rs, uint64_t ve) {
+    for (uint64_t row = (rs + kRow - 1) / kRow; row < (ve + kRow - 1) / kRow; ++row) row_first[row] = (uint32_t)r;
+}
+
 struct DirectEmit {
     uint64_t *rec_off;
     uint2 *rec_kv;
     uint32_t *rec_file;
+    uint32_t *row_first;
     uint64_t rb, n_total, base;
     uint32_t f;
     __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
@@ -605,6 +613,7 @@ struct DirectEmit {
             rec_off[r] = base + p;
             rec_kv[r] = make_uint2(h.ks, h.vs);
             rec_file[r] = f;
+            set_row_first(row_first, r, base + p, base + p + 16 + (uint64_t)h.ks + h.vs);
         }
     }
     __device__ void prime() const {}
@@ -626,7 +635,8 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   const uint64_t *__restrict__ rec_base,
                                                   const uint2 *__restrict__ s_kv, uint32_t cap,
                                                   uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
-                                                  uint2 *rec_kv, uint32_t *rec_file, uint32_t *counters) {
+                                                  uint2 *rec_kv, uint32_t *rec_file, uint32_t *row_first,
+                                                  uint32_t *counters) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
     if (c >= n_chunks) return;
@@ -648,16 +658,18 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
             const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
             const uint64_t r = rb + i;
             if (in && r < n_total) {
-                rec_off[r] = run + (((uint64_t)hi << 24) + lo) - e;
+                const uint64_t ve = run + (((uint64_t)hi << 24) + lo);
+                rec_off[r] = ve - e;
                 rec_kv[r] = kv;
                 rec_file[r] = f;
+                set_row_first(row_first, r, ve - e, ve);
             }
             run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
                    (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
         }
     } else if (lane == 0) {
         atomicAdd(&counters[2], 1u);
-        DirectEmit em{rec_off, rec_kv, rec_file, rb, n_total, base, f};
+        DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb, n_total, base, f};
         uint32_t count, term;
         uint64_t exit, tpos;
         walk_chain(arena, base, flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
@@ -683,16 +695,22 @@ __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64
         row_first[row] = v;
 }
 
-__global__ void k_row_index(const uint64_t *__restrict__ rec_off, const uint2 *__restrict__ rec_kv,
-                            const uint64_t *__restrict__ rng, uint64_t r0, uint32_t *__restrict__ row_first) {
-    const uint64_t rb = rng[0], re = rng[1];
-    for (uint64_t r = rb + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < re;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t ve_r = value_end(rec_off, rec_kv, r);
-        const uint64_t lo = r == rb ? r0 : (value_end(rec_off, rec_kv, r - 1) + kRow - 1) / kRow;
-        const uint64_t hi = (ve_r + kRow - 1) / kRow;
-        for (uint64_t row = lo; row < hi; ++row) row_first[row] = (uint32_t)r;
-    }
+// Rows after file f's last record, up to the next file's first row, get the
+// next record: ffirst[f] + fnrec[f] (the rows of records are set by
+// k_compact).  The last record ends at the file's length, or where its walk
+// stopped (EOF class or startup error, as k_account).  Files whose records
+// all lie past the run's range keep k_row_fill's value.  One workgroup per file.
+__global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *__restrict__ flen,
+                           const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
+                           const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec, uint32_t nf,
+                           uint64_t n_rows, const uint64_t *__restrict__ rng, uint32_t *__restrict__ row_first) {
+    const uint32_t f = blockIdx.x;
+    const uint64_t re = rng[1];
+    if (f >= nf || ffirst[f] >= re) return;
+    const uint64_t end = fbase[f] + (fterm[f] != T_NONE ? ftpos[f] : flen[f]);
+    const uint64_t r1 = f + 1 < nf ? fbase[f + 1] / kRow : n_rows;
+    const uint32_t v = (uint32_t)min(ffirst[f] + fnrec[f], re);
+    for (uint64_t row = (end + kRow - 1) / kRow + threadIdx.x; row < r1; row += blockDim.x) row_first[row] = v;
 }
 
 constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
@@ -716,7 +734,7 @@ constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the re
 //   of slab k, i.e. in row bytes [64k + 16b, 64k + 16b + 16).  A 16 B block
 //   holds at most one record end: records are at least 16 B (a bare header).
 // The first record whose end lies past a row's start is row_first[row]
-// (k_row_index); record ids of the ends follow from it and a count over the
+// (k_compact, k_row_tail); record ids of the ends follow from it and a count over the
 // lanes, so the plan carries no ids.
 //
 // One wavefront per block: the records ending in its rows are a contiguous
@@ -1369,7 +1387,7 @@ __global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ are
 
 // ------------------------------------------------------------- host side ---
 static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib, std::vector<uint32_t> &xinv,
-                        std::vector<uint32_t> &xfw, std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
+                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
                         std::vector<uint32_t> &zl) {
     slice.assign(4 * 256, 0);
     for (uint32_t n = 0; n < 256; ++n) {
@@ -1391,9 +1409,6 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
     xinv.assign(kRow, 0);
     xinv[0] = kX0;
     for (int d = 1; d < kRow; ++d) xinv[d] = multmodp(xinv[d - 1], xinv8);
-    xfw.assign(kRow, 0);  // x^(8d): forward shifts inside a row
-    xfw[0] = kX0;
-    for (int d = 1; d < kRow; ++d) xfw[d] = multmodp(xfw[d - 1], kX0 >> 8);
     xa.assign(65536, 0);
     xb.assign(65536, 0);
     xa[0] = xb[0] = kX0;
@@ -1456,15 +1471,15 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     // the constant tables are the same for every context: built once per process
     struct Tables {
-        std::vector<uint32_t> slice, nib, xinv, xfw, xa, xb, zrow, zl;
-        Tables() { make_tables(slice, nib, xinv, xfw, xa, xb, zrow, zl); }
+        std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow, zl;
+        Tables() { make_tables(slice, nib, xinv, xa, xb, zrow, zl); }
     };
     static const Tables tabs;
-    const std::vector<uint32_t> &slice = tabs.slice, &nib = tabs.nib, &xinv = tabs.xinv, &xfw = tabs.xfw,
+    const std::vector<uint32_t> &slice = tabs.slice, &nib = tabs.nib, &xinv = tabs.xinv,
                                 &xa = tabs.xa, &xb = tabs.xb, &zrow = tabs.zrow, &zl = tabs.zl;
     int rc;
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
-        (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xfw.ensure(xfw.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
+        (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
         (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(128)))
         return rc;
@@ -1473,7 +1488,6 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipMemcpy(c->d_slice.p, slice.data(), slice.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xinv.p, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
-    GCK_HIP(hipMemcpy(c->d_xfw.p, xfw.data(), xfw.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xa.p, xa.data(), xa.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xb.p, xb.data(), xb.size() * 4, hipMemcpyHostToDevice));
     return GCK_OK;
@@ -1485,7 +1499,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
-                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xfw, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
+                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
@@ -1635,6 +1649,8 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
 static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
                            const uint64_t *rng, uint64_t cap) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
+    const uint32_t grid = (uint32_t)c->n_cu * 4;
+    k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
     if (n)
         k_compact<<<nblk(n, 16), 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                              c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
@@ -1642,11 +1658,13 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_rec_base.as<uint64_t>() + c0,
                                              c->d_stage.as<uint2>(), ccap, n, cap,
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
-                                             c->d_rec_file.as<uint32_t>(), c->d_counters.as<uint32_t>());
-    const uint32_t grid = (uint32_t)c->n_cu * 4;
-    k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
-    k_row_index<<<grid, 256, 0, s>>>(c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), rng, r0,
-                                     c->d_row_first.as<uint32_t>());
+                                             c->d_rec_file.as<uint32_t>(), c->d_row_first.as<uint32_t>(),
+                                             c->d_counters.as<uint32_t>());
+    if (c->nfiles)
+        k_row_tail<<<c->nfiles, 256, 0, s>>>(c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
+                                             c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
+                                             c->d_fnrec.as<uint64_t>(), c->nfiles, c->n_rows, rng,
+                                             c->d_row_first.as<uint32_t>());
     if (r1 > r0)
         k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
             c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
