@@ -1196,6 +1196,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
     // gf_mul_lds: one 4 KiB table region per wave, then y * x^4 = (y >> 4) ^ R[y & 15]
     __shared__ uint32_t Gm[4 * 1024 + 16];
+    // output staging: a wave's 64 gck_rec (2560 B), stored back as 16 B per lane
+    __shared__ uint4 Ost[4][64 * sizeof(gck_rec) / 16];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
         Tz[i] = zrow[i];
         T[i] = g_slice[i];
@@ -1237,7 +1239,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
     for (; base < re; base += G) {
         const uint64_t r_ = base + lane;
         const bool valid = r_ < re;
-        const uint64_t r = valid ? r_ : re - 1;
         const uint64_t rs = cur.rs;
         const uint2 kv = cur.kv;
         const uint32_t f = cur.f, V = kv.y;
@@ -1258,17 +1259,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint64_t w0 = rs & ~3ull;
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
         // ---- every dependent load of this iteration
-        const uint4 vp = *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
+#ifndef GCK_FIN_XP
+#define GCK_FIN_XP 0  // ablation (timing only, wrong results): 1 no arena loads, 2 no table loads, 4 no stores, 8 no row sums
+#endif
+        const uint4 vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)rs, (uint32_t)bsp, V, f)
+                                          : *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
         uint32_t pw[11];
 #pragma unroll
-        for (int i = 0; i < 11; ++i) pw[i] = wp[i];  // header + keys up to 24 B (the arena is padded)
+        for (int i = 0; i < 11; ++i) pw[i] = (GCK_FIN_XP & 1) ? (uint32_t)rs * (i + 3) : wp[i];  // header + keys up to 24 B (the arena is padded)
         uint4 vend = make_uint4(0, 0, 0, 0);
-        if (!have) vend = *reinterpret_cast<const uint4 *>(arena + bse);
+        if (!have) vend = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)bse, 1, 2, 3) : *reinterpret_cast<const uint4 *>(arena + bse);
         uint32_t rr[9];  // row sums rend[fr .. fr + 8] the record crosses
 #pragma unroll
-        for (int j = 0; j < 9; ++j) rr[j] = fr + j < lr ? rend[fr + j] : 0u;
-        const uint32_t xi = xinv[d], xv0 = xb[V & 0xFFFF], xhi = xa[V >> 16];
-        const uint32_t zlv = zl[min(V, (1u << 17) - 1)];
+        for (int j = 0; j < 9; ++j) rr[j] = fr + j < lr ? ((GCK_FIN_XP & 8) ? (uint32_t)fr * 7 + j : rend[fr + j]) : 0u;
+        const uint32_t xi = (GCK_FIN_XP & 2) ? d * 0x9E3779B9u : xinv[d];
+        const uint32_t xv0 = (GCK_FIN_XP & 2) ? V * 0x85EBCA6Bu : xb[V & 0xFFFF];
+        const uint32_t xhi = (GCK_FIN_XP & 2) ? (V >> 16) + 1 : xa[V >> 16];
+        const uint32_t zlv = (GCK_FIN_XP & 2) ? V ^ 0xC2B2AE35u : zl[min(V, (1u << 17) - 1)];
         const uint32_t cf = carry[f];
         const uint64_t fb = fbase[f];
         // ---- the next iteration's record table
@@ -1323,21 +1330,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint32_t raw0 = chain ^ gf_mul_lds(ldsb, mw, rxb, xv, p);
         const uint32_t z = V < (1u << 17) ? zlv : gf_mul_lds(ldsb, mw, rxb, xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         const uint32_t calc = raw0 ^ z;
-        if (valid) {
+        {
+            // The wave's records are consecutive gck_recs (40 B each): staged in
+            // LDS, then stored as 16 B per lane, 1 KiB contiguous per instruction
+            // (three 8/16 B stores per lane at a 40 B stride write partial lines)
             const uint64_t fo = rs - fb;
             const bool tomb = kv.x == 0;
-            gck_rec o;
-            o.rec_off = fo;
-            o.file = f;
-            o.key_len = tomb ? kv.y : kv.x;
-            o.value_pos = cf + (uint32_t)fo + 16u + kv.x;
-            o.value_size = kv.y;
-            o.crc = hcrc;
-            o.ts = hts;
-            o.flags = (tomb ? GCK_F_TOMBSTONE : 0u) | (calc == hcrc ? GCK_F_CRC_OK : 0u);
-            o.crc_calc = calc;
-            out[r] = o;
-            n_rej += calc != hcrc;
+            uint2 *sl = reinterpret_cast<uint2 *>(reinterpret_cast<char *>(Ost[threadIdx.x >> 6]) + lane * sizeof(gck_rec));
+            sl[0] = make_uint2((uint32_t)fo, (uint32_t)(fo >> 32));                    // rec_off
+            sl[1] = make_uint2(f, tomb ? kv.y : kv.x);                                 // file, key_len
+            sl[2] = make_uint2(cf + (uint32_t)fo + 16u + kv.x, kv.y);                  // value_pos, value_size
+            sl[3] = make_uint2(hcrc, hts);                                             // crc, ts
+            sl[4] = make_uint2((tomb ? GCK_F_TOMBSTONE : 0u) | (calc == hcrc ? GCK_F_CRC_OK : 0u), calc);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t nbytes = (uint32_t)min(re - base, (uint64_t)64) * (uint32_t)sizeof(gck_rec);
+            char *dst = reinterpret_cast<char *>(out + base);
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k) {
+                const uint32_t off = k * 1024 + lane * 16;
+                const uint4 v = Ost[threadIdx.x >> 6][off / 16];
+                if (off + 16 <= nbytes) {
+                    if (!(GCK_FIN_XP & 4)) *reinterpret_cast<u32x4_a4 *>(dst + off) = u32x4_a4{v.x, v.y, v.z, v.w};
+                } else if (off < nbytes) {  // an odd record count ends mid-chunk
+                    if (!(GCK_FIN_XP & 4)) *reinterpret_cast<uint2 *>(dst + off) = make_uint2(v.x, v.y);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            n_rej += valid && calc != hcrc;
         }
         cur = nxt;
     }
