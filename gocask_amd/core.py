@@ -266,6 +266,11 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0):
                 n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset, files_walked=res.files_walked)
 
 
+def release_cache():
+    """gck_replay_release_cache: free the device contexts gck_replay keeps."""
+    _lib.load().gck_replay_release_cache()
+
+
 def keydir(files, recs):
     """Apply the tuples in walk order (core/keydir.go:22-49): {key: record row}."""
     kd = {}

@@ -61,6 +61,10 @@ enum Phase {
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // end-of-run counters and results land here by a kernel's PCIe writes
+    // (coherent pinned host memory, mapped): no DMA-engine copy, which would
+    // queue behind any large H2D already queued (gck_replay's file groups)
+    uint32_t *h_mbox = nullptr, *d_mbox = nullptr;
     gck_opts opts{};
     int n_cu = 256;
     int fin_blocks_per_cu = 4;  // resident k_finalize workgroups per CU

@@ -1502,6 +1502,13 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
         (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(128)))
         return rc;
+    {
+        void *hp = nullptr, *dp = nullptr;
+        GCK_HIP(hipHostMalloc(&hp, 128, hipHostMallocMapped | hipHostMallocCoherent));
+        c->h_mbox = static_cast<uint32_t *>(hp);
+        GCK_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+        c->d_mbox = static_cast<uint32_t *>(dp);
+    }
     GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_slice.p, slice.data(), slice.size() * 4, hipMemcpyHostToDevice));
@@ -1525,6 +1532,8 @@ static void ctx_free(Ctx *c) {
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
                    &c->d_gvoff, &c->d_gvals};
     for (DBuf *b : all) b->release();
+    if (c->h_mbox) (void)hipHostFree(c->h_mbox);
+    c->h_mbox = c->d_mbox = nullptr;
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t *st : {&c->stream}) {
@@ -1863,6 +1872,11 @@ static int ctx_run_host(Ctx *c) {
     return c->status;
 }
 
+// 32 counters / results of a run into the mapped mailbox (Ctx::h_mbox)
+__global__ void k_publish(const uint32_t *__restrict__ cnt, uint32_t *mbox) {
+    __hip_atomic_store(mbox + threadIdx.x, cnt[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The same run with no host round trip, for a context whose record table
 // was sized by an earlier run (repeated replays of a resident arena): the
 // bookkeeping runs on the device (k_account), the record table is clamped to
@@ -1897,10 +1911,11 @@ static int ctx_run_device(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, cap);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
-    uint32_t h[32] = {};
-    GCK_HIP(hipMemcpyAsync(h, cnt, 128, hipMemcpyDeviceToHost, s));
+    k_publish<<<1, 32, 0, s>>>(cnt, c->d_mbox);
     GCK_HIP(hipStreamSynchronize(s));
     GCK_HIP(hipGetLastError());
+    uint32_t h[32];
+    memcpy(h, c->h_mbox, 128);
     const uint64_t *hr = reinterpret_cast<const uint64_t *>(h + 16);
     if (h[CNT_VAL + kRounds] != 0 || h[CNT_CAP] != 0 || hr[5] > cap) return GCK_ERERUN;
     c->status = (int32_t)hr[0];
@@ -2085,6 +2100,73 @@ __global__ void k_rebase_file(gck_rec *recs, uint64_t n, uint32_t base) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         recs[i].file += base;
 }
+// The group's tuples straight into the caller's pinned array (its device
+// mapping) by the GPU's own PCIe writes, file indices rebased on the way:
+// no DMA-engine copy, so it never queues behind the H2D of later groups.
+// 16 B per lane; two records are 80 B = 5 uint4, the file field (bytes 8..11
+// of a record) is .z of uint4 5m and .x of uint4 5m + 3.
+__global__ void k_push_recs(const uint4 *__restrict__ src, uint4 *__restrict__ dst, uint64_t n_rec, uint32_t base) {
+    const uint64_t bytes = n_rec * sizeof(gck_rec), n16 = bytes / 16;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i * 16 < bytes;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint4 v = src[i];
+        const uint32_t m = (uint32_t)(i % 5);
+        if (m == 0) v.z += base;
+        if (m == 3) v.x += base;
+        if (i < n16)
+            dst[i] = v;
+        else  // an odd record count ends 8 B into the last uint4
+            *reinterpret_cast<uint2 *>(dst + i) = make_uint2(v.x, v.y);
+    }
+}
+
+// Contexts of the grouped replay are kept for the next call (per device and
+// options): their arenas and tables stay allocated, so a repeated Open pays
+// no hipMalloc and no table upload.  gck_replay_release_cache frees them.
+namespace {
+struct PoolEntry {
+    gck_opts key;
+    gck_ctx *ctx;
+};
+std::mutex g_pool_mu;
+std::vector<PoolEntry> g_pool;
+gck_opts pool_key(const gck_opts *o) {
+    gck_opts k{};
+    if (o) k = *o;
+    return k;
+}
+bool same_opts(const gck_opts &a, const gck_opts &b) {
+    return a.device == b.device && a.chunk_bytes == b.chunk_bytes && a.max_key == b.max_key &&
+           a.chunk_cap == b.chunk_cap && a.spec_window == b.spec_window && a.flags == b.flags;
+}
+int pool_take(const gck_opts *o, gck_ctx **out) {
+    const gck_opts k = pool_key(o);
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i)
+            if (same_opts(g_pool[i].key, k)) {
+                *out = g_pool[i].ctx;
+                g_pool.erase(g_pool.begin() + (ptrdiff_t)i);
+                return GCK_OK;
+            }
+    }
+    return gck_ctx_create(o, out);
+}
+void pool_give(const gck_opts *o, gck_ctx *c) {
+    if (!c) return;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back(PoolEntry{pool_key(o), c});
+}
+}  // namespace
+
+void gck_replay_release_cache(void) {
+    std::vector<PoolEntry> all;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        all.swap(g_pool);
+    }
+    for (auto &e : all) gck_ctx_destroy(e.ctx);
+}
 
 static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
                           uint64_t cap, gck_result *out) {
@@ -2104,26 +2186,59 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     const uint32_t G = (uint32_t)cut.size() - 1;
     std::vector<gck_ctx *> cs(G, nullptr);
     std::vector<hipEvent_t> ev(G, nullptr);
-    hipStream_t copy = nullptr;
+    hipStream_t copy = nullptr, run_s = nullptr;
+    std::vector<hipStream_t> own_s(G, nullptr);  // the contexts' own streams while they run on run_s
     int rc = GCK_OK;
-    auto cleanup = [&]() {
+    auto cleanup = [&](bool keep) {
         if (copy) (void)hipStreamSynchronize(copy);
+        if (run_s) {
+            (void)hipStreamSynchronize(run_s);
+            for (uint32_t g = 0; g < G; ++g)
+                if (own_s[g]) cs[g]->c.stream = own_s[g];
+            (void)hipStreamDestroy(run_s);
+        }
+        for (auto *c : cs)
+            if (c) (void)hipStreamSynchronize(c->c.stream);
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (copy) (void)hipStreamDestroy(copy);
-        for (auto *c : cs) gck_ctx_destroy(c);
+        for (auto *c : cs) {
+            if (keep)
+                pool_give(opts, c);
+            else
+                gck_ctx_destroy(c);
+        }
     };
-    for (uint32_t g = 0; g < G && !rc; ++g) rc = gck_ctx_create(opts, &cs[g]);
+    for (uint32_t g = 0; g < G && !rc; ++g) rc = pool_take(opts, &cs[g]);
     if (rc) {
-        cleanup();
+        cleanup(true);
         return rc;
     }
     const int dev = cs[0]->c.device;
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) != hipSuccess) {
-        cleanup();
+        cleanup(false);
         return GCK_EDEVICE;
     }
-    for (uint32_t g = 0; g < G && !rc; ++g) {  // layouts, then every H2D queued on the copy stream
+    // Every group runs on ONE stream, created right after the copy stream.
+    // Streams beyond the device's hardware queues share them in order, and a
+    // group stream that shared the copy stream's queue would sit behind every
+    // queued file copy; two streams map to two queues.
+    if (hipStreamCreateWithFlags(&run_s, hipStreamNonBlocking) != hipSuccess) {
+        cleanup(false);
+        return GCK_EDEVICE;
+    }
+    for (uint32_t g = 0; g < G; ++g) {
+        own_s[g] = cs[g]->c.stream;
+        cs[g]->c.stream = run_s;
+    }
+    const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
+    const auto t_begin = std::chrono::steady_clock::now();
+    hipEvent_t tev0 = nullptr;
+    if (trace) {
+        (void)hipEventCreate(&tev0);
+        (void)hipEventRecord(tev0, copy);
+    }
+    for (uint32_t g = 0; g < G && !rc; ++g) {  // layouts, then every H2D queued on the copy stream (below)
         Ctx *c = &cs[g]->c;
         const uint32_t f0 = cut[g], n = cut[g + 1] - f0;
         std::vector<uint64_t> lens(n);
@@ -2133,25 +2248,77 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
             reset[k] = files[f0 + k].reset_after ? 1 : 0;
         }
         if ((rc = ctx_layout(c, lens.data(), n, reset.data()))) break;
+        // a fresh context would take the host path on its first run, whose
+        // small D2H copies queue behind the file copies: give it a record table
+        // for the device path (one record per 256 B; more reruns exactly)
+        if (!c->rec_cap) {
+            uint64_t bytes = 0;
+            for (uint32_t k = 0; k < n; ++k) bytes += lens[k];
+            const uint64_t est = bytes / 256 + 4096;
+            if ((rc = ensure_records(c, est))) break;
+            c->rec_cap = est;
+        }
+    }
+    // every layout first: their small synchronous copies would otherwise
+    // queue behind the file copies of earlier groups on the DMA engine
+    for (uint32_t g = 0; g < G && !rc; ++g) {
+        Ctx *c = &cs[g]->c;
+        const uint32_t f0 = cut[g], n = cut[g + 1] - f0;
         for (uint32_t k = 0; k < n; ++k)
-            if (lens[k] && hipMemcpyAsync(c->arena.as<uint8_t>() + c->f_base[k], files[f0 + k].data, lens[k],
-                                          hipMemcpyHostToDevice, copy) != hipSuccess)
+            if (files[f0 + k].len && hipMemcpyAsync(c->arena.as<uint8_t>() + c->f_base[k], files[f0 + k].data,
+                                                    files[f0 + k].len, hipMemcpyHostToDevice, copy) != hipSuccess)
                 rc = GCK_EDEVICE;
-        if (hipEventCreateWithFlags(&ev[g], hipEventDisableTiming) != hipSuccess ||
+        if (hipEventCreateWithFlags(&ev[g], trace ? hipEventDefault : hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(ev[g], copy) != hipSuccess)
             rc = GCK_EDEVICE;
     }
+    // Each group replays once its files are resident; into caller memory, its
+    // tuples (file indices rebased) leave right away on its own stream, so the
+    // D2H of group g overlaps the H2D and replay of the groups after it.
     uint32_t last = G;  // groups [0, last) contribute
+    uint64_t off = 0;
+    bool early = into;  // D2H issued group by group while the caller's array has room
+    // the device mapping of a registered (pinned) dst, for k_push_recs; plain
+    // pageable memory has none and takes the DMA copy
+    gck_rec *ddst = nullptr;
+    if (into && dst && cap) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp) ddst = static_cast<gck_rec *>(dp);
+        else (void)hipGetLastError();
+    }
     for (uint32_t g = 0; g < G && !rc; ++g) {
         Ctx *c = &cs[g]->c;
         if (hipStreamWaitEvent(c->stream, ev[g], 0) != hipSuccess) {
             rc = GCK_EDEVICE;
             break;
         }
+        const auto tr0 = std::chrono::steady_clock::now();
         const int r = ctx_run(c);
+        if (trace)
+            fprintf(stderr, "[gck_replay] group %u run returned at %.2f ms (run call %.2f ms, device path %d)\n", g,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(),
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(),
+                    (int)c->device_path);
         if (r != GCK_OK && r != GCK_EUNEXPECTED_EOF) {
             rc = r;
             break;
+        }
+        if (early && c->n_recs) {
+            if (off + c->n_recs > cap) {
+                early = false;
+            } else if (ddst) {
+                k_push_recs<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<uint4>(),
+                                                                         reinterpret_cast<uint4 *>(ddst + off),
+                                                                         c->n_recs, cut[g]);
+                off += c->n_recs;
+            } else {
+                if (cut[g])
+                    k_rebase_file<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<gck_rec>(), c->n_recs, cut[g]);
+                if (hipMemcpyAsync(dst + off, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost,
+                                   c->stream) != hipSuccess)
+                    rc = GCK_EDEVICE;
+                off += c->n_recs;
+            }
         }
         if (r == GCK_EUNEXPECTED_EOF) {
             last = g + 1;
@@ -2159,8 +2326,17 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         }
     }
     if (rc) {
-        cleanup();
+        cleanup(false);
         return rc;
+    }
+    if (trace) {
+        for (uint32_t g = 0; g < G; ++g) (void)hipStreamSynchronize(cs[g]->c.stream);
+        (void)hipStreamSynchronize(copy);
+        const double host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
+        float copy_ms = 0;
+        (void)hipEventElapsedTime(&copy_ms, tev0, ev[G - 1]);
+        fprintf(stderr, "[gck_replay] groups %u host %.2f ms, H2D (copy stream) %.2f ms\n", G, host_ms, copy_ms);
+        (void)hipEventDestroy(tev0);
     }
     uint64_t n_total = 0;
     for (uint32_t g = 0; g < last; ++g) n_total += cs[g]->c.n_recs;
@@ -2173,20 +2349,20 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     // cuts follow resetting files: the last contributing group's lastOffset
     out->final_last_offset = lc->final_last_offset;
     for (uint32_t g = 0; g < last; ++g) out->n_crc_fail += cs[g]->c.n_crc_fail;
-    if (into && cap < n_total) {
-        cleanup();
-        return GCK_EINVAL;  // out->n says how many records to make room for
+    if (into) {
+        cleanup(true);
+        if (cap < n_total) return GCK_EINVAL;  // out->n says how many records to make room for
+        return out->status;
     }
-    gck_rec *h = into ? dst : nullptr;
-    if (!into && n_total) {
+    gck_rec *h = nullptr;
+    if (n_total) {
         void *p = nullptr;
         if (hipHostMalloc(&p, n_total * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) {
-            cleanup();
+            cleanup(true);
             return GCK_ENOMEM;
         }
         h = static_cast<gck_rec *>(p);
     }
-    uint64_t off = 0;
     for (uint32_t g = 0; g < last && !rc; ++g) {
         Ctx *c = &cs[g]->c;
         if (!c->n_recs) continue;
@@ -2199,12 +2375,12 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     for (uint32_t g = 0; g < last; ++g)
         if (hipStreamSynchronize(cs[g]->c.stream) != hipSuccess) rc = GCK_EDEVICE;
     if (rc) {
-        if (!into && h) (void)hipHostFree(h);
-        cleanup();
+        if (h) (void)hipHostFree(h);
+        cleanup(false);
         return rc;
     }
-    out->recs = into ? nullptr : h;  // caller memory: nothing for gck_result_free
-    cleanup();
+    out->recs = h;
+    cleanup(true);
     return out->status;
 }
 

@@ -107,11 +107,16 @@ typedef struct gck_result {
  * of all files in walk order. */
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
 /* The same, tuples into caller memory dst (cap records; pin it for DMA rate);
- * out->recs = NULL.  GCK_EINVAL (out->n = records needed, nothing copied)
- * when cap < out->n. */
+ * out->recs = NULL.  Each group's tuples leave as soon as it has replayed.
+ * GCK_EINVAL (out->n = records needed, dst contents unspecified) when
+ * cap < out->n. */
 int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_rec *dst, uint64_t cap,
                     gck_result *out);
 void gck_result_free(gck_result *res);
+/* gck_replay / gck_replay_into keep their device contexts (arenas, tables) for
+ * the next call with the same options, so a repeated Open allocates nothing;
+ * this frees them (call it when no replay will follow, or to return HBM). */
+void gck_replay_release_cache(void);
 
 /* ---- device-resident context (benchmarks, repeated replays) ---------------- */
 typedef struct gck_ctx gck_ctx;

@@ -535,6 +535,19 @@ def test_replay_grouped_equals_oracle(g, orc, monkeypatch):
     small = np.zeros(10, dtype=g.REC_DTYPE)
     with pytest.raises(Exception):
         g.replay_into(wf, small, reset)
+    # the contexts kept from the calls above serve the next ones (same answers),
+    # and after gck_replay_release_cache new ones do
+    # (a pinned array: the tuples are written by k_push_recs over PCIe)
+    recs2 = np.zeros(len(want), dtype=g.REC_DTYPE)
+    g.host_register(recs2)
+    try:
+        st2 = g.replay_into(wf, recs2, reset)
+        assert_same(recs2[:st2["n_recs"]], st2, want, wst)
+    finally:
+        g.host_unregister(recs2)
+    g.release_cache()
+    got3, gst3 = g.replay(wf, reset)
+    assert_same(got3, gst3, want, wst)
 
 
 def test_replay_grouped_startup_error(g, orc):
