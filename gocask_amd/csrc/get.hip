@@ -8,31 +8,20 @@
 // resident arena, so a batch of Gets is one lookup kernel and one verify
 // kernel; gck_ctx_scrub_keydir runs the verify over every live entry.
 #include "kd_common.h"
+#include "gck_crc_lds.h"
 
 namespace gck {
 
-// LDS tables (8 KiB per workgroup): slicing-by-4 (T), and multiplication by
-// the constant Z_1008 as four byte tables: Z(A) = XOR_k Zs[k][byte k of A]
-// (Z is linear in A).
+// LDS tables: the conflict-free slicing-by-4 image (gck_crc_lds.h, 128 KiB,
+// from the context's global tables) and multiplication by the constant Z_1008
+// as four byte tables: Z(A) = XOR_k Zs[k][byte k of A] (Z is linear in A).
 struct CrcTabs {
-    uint32_t T[4][256];
+    uint32_t S[kSliceLdsWords];
     uint32_t Zs[4][256];
 };
 
-__device__ void crc_tables(CrcTabs &t) {
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-        uint32_t c = i;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
-        t.T[0][i] = c;
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
-        uint32_t c = t.T[0][i];
-        for (int k = 1; k < 4; ++k) {
-            c = (c >> 8) ^ t.T[0][c & 0xFF];
-            t.T[k][i] = c;
-        }
-    }
+__device__ void crc_tables(CrcTabs &t, const uint32_t *__restrict__ g_slice) {
+    fill_slice_lds(t.S, g_slice);
     const uint32_t z = xpow8n(1008);
     for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) t.Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
     __syncthreads();
@@ -54,12 +43,25 @@ __device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
 }
 
 // The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
-// pad bytes): aligned dword loads, only of dwords that reach into the value.
+// pad bytes), plus the next dword for the byte shift: one 16 B and one 4 B
+// load (dword aligned), unconditional.  A lane wholly in the padding loads
+// the value's first dwords instead (never before the arena; wave_crc masks its
+// bytes); a lane straddling the value start reads up to 15 bytes before it
+// (the record's header and key: inside the arena).
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+// (Pointer arithmetic only, never an integer cast back to a pointer: that
+// would make the loads flat, and flat loads also count on lgkmcnt, so every
+// LDS table wait would wait for HBM too.)
 __device__ __forceinline__ void stripe_load(const uint8_t *p, uint64_t v, uint64_t pad, uint32_t d[5]) {
-    const uintptr_t q = reinterpret_cast<uintptr_t>(p) + v - pad, a = q & ~(uintptr_t)3;
-    const uintptr_t p0 = reinterpret_cast<uintptr_t>(p);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) d[i] = a + 4 * i + 4 > p0 ? reinterpret_cast<const uint32_t *>(a)[i] : 0u;
+    const uint8_t *q = p + v - pad;
+    q = v + 16 <= pad ? p : q;
+    const uint8_t *a = q - (reinterpret_cast<uintptr_t>(q) & 3);
+    const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
+    d[0] = x.x;
+    d[1] = x.y;
+    d[2] = x.z;
+    d[3] = x.w;
+    d[4] = *reinterpret_cast<const uint32_t *>(a + 16);
 }
 
 // Start of a value's CRC: J = ceil(L / 1 KiB) stripes, pad = J KiB - L.
@@ -71,52 +73,104 @@ struct CrcJob {
 
 // crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
 // virtual buffer of J stripes of 1 KiB, zero-padded at the FRONT (F(0, .)
-// ignores leading zeros), lane l taking the 16 bytes at 16 l of every stripe:
-// coalesced loads, the next stripe's issued before this one is folded (after
-// the last one: the first stripe of the next value, `nx`).  dn holds this
-// value's first stripe on entry.  Lane state: A <- F(Z_1008(A), chunk), i.e.
-// Horner over the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the
-// complement of the value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3
-// ^ 0xFF)).  Lane l's part is finally shifted past the 16 (63-l) bytes after it
-// (kl = x^(8 * 16 (63-l))) and the lanes XOR-reduced: F(~0, V); crc = ~that.
-__device__ uint32_t wave_crc(const CrcJob &jb, uint32_t dn[5], const CrcJob *nx, uint32_t kl, const CrcTabs &t) {
+// ignores leading zeros), lane l taking the 16 bytes at 16 l of every stripe
+// (coalesced loads).  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner over
+// the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement of the
+// value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).  Lane l's
+// part is finally shifted past the 16 (63-l) bytes after it (kl = x^(8 * 16
+// (63-l))) and the lanes XOR-reduced: F(~0, V); crc = ~that.
+//
+// One stripe of the value at virtual stripe j into A:
+__device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, const uint32_t d[5], uint32_t A,
+                                                const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t A = 0;
-    for (uint64_t j = 0; j < jb.J; ++j) {
-        const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
-        uint32_t d[5];
+    const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
+    const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(jb.p) + v - jb.pad) & 3);
+    uint32_t w[4];
 #pragma unroll
-        for (int i = 0; i < 5; ++i) d[i] = dn[i];
-        if (j + 1 < jb.J)
-            stripe_load(jb.p, v + 1024, jb.pad, dn);
-        else if (nx)
-            stripe_load(nx->p, 16ull * lane, nx->pad, dn);
-        const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(jb.p) + v - jb.pad) & 3);
-        uint32_t w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-        if (v < jb.pad + 4) {  // chunks at the value's start: bytes before it are zero, its first 4 complemented
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
-                const uint32_t keep = lead >= 4 ? 0u : lead <= 0 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (8 * lead);
-                const int64_t cl = lead + 4;  // bytes of dword i before the value's byte 4
-                const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
-                w[i] = (w[i] & keep) ^ (flip & keep);
-            }
-        }
-        uint32_t c = zmul(t.Zs, A);
+    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
+    if (v < jb.pad + 4) {  // chunks at the value's start: bytes before it are zero, its first 4 complemented
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            c ^= w[i];
-            c = t.T[3][c & 0xFF] ^ t.T[2][(c >> 8) & 0xFF] ^ t.T[1][(c >> 16) & 0xFF] ^ t.T[0][c >> 24];
+            const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
+            const uint32_t keep = lead >= 4 ? 0u : lead <= 0 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (8 * lead);
+            const int64_t cl = lead + 4;  // bytes of dword i before the value's byte 4
+            const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
+            w[i] = (w[i] & keep) ^ (flip & keep);
         }
-        A = c;
     }
-    A = gmul(kl, A);
+    uint32_t c = zmul(t.Zs, A) ^ w[0];
+    c = slice4x(t.S, lb0, lb1, c, w[1]);
+    c = slice4x(t.S, lb0, lb1, c, w[2]);
+    c = slice4x(t.S, lb0, lb1, c, w[3]);
+    return slice4x(t.S, lb0, lb1, c, 0u);
+}
+
+// The large values of a wavefront's 64 items (mask todo), one after another,
+// with kRing stripes in flight across value boundaries: the stripe folded now
+// was loaded kRing stripes earlier (16 KiB per CU in flight with one stripe
+// ahead is far below what HBM latency needs).  All control is wave-uniform;
+// every load is issued unconditionally (a dummy reload past the last stripe),
+// so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
+#ifndef GCK_RING
+#define GCK_RING 4
+#endif
+constexpr int kRing = GCK_RING;
+__device__ uint32_t wave_crcs(uint64_t todo, const uint8_t *arena, uint64_t off, uint32_t len, uint32_t kl,
+                              const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t out = 0;
+    auto job = [&](int it) { return CrcJob(arena + __shfl(off, it), __shfl(len, it)); };
+    // load cursor
+    uint64_t lrem = todo;
+    int lt = __builtin_ctzll(todo);
+    CrcJob lj = job(lt);
+    uint64_t ls = 0;
+    auto load_next = [&](uint32_t d[5]) {
+        stripe_load(lj.p, (ls << 10) + 16ull * lane, lj.pad, d);
+        if (lrem && ++ls == lj.J) {  // the next value (or stay on the last stripe: dummy reloads)
+            lrem &= lrem - 1;
+            if (lrem) {
+                lt = __builtin_ctzll(lrem);
+                lj = job(lt);
+                ls = 0;
+            } else {
+                ls = lj.J - 1;
+            }
+        }
+    };
+    uint32_t ring[kRing][5];
 #pragma unroll
-    for (int k = 32; k >= 1; k >>= 1) A ^= __shfl_xor(A, k);
-    return ~A;
+    for (int k = 0; k < kRing; ++k) load_next(ring[k]);
+    // compute cursor
+    uint64_t crem = todo;
+    int ct = __builtin_ctzll(todo);
+    CrcJob cj = job(ct);
+    uint64_t cs = 0;
+    uint32_t A = 0;
+    while (crem) {
+#pragma unroll
+        for (int k = 0; k < kRing; ++k) {
+            if (crem) {
+                A = fold_stripe(cj, cs, ring[k], A, t, lb0, lb1);
+                load_next(ring[k]);
+                if (++cs == cj.J) {  // value done
+                    uint32_t f = gmul(kl, A);
+#pragma unroll
+                    for (int m = 32; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
+                    if (lane == (uint32_t)ct) out = ~f;
+                    A = 0;
+                    cs = 0;
+                    crem &= crem - 1;
+                    if (crem) {
+                        ct = __builtin_ctzll(crem);
+                        cj = job(ct);
+                    }
+                }
+            }
+        }
+    }
+    return out;
 }
 
 constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
@@ -124,10 +178,10 @@ constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
 // crc32.ChecksumIEEE of a small value by one lane (lanes run different
 // values): aligned dwords, 64 bytes of loads in flight per round, slicing-by-4
 // per word, the last 0..3 bytes one at a time.
-__device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t) {
-    const uintptr_t q = reinterpret_cast<uintptr_t>(p);
-    const uint32_t *a = reinterpret_cast<const uint32_t *>(q & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(q & 3), nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
+__device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
+    const uint32_t nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
     uint32_t c = 0xFFFFFFFFu, pos = 0;
     for (uint32_t b = 0; __ballot(b < nw); b += 16) {
         uint32_t d[17];
@@ -137,10 +191,9 @@ __device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTa
         for (int i = 0; i < 16; ++i) {
             const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
             if (pos + 4 <= L) {
-                c ^= w;
-                c = t.T[3][c & 0xFF] ^ t.T[2][(c >> 8) & 0xFF] ^ t.T[1][(c >> 16) & 0xFF] ^ t.T[0][c >> 24];
+                c = slice4x(t.S, lb0, lb1, c ^ w, 0u);
             } else {
-                for (uint32_t k = 0; pos + k < L; ++k) c = t.T[0][(c ^ (w >> (8 * k))) & 0xFF] ^ (c >> 8);
+                for (uint32_t k = 0; pos + k < L; ++k) c = byte1x(t.S, lb1, c, w >> (8 * k));
             }
             pos = pos + 4 <= L ? pos + 4 : L;
         }
@@ -225,15 +278,18 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
 // expected CRC in one coalesced load each), then the CRC of every item still
 // GCK_OK in turn, all lanes on one value; a mismatch is GCK_ECRC_FAILED, a
 // match copies the value to dst + dst_off (if dst).
-__global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ arena, uint64_t n,
+__global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ arena, const uint32_t *__restrict__ g_slice,
+                                                 uint64_t n,
                                                 const uint64_t *__restrict__ item,
                                                 const uint32_t *__restrict__ vsize,
                                                 const uint32_t *__restrict__ expect, int32_t *__restrict__ status,
                                                 uint32_t *__restrict__ crc_out, const uint64_t *__restrict__ dst_off,
                                                 uint8_t *__restrict__ dst) {
     __shared__ CrcTabs T;
-    crc_tables(T);
+    crc_tables(T, g_slice);
     const uint32_t lane = threadIdx.x & 63;
+    uint32_t lb0, lb1;
+    slice_bases(lane, lb0, lb1);
     const uint32_t kl = xpow8n(16ull * (63 - lane));  // lane l's chunk is followed by 16 (63-l) bytes of its stripe
     const uint64_t groups = (n + 63) >> 6, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); gi < groups; gi += waves) {
@@ -243,31 +299,16 @@ __global__ __launch_bounds__(256) void k_verify(const uint8_t *__restrict__ aren
         const uint64_t off = ok ? item[mine] : 0;
         const uint32_t len = ok ? vsize[mine] : 0u, want = ok ? expect[mine] : 0u;
         const uint64_t doff = ok && dst ? dst_off[mine] : 0;
-        uint32_t crc = 0, dn[5] = {0u, 0u, 0u, 0u, 0u};
+        uint32_t crc = 0;
         const bool small = ok && len <= kLaneMax;
-        uint64_t todo = __ballot(ok && !small);
+        const uint64_t todo = __ballot(ok && !small);
         if (__ballot(small)) {  // small values: a lane each, all at once
-            const uint32_t c = lane_crc(arena + off, len, small, T);
+            const uint32_t c = lane_crc(arena + off, len, small, T, lb0, lb1);
             if (small) crc = c;
         }
         if (todo) {
-            const int t0 = __builtin_ctzll(todo);
-            const CrcJob first(arena + __shfl(off, t0), __shfl(len, t0));
-            stripe_load(first.p, 16ull * lane, first.pad, dn);
-        }
-        while (todo) {
-            const int t = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const CrcJob cur(arena + __shfl(off, t), __shfl(len, t));
-            uint32_t c;
-            if (todo) {
-                const int t2 = __builtin_ctzll(todo);
-                const CrcJob nx(arena + __shfl(off, t2), __shfl(len, t2));
-                c = wave_crc(cur, dn, &nx, kl, T);
-            } else {
-                c = wave_crc(cur, dn, nullptr, kl, T);
-            }
-            if (lane == (uint32_t)t) crc = c;
+            const uint32_t c = wave_crcs(todo, arena, off, len, kl, T, lb0, lb1);
+            if ((todo >> lane) & 1) crc = c;
         }
         if (dst) {  // the values that passed, copied by the whole wave
             for (uint64_t cp = __ballot(ok && crc == want); cp; cp &= cp - 1) {
@@ -342,8 +383,9 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
         GCK_HIP(hipMemcpyAsync(c->d_gvoff.p, val_off, n * 8ull, hipMemcpyHostToDevice, s));
         dvals = c->d_gvals.as<uint8_t>();
     }
-    const uint32_t grid = std::min<uint32_t>((n + 255) / 256, (uint32_t)c->n_cu * 16);
-    k_verify<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
+    // one 1024-thread workgroup per CU (the tables take 132 KiB of LDS)
+    const uint32_t grid = std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->n_cu);
+    k_verify<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
                                   c->d_gvoff.as<uint64_t>(), dvals);
     GCK_HIP(hipEventRecord(b, s));
@@ -391,7 +433,7 @@ int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint
                                                        c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
                                                        c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                                        c->d_gexp.as<uint32_t>());
-    k_verify<<<(uint32_t)c->n_cu * 16, 256, 0, s>>>(c->arena.as<uint8_t>(), n, c->d_gitem.as<uint64_t>(),
+    k_verify<<<(uint32_t)c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(),
                                                     c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>(),
                                                     c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(), nullptr,
                                                     nullptr);
