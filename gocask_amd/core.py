@@ -524,8 +524,9 @@ def encode_batch(ops, device="cuda"):
     def dev(a, dtype):
         return torch.from_numpy(np.array(a, copy=True).view(dtype)).to(device)
 
-    d_keys = dev(np.frombuffer(keys or b"\0", dtype=np.uint8), np.uint8)
-    d_vals = dev(np.frombuffer(vals or b"\0", dtype=np.uint8), np.uint8)
+    # the kernel reads whole dwords: up to 4 bytes past a blob's end (header)
+    d_keys = dev(np.frombuffer(keys + bytes(16), dtype=np.uint8), np.uint8)
+    d_vals = dev(np.frombuffer(vals + bytes(16), dtype=np.uint8), np.uint8)
     d_koff, d_voff = dev(koff, np.int64), dev(voff, np.int64)
     d_ts, d_tomb = dev(ts, np.int32), dev(tomb, np.uint8)
     need = int(16 * n + len(keys) + sum(len(v) for _, _, v in ops if v is not None))

@@ -16,6 +16,7 @@
 #include <string>
 
 #include "gck_internal.h"
+#include "gck_crc_wave.h"
 
 namespace gck {
 
@@ -263,155 +264,284 @@ int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n) {
 // ------------------------------------------------ bulk serializeEntry (f4) ---
 // gck_encode_batch: caller records (already in HBM) -> GoCask bytes, back to
 // back, as DB.Put / DB.Delete write them (core/db.go:185-212, :245-247,
-// serializeEntry :272-284).  One wavefront per record: the lanes copy key and
-// value with strided byte stores and CRC the payload in 64 contiguous
-// segments, combined through Z_n (gck_math.h):
-//   F(0, V) = XOR_l Z_{|V| - end_l}(F(0, seg_l)),  crc = ~(F(0,V) ^ Z_|V|(~0)).
+// serializeEntry :272-284).  Three steps, all on the device:
+//   1. record sizes 16 + len(key) + len(value) (a Delete: 16 + len(key)) and
+//      their exclusive scan: out_off (k_enc_sizes, k_enc_top, k_enc_add),
+//      with the refusals of the host API (an empty key: ErrInvalidKey,
+//      core/db.go:186-188 / :294-297; a length past u32; decreasing offsets);
+//   2. per wavefront, 64 records: the CRC of each payload (value, or key for a
+//      Delete) -- a lane per payload up to 256 B, the whole wavefront in 1 KiB
+//      stripes with a ring of stripes in flight for larger ones (gck_crc_wave.h,
+//      the machinery of the device Get);
+//   3. the wavefront writes its records' output range in 16 B aligned chunks,
+//      lane l the chunk at 16 l of each 1 KiB row: a chunk inside one record's
+//      key or value is one unaligned 16 B read (two loads + alignbyte) and one
+//      aligned 16 B store; a chunk holding header bytes or a record boundary
+//      is assembled byte by byte (at most two records meet in 16 B: a record
+//      is at least 17 B) and stored whole when it is the group's, else by bytes.
 namespace gck {
 
-__global__ __launch_bounds__(256) void k_encode_batch(const uint8_t *__restrict__ keys,
-                                                      const uint64_t *__restrict__ key_off,
-                                                      const uint8_t *__restrict__ vals,
-                                                      const uint64_t *__restrict__ val_off,
-                                                      const uint32_t *__restrict__ ts,
-                                                      const uint8_t *__restrict__ tomb, uint64_t n,
-                                                      const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out) {
-    __shared__ uint32_t T[256];
-    for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
-        uint32_t c = v;
-        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
-        T[v] = c;
-    }
-    __shared__ uint32_t X8[64];  // x^(8 * 2^k) mod P: powers by set bits, no squarings
-    if (threadIdx.x == 0) {
-        uint32_t x = kX0 >> 8;
-        for (int k = 0; k < 64; ++k) {
-            X8[k] = x;
-            x = multmodp(x, x);
-        }
-    }
-    __syncthreads();
-    auto zpow = [&](uint64_t m) {  // x^(8m) mod P
-        uint32_t r = kX0;
-        for (; m; m &= m - 1) r = multmodp(X8[__builtin_ctzll(m)], r);
-        return r;
-    };
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    // records in groups of 64 per wavefront: payloads up to kLaneMax bytes (1 KiB: A/B of 512..4096, tools/xp_lane_max.sh) are
-    // encoded by one lane each (a serial CRC, no GF(2) combine), larger ones by
-    // the whole wavefront, one after another
-#ifndef GCK_LANE_MAX
-#define GCK_LANE_MAX 1024
+constexpr uint32_t kEncScanBlock = 1024;
+#ifndef GCK_ENC_XP
+#define GCK_ENC_XP 0  // ablation (timing only): 1 no byte path, 2 no stores
 #endif
-    constexpr uint64_t kLaneMax = GCK_LANE_MAX;
-    for (uint64_t g = wave * 64; g < n; g += n_waves * 64) {
-        const uint64_t li = g + lane;
-        bool big = false;
-        if (li < n) {
-            const bool del = tomb[li] != 0;
-            const uint8_t *key = keys + key_off[li];
-            const uint64_t kl = key_off[li + 1] - key_off[li];
-            const uint8_t *val = vals + val_off[li];
-            const uint64_t vl = del ? 0 : val_off[li + 1] - val_off[li];
-            big = (del ? kl : vl) > kLaneMax;
-            if (!big) {
-                uint8_t *dst = out + out_off[li];
-                uint32_t c = 0xFFFFFFFFu;
-                // bytes of src to d, eight aligned dwords in flight; CRC'd when crc
-                auto put = [&](const uint8_t *src, uint8_t *d, uint64_t len, bool crc) {
-                    auto one = [&](uint64_t j, uint8_t x) {
-                        d[j] = x;
-                        if (crc) c = T[(c ^ x) & 0xff] ^ (c >> 8);
-                    };
-                    uint64_t j = 0;
-                    const uint64_t al = min(len, (uint64_t)((4u - ((uintptr_t)src & 3u)) & 3u));
-                    for (; j < al; ++j) one(j, src[j]);
-                    const uint32_t *pw = reinterpret_cast<const uint32_t *>(src + j);
-                    const uint64_t nw = (len - j) / 4;
-                    uint64_t q = 0;
-                    for (; q + 8 <= nw; q += 8) {
-                        uint32_t v[8];
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(pw + q + k);
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-#pragma unroll
-                            for (int b = 0; b < 4; ++b) one(j + 4 * (q + k) + b, (uint8_t)(v[k] >> (8 * b)));
-                    }
-                    for (; q < nw; ++q) {
-                        const uint32_t w = pw[q];
-#pragma unroll
-                        for (int b = 0; b < 4; ++b) one(j + 4 * q + b, (uint8_t)(w >> (8 * b)));
-                    }
-                    for (j += 4 * nw; j < len; ++j) one(j, src[j]);
-                };
-                put(key, dst + 16, kl, del);
-                put(val, dst + 16 + kl, vl, !del);
-                const uint32_t hv[4] = {~c, ts[li], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
-#pragma unroll
-                for (int k = 0; k < 16; ++k) dst[k] = (uint8_t)(hv[k / 4] >> (8 * (k % 4)));
-            }
-        }
-        uint64_t bigs = __ballot(big);
-        while (bigs) {
-        const uint64_t i = g + (uint64_t)__builtin_ctzll(bigs);
-        bigs &= bigs - 1;
+
+// 1a. sizes, block-local exclusive prefix (into out_off), block sums, refusals
+__global__ __launch_bounds__(1024) void k_enc_sizes(const uint64_t *__restrict__ key_off,
+                                                   const uint64_t *__restrict__ val_off,
+                                                   const uint8_t *__restrict__ tomb, uint64_t n,
+                                                   uint64_t *__restrict__ out_off, uint64_t *__restrict__ bsum,
+                                                   uint32_t *__restrict__ err) {
+    __shared__ uint64_t wsum[16];
+    const uint64_t i = (uint64_t)blockIdx.x * kEncScanBlock + threadIdx.x;
+    uint64_t sz = 0;
+    uint32_t e = 0;
+    if (i < n) {
+        const uint64_t k0 = key_off[i], k1 = key_off[i + 1], v0 = val_off[i], v1 = val_off[i + 1];
         const bool del = tomb[i] != 0;
-        const uint8_t *key = keys + key_off[i];
-        const uint64_t kl = key_off[i + 1] - key_off[i];
-        const uint8_t *val = vals + val_off[i];
-        const uint64_t vl = del ? 0 : val_off[i + 1] - val_off[i];
-        uint8_t *dst = out + out_off[i];
-        // coalesced byte copies, eight loads in flight per lane before the stores
-        auto copy = [&](const uint8_t *src, uint8_t *d, uint64_t len) {
-            uint64_t j = lane;
-            for (; j + 7 * 64 < len; j += 8 * 64) {
-                uint8_t v[8];
+        if (k1 < k0 || v1 < v0) e |= 2u;
+        const uint64_t kl = k1 - k0, vl = del ? 0 : v1 - v0;
+        if (kl == 0) e |= 1u;                                           // ErrInvalidKey
+        if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) e |= 2u;          // u32 header fields
+        sz = 16 + kl + vl;
+    }
+    // exclusive scan over the block: wave scans (u64 in two halves), then the wave totals
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t inc = sz;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(src + j + 64 * k);
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    const uint64_t me = __ballot(e != 0);
+    if (me && lane == (uint32_t)__builtin_ctzll(me)) atomicOr(err, e);
+    __syncthreads();
+    uint64_t before = 0;
+    for (uint32_t k = 0; k < w; ++k) before += wsum[k];
+    if (i < n) out_off[i] = before + inc - sz;
+    if (threadIdx.x == blockDim.x - 1) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < 16; ++k) tot += wsum[k];
+        bsum[blockIdx.x] = tot;
+    }
+}
+// 1b. exclusive scan of the block sums (one wavefront); total -> out_off[n]
+__global__ void k_enc_top(uint64_t *__restrict__ bsum, uint64_t nb, uint64_t n, uint64_t *__restrict__ out_off,
+                          uint64_t *__restrict__ res) {
+    const uint32_t lane = threadIdx.x;
+    uint64_t run = 0;
+    for (uint64_t b0 = 0; b0 < nb; b0 += 64) {
+        const uint64_t b = b0 + lane;
+        const uint64_t v = b < nb ? bsum[b] : 0;
+        uint64_t inc = v;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) d[j + 64 * k] = v[k];
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(inc, d, 64);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (b < nb) bsum[b] = run + inc - v;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) {
+        out_off[n] = run;
+        res[0] = run;
+    }
+}
+__global__ void k_enc_add(uint64_t *__restrict__ out_off, const uint64_t *__restrict__ bsum, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out_off[i] += bsum[i / kEncScanBlock];
+}
+
+// Work units of the encode kernel: unit u = the records whose output starts
+// in [u W, (u+1) W), W = 64 KiB (a unit's records may run past its window; a
+// record larger than W leaves the units it spans empty).  ufirst[u] = the
+// first record starting at or after u W (record r is that for the units in
+// (start_{r-1} / W, start_r / W]); ufirst[U] = n.  Units balance the kernel
+// by bytes: groups of 64 records differ by orders of magnitude.
+constexpr uint64_t kEncUnit = 64 << 10;
+__global__ void k_enc_units(const uint64_t *__restrict__ out_off, uint64_t n, uint64_t n_units,
+                            uint32_t *__restrict__ ufirst) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t s = r < n ? out_off[r] : ~0ull;
+        const uint64_t lo = r ? out_off[r - 1] / kEncUnit + 1 : 0;
+        const uint64_t hi = r < n ? s / kEncUnit : n_units;  // inclusive
+        for (uint64_t u = lo; u <= hi && u <= n_units; ++u) ufirst[u] = (uint32_t)r;
+    }
+}
+
+// The 16 bytes at src (any alignment): two dword-aligned loads, a byte shift
+// (reads up to 3 bytes before src and 4 after the 16).
+__device__ __forceinline__ uint4 load16u(const uint8_t *src) {
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
+    const uint8_t *a = src - sh;
+    const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
+    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + 16);
+    return make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
+                      __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
+}
+
+__device__ __forceinline__ CrcTabs &enc_tabs() {
+    __shared__ CrcTabs t;
+    return t;
+}
+// MODE 1: the CRCs (into crcs[]; 1024-thread workgroups, the LDS tables);
+// MODE 2: the output bytes (headers take crcs[]; no LDS, so many more
+// wavefronts per CU hide the row loads' latency).
+template <int MODE>
+__global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const uint8_t *__restrict__ keys,
+                                                       const uint64_t *__restrict__ key_off,
+                                                       const uint8_t *__restrict__ vals,
+                                                       const uint64_t *__restrict__ val_off,
+                                                       const uint32_t *__restrict__ ts,
+                                                       const uint8_t *__restrict__ tomb, uint64_t n,
+                                                       const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+                                                       const uint32_t *__restrict__ ufirst, uint64_t n_units,
+                                                       uint32_t *__restrict__ queue, uint32_t *__restrict__ crcs) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t lb0 = 0, lb1 = 0, kl_shift = 0;
+    CrcTabs *T = nullptr;  // MODE 1 only (static LDS of the one kernel that uses it)
+    if constexpr (MODE == 1) T = &enc_tabs();
+    // the slicing tables, built here (no context): T0..T3 into Zs, expanded
+    // into the conflict-free image, then Zs itself
+    if constexpr (MODE == 1) {
+        uint32_t *t4 = &T->Zs[0][0];
+        for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
+            uint32_t c = v;
+            for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ kPoly : c >> 1;
+            t4[v] = c;
+        }
+        __syncthreads();
+        for (uint32_t v = threadIdx.x; v < 256; v += blockDim.x) {
+            uint32_t c = t4[v];
+            for (int k = 1; k < 4; ++k) {
+                c = (c >> 8) ^ t4[c & 0xFF];
+                t4[k * 256 + v] = c;
             }
-            for (; j < len; j += 64) d[j] = src[j];
-        };
-        copy(key, dst + 16, kl);
-        copy(val, dst + 16 + kl, vl);
-        // the CRC payload: the value (Put) or the key (Delete)
-        const uint8_t *pl = del ? key : val;
-        const uint64_t len = del ? kl : vl;
-        const uint64_t seg = (len + 63) / 64, b = min(len, lane * seg), e = min(len, b + seg);
-        // the lane's segment: head bytes up to a 4 B boundary, aligned dwords
-        // eight at a time (independent loads in flight), tail bytes
-        uint32_t c = 0;
-        auto byte = [&](uint8_t x) { c = T[(c ^ x) & 0xff] ^ (c >> 8); };
-        auto word = [&](uint32_t w) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) byte((uint8_t)(w >> (8 * k)));
-        };
-        uint64_t j = b;
-        const uint64_t al = min(e, b + ((4u - ((uintptr_t)(pl + b) & 3u)) & 3u));
-        for (; j < al; ++j) byte(pl[j]);
-        const uint32_t *pw = reinterpret_cast<const uint32_t *>(pl + j);
-        const uint64_t nw = (e - j) / 4;
-        uint64_t q = 0;
-        for (; q + 8 <= nw; q += 8) {
-            uint32_t v[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = __builtin_nontemporal_load(pw + q + k);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) word(v[k]);
         }
-        for (; q < nw; ++q) word(pw[q]);
-        for (j += 4 * nw; j < e; ++j) byte(pl[j]);
-        uint32_t f = c ? multmodp(zpow(len - e), c) : 0u;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) f ^= (uint32_t)__shfl_xor((int)f, m, 64);
-        const uint32_t crc = ~(f ^ multmodp(zpow(len), 0xFFFFFFFFu));
-        const uint32_t hv[4] = {crc, ts[i], del ? 0u : (uint32_t)kl, (uint32_t)(del ? kl : vl)};
-        if (lane < 16) dst[lane] = (uint8_t)(hv[lane / 4] >> (8 * (lane % 4)));
+        __syncthreads();
+        fill_slice_lds(T->S, t4);
+        __syncthreads();
+        const uint32_t z = xpow8n(1008);
+        for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) T->Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
+        __syncthreads();
+        slice_bases(lane, lb0, lb1);
+        kl_shift = xpow8n(16ull * (63 - lane));
+    }
+    // units from an atomic queue, each as groups of up to 64 records
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(queue, 1u);
+        u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+        if (u >= n_units) break;
+        const uint64_t ua = ufirst[u], ub = ufirst[u + 1];
+    for (uint64_t g0 = ua; g0 < ub; g0 += 64) {
+        const uint64_t mine = g0 + lane;
+        const uint32_t cnt = (uint32_t)min<uint64_t>(64, ub - g0);
+        const bool have = mine < g0 + cnt;
+        const uint64_t ko = have ? key_off[mine] : 0, kl = have ? key_off[mine + 1] - ko : 0;
+        const bool del = have && tomb[mine] != 0;
+        const uint64_t vo = have ? val_off[mine] : 0, vl = have && !del ? val_off[mine + 1] - vo : 0;
+        const uint32_t t = have ? ts[mine] : 0u;
+        const uint64_t oo = have ? out_off[mine] : 0;
+        const uint64_t O0 = __shfl(oo, 0), O1 = out_off[g0 + cnt];  // the group's output range
+        // 2. CRCs: a lane per small payload (and per payload at its blob's
+        // first 16 bytes: the stripe reads may reach 15 bytes before it),
+        // the wavefront for the rest
+        const uint64_t po = del ? ko : vo;
+        const uint32_t L = (uint32_t)(del ? kl : vl);
+        const bool small = have && (L <= kLaneMax || po < 16);
+        uint32_t crc = 0;
+        if constexpr (MODE == 1) {
+            if (__ballot(small)) {
+                const uint32_t c = lane_crc((del ? keys : vals) + po, L, small, *T, lb0, lb1);
+                if (small) crc = c;
+            }
+            const uint64_t todo = __ballot(have && !small);
+            if (todo) {
+                const uint32_t c = wave_crcs(
+                    todo, [&](int it) { return (__shfl((int)del, it) ? keys : vals) + __shfl(po, it); }, L,
+                    kl_shift, *T, lb0, lb1);
+                if ((todo >> lane) & 1) crc = c;
+            }
+            if (have) crcs[mine] = crc;
+            continue;
+        } else {
+            crc = have ? crcs[mine] : 0u;
         }
+        const uint32_t h1 = t, h2 = del ? 0u : (uint32_t)kl, h3 = (uint32_t)(del ? kl : vl);
+        // 3. the group's output, 1 KiB rows of 16 B chunks
+        uint32_t rr = 0;  // first record overlapping the row (wave-uniform)
+        for (uint64_t R = O0 & ~15ull; R < O1; R += 1024) {
+            const uint64_t X = R + 16ull * lane;
+            // the record holding X (the group's first for chunks before O0)
+            uint32_t r = rr;
+            for (uint32_t k = rr + 1; k < cnt; ++k) {  // k wave-uniform: readlane, not a permute
+                const uint64_t sk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oo >> 32), (int)k) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oo, (int)k);
+                if (sk >= R + 1024) break;
+                if (X >= sk) r = k;
+            }
+            rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
+            // at most two records meet in a chunk: r, and r + 1 from its end on
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            uint32_t mask = 0;  // bytes of the chunk written from this group's records
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int src = (int)min<uint32_t>(r + j, cnt - 1);
+                const uint64_t s = __shfl(oo, src), k_o = __shfl(ko, src), k_l = __shfl(kl, src);
+                const uint64_t v_o = __shfl(vo, src), v_l = __shfl(vl, src);
+                const uint32_t hv[4] = {(uint32_t)__shfl((int)crc, src), (uint32_t)__shfl((int)h1, src),
+                                        (uint32_t)__shfl((int)h2, src), (uint32_t)__shfl((int)h3, src)};
+                const bool use = r + j < cnt && X < O1;
+                const uint64_t e = s + 16 + k_l + v_l;
+                const uint64_t b0 = max(X, s), b1 = min(X + 16, e);
+                if (!use || b0 >= b1) continue;
+                const uint8_t *kp = keys + k_o, *vp = vals + v_o;
+                const uint64_t q0 = b0 - s;
+                if (b0 == X && b1 == X + 16 && q0 >= 16 && (q0 + 16 <= 16 + k_l || q0 >= 16 + k_l)) {
+                    // the whole chunk inside the key or inside the value
+                    const uint4 v = load16u(q0 >= 16 + k_l ? vp + (q0 - 16 - k_l) : kp + (q0 - 16));
+                    w[0] = v.x;
+                    w[1] = v.y;
+                    w[2] = v.z;
+                    w[3] = v.w;
+                    mask = 0xFFFFu;
+                } else if (GCK_ENC_XP & 1) {
+                    mask = 0xFFFFu;  // ablation: no byte path (wrong bytes)
+                } else {
+                    // byte by byte, the 16 source bytes loaded at once (addresses
+                    // clamped into the key / value, so every load is in range)
+                    uint32_t by[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const uint64_t q = X + i - s;  // may be past the record: clamped, unused
+                        const bool in_key = q < 16 + k_l || v_l == 0;
+                        const uint64_t kq = q < 16 ? 0 : min(q - 16, k_l - 1);
+                        const uint64_t vq = q < 16 + k_l ? 0 : min(q - 16 - k_l, v_l - 1);
+                        by[i] = in_key ? kp[kq] : vp[vq];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const uint64_t b = X + i;
+                        if (b < b0 || b >= b1) continue;
+                        const uint64_t q = b - s;
+                        const uint32_t v = q < 16 ? (hv[q >> 2] >> (8 * (q & 3))) & 0xFFu : by[i];
+                        w[i >> 2] |= v << (8 * (i & 3));
+                        mask |= 1u << i;
+                    }
+                }
+            }
+            if (GCK_ENC_XP & 2) {
+                if (w[0] == 0x12345678u && w[1] == mask) out[X] = 1;  // keep the work live
+            } else if (mask == 0xFFFFu) {
+                *reinterpret_cast<uint4 *>(out + X) = make_uint4(w[0], w[1], w[2], w[3]);
+            } else if (mask) {  // the group's first or last chunk: its bytes only
+                for (uint32_t i = 0; i < 16; ++i)
+                    if ((mask >> i) & 1) out[X + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+    }
     }
 }
 
@@ -422,33 +552,57 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
                                 uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *total,
                                 void *stream) {
     if (!key_off || !val_off || !out_off || !total || (n && (!keys || !out || !ts || !tomb))) return GCK_EINVAL;
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return GCK_EDEVICE;
+    int ndev = 0, dev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || hipGetDevice(&dev) != hipSuccess) return GCK_EDEVICE;
     hipStream_t s = (hipStream_t)stream;
-    // record offsets: a sequential sum over the sizes (17 B per record crosses
-    // PCIe twice; the bytes themselves never leave the device)
-    std::vector<uint64_t> ko(n + 1), vo(n + 1), off(n + 1);
-    std::vector<uint8_t> tb(n);
-    GCK_HIP(hipMemcpyAsync(ko.data(), key_off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    GCK_HIP(hipMemcpyAsync(vo.data(), val_off, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    if (n) GCK_HIP(hipMemcpyAsync(tb.data(), tomb, n, hipMemcpyDeviceToHost, s));
+    *total = 0;
+    // 1. sizes and offsets on the device; 16 B (total, refusals) come back
+    const uint64_t nb = (n + kEncScanBlock - 1) / kEncScanBlock;
+    void *tmp = nullptr;
+    GCK_HIP(hipMallocAsync(&tmp, (nb + 1) * 8 + 16, s));
+    uint64_t *bsum = static_cast<uint64_t *>(tmp), *res = bsum + nb + 1;
+    GCK_HIP(hipMemsetAsync(res, 0, 16, s));
+    if (n) k_enc_sizes<<<(uint32_t)nb, kEncScanBlock, 0, s>>>(key_off, val_off, tomb, n, out_off, bsum,
+                                                              reinterpret_cast<uint32_t *>(res + 1));
+    k_enc_top<<<1, 64, 0, s>>>(bsum, nb, n, out_off, res);
+    if (n) k_enc_add<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(out_off, bsum, n);
+    uint64_t h[2] = {0, 0};
+    GCK_HIP(hipMemcpyAsync(h, res, 16, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
-    off[0] = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        if (ko[i + 1] < ko[i] || vo[i + 1] < vo[i]) return GCK_EINVAL;
-        const uint64_t kl = ko[i + 1] - ko[i], vl = tb[i] ? 0 : vo[i + 1] - vo[i];
-        if (kl == 0) return GCK_EINVALID_KEY;  // Put / Delete of an empty key (core/db.go:186, :294)
-        if (kl > 0xFFFFFFFFull || vl > 0xFFFFFFFFull) return GCK_EINVAL;  // u32 header fields
-        off[i + 1] = off[i] + 16 + kl + vl;
-    }
-    *total = off[n];
+    (void)hipFreeAsync(tmp, s);
+    const uint32_t err = (uint32_t)h[1];
+    if (err & 1u) return GCK_EINVALID_KEY;  // Put / Delete of an empty key (core/db.go:186, :294)
+    if (err & 2u) return GCK_EINVAL;        // decreasing offsets, or u32 header fields overflow
+    *total = h[0];
     if (*total > out_cap) return GCK_EINVAL;  // *total says how much is needed
-    GCK_HIP(hipMemcpyAsync(out_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     if (n) {
-        const uint64_t waves = std::min<uint64_t>((n + 63) / 64, 256ull * 64);
-        k_encode_batch<<<(uint32_t)((waves + 3) / 4), 256, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n,
-                                                                   out_off, out);
+        int n_cu = 0;
+        GCK_HIP(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+        // units of 64 KiB of output (the last record starts in the last unit)
+        uint64_t last = 0;
+        GCK_HIP(hipMemcpyAsync(&last, out_off + n - 1, 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        const uint64_t n_units = last / kEncUnit + 1;
+        void *ub = nullptr;
+        GCK_HIP(hipMallocAsync(&ub, (n_units + 1) * 4 + 4, s));
+        uint32_t *ufirst = static_cast<uint32_t *>(ub), *queue = ufirst + n_units + 1;
+        GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
+        k_enc_units<<<(uint32_t)std::min<uint64_t>((n + 256) / 256, 4096), 256, 0, s>>>(out_off, n, n_units, ufirst);
+        // the CRCs: one 1024-thread workgroup per CU (the tables take 132 KiB
+        // of LDS); then the bytes: 256-thread workgroups, eight per CU
+        uint32_t *crcs = nullptr;
+        GCK_HIP(hipMallocAsync(reinterpret_cast<void **>(&crcs), n * 4, s));
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((n_units + 15) / 16, (uint64_t)n_cu);
+        k_encode_batch<1><<<grid, 1024, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst,
+                                                n_units, queue, crcs);
+        GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
+        const uint32_t grid2 = (uint32_t)std::min<uint64_t>((n_units + 3) / 4, (uint64_t)n_cu * 8);
+        k_encode_batch<2><<<grid2, 256, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst,
+                                                n_units, queue, crcs);
         GCK_HIP(hipGetLastError());
+        (void)hipFreeAsync(crcs, s);
+        GCK_HIP(hipStreamSynchronize(s));
+        (void)hipFreeAsync(ub, s);
     }
     GCK_HIP(hipStreamSynchronize(s));
     return GCK_OK;

@@ -8,198 +8,9 @@
 // resident arena, so a batch of Gets is one lookup kernel and one verify
 // kernel; gck_ctx_scrub_keydir runs the verify over every live entry.
 #include "kd_common.h"
-#include "gck_crc_lds.h"
+#include "gck_crc_wave.h"
 
 namespace gck {
-
-// LDS tables: the conflict-free slicing-by-4 image (gck_crc_lds.h, 128 KiB,
-// from the context's global tables) and multiplication by the constant Z_1008
-// as four byte tables: Z(A) = XOR_k Zs[k][byte k of A] (Z is linear in A).
-struct CrcTabs {
-    uint32_t S[kSliceLdsWords];
-    uint32_t Zs[4][256];
-};
-
-__device__ void crc_tables(CrcTabs &t, const uint32_t *__restrict__ g_slice) {
-    fill_slice_lds(t.S, g_slice);
-    const uint32_t z = xpow8n(1008);
-    for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) t.Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
-    __syncthreads();
-}
-
-// a * b mod P (reflected), 32 steps without early exit (a varies by lane).
-__device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b) {
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-        p ^= (a & (0x80000000u >> i)) ? b : 0u;
-        b = (b >> 1) ^ ((b & 1u) ? kPoly : 0u);
-    }
-    return p;
-}
-
-__device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
-    return Z[0][a & 0xFF] ^ Z[1][(a >> 8) & 0xFF] ^ Z[2][(a >> 16) & 0xFF] ^ Z[3][a >> 24];
-}
-
-// The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
-// pad bytes), plus the next dword for the byte shift: one 16 B and one 4 B
-// load (dword aligned), unconditional.  A lane wholly in the padding loads
-// the value's first dwords instead (never before the arena; wave_crc masks its
-// bytes); a lane straddling the value start reads up to 15 bytes before it
-// (the record's header and key: inside the arena).
-typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-// (Pointer arithmetic only, never an integer cast back to a pointer: that
-// would make the loads flat, and flat loads also count on lgkmcnt, so every
-// LDS table wait would wait for HBM too.)
-__device__ __forceinline__ void stripe_load(const uint8_t *p, uint64_t v, uint64_t pad, uint32_t d[5]) {
-    const uint8_t *q = p + v - pad;
-    q = v + 16 <= pad ? p : q;
-    const uint8_t *a = q - (reinterpret_cast<uintptr_t>(q) & 3);
-    const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
-    d[0] = x.x;
-    d[1] = x.y;
-    d[2] = x.z;
-    d[3] = x.w;
-    d[4] = *reinterpret_cast<const uint32_t *>(a + 16);
-}
-
-// Start of a value's CRC: J = ceil(L / 1 KiB) stripes, pad = J KiB - L.
-struct CrcJob {
-    const uint8_t *p;
-    uint64_t L, J, pad;
-    __device__ CrcJob(const uint8_t *p_, uint64_t L_) : p(p_), L(L_), J((L_ + 1023) >> 10), pad((J << 10) - L_) {}
-};
-
-// crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
-// virtual buffer of J stripes of 1 KiB, zero-padded at the FRONT (F(0, .)
-// ignores leading zeros), lane l taking the 16 bytes at 16 l of every stripe
-// (coalesced loads).  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner over
-// the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement of the
-// value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).  Lane l's
-// part is finally shifted past the 16 (63-l) bytes after it (kl = x^(8 * 16
-// (63-l))) and the lanes XOR-reduced: F(~0, V); crc = ~that.
-//
-// One stripe of the value at virtual stripe j into A:
-__device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, const uint32_t d[5], uint32_t A,
-                                                const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
-    const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(jb.p) + v - jb.pad) & 3);
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-    if (v < jb.pad + 4) {  // chunks at the value's start: bytes before it are zero, its first 4 complemented
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
-            const uint32_t keep = lead >= 4 ? 0u : lead <= 0 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (8 * lead);
-            const int64_t cl = lead + 4;  // bytes of dword i before the value's byte 4
-            const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
-            w[i] = (w[i] & keep) ^ (flip & keep);
-        }
-    }
-    uint32_t c = zmul(t.Zs, A) ^ w[0];
-    c = slice4x(t.S, lb0, lb1, c, w[1]);
-    c = slice4x(t.S, lb0, lb1, c, w[2]);
-    c = slice4x(t.S, lb0, lb1, c, w[3]);
-    return slice4x(t.S, lb0, lb1, c, 0u);
-}
-
-// The large values of a wavefront's 64 items (mask todo), one after another,
-// with kRing stripes in flight across value boundaries: the stripe folded now
-// was loaded kRing stripes earlier (16 KiB per CU in flight with one stripe
-// ahead is far below what HBM latency needs).  All control is wave-uniform;
-// every load is issued unconditionally (a dummy reload past the last stripe),
-// so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
-#ifndef GCK_RING
-#define GCK_RING 4
-#endif
-constexpr int kRing = GCK_RING;
-__device__ uint32_t wave_crcs(uint64_t todo, const uint8_t *arena, uint64_t off, uint32_t len, uint32_t kl,
-                              const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t out = 0;
-    auto job = [&](int it) { return CrcJob(arena + __shfl(off, it), __shfl(len, it)); };
-    // load cursor
-    uint64_t lrem = todo;
-    int lt = __builtin_ctzll(todo);
-    CrcJob lj = job(lt);
-    uint64_t ls = 0;
-    auto load_next = [&](uint32_t d[5]) {
-        stripe_load(lj.p, (ls << 10) + 16ull * lane, lj.pad, d);
-        if (lrem && ++ls == lj.J) {  // the next value (or stay on the last stripe: dummy reloads)
-            lrem &= lrem - 1;
-            if (lrem) {
-                lt = __builtin_ctzll(lrem);
-                lj = job(lt);
-                ls = 0;
-            } else {
-                ls = lj.J - 1;
-            }
-        }
-    };
-    uint32_t ring[kRing][5];
-#pragma unroll
-    for (int k = 0; k < kRing; ++k) load_next(ring[k]);
-    // compute cursor
-    uint64_t crem = todo;
-    int ct = __builtin_ctzll(todo);
-    CrcJob cj = job(ct);
-    uint64_t cs = 0;
-    uint32_t A = 0;
-    while (crem) {
-#pragma unroll
-        for (int k = 0; k < kRing; ++k) {
-            if (crem) {
-                A = fold_stripe(cj, cs, ring[k], A, t, lb0, lb1);
-                load_next(ring[k]);
-                if (++cs == cj.J) {  // value done
-                    uint32_t f = gmul(kl, A);
-#pragma unroll
-                    for (int m = 32; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
-                    if (lane == (uint32_t)ct) out = ~f;
-                    A = 0;
-                    cs = 0;
-                    crem &= crem - 1;
-                    if (crem) {
-                        ct = __builtin_ctzll(crem);
-                        cj = job(ct);
-                    }
-                }
-            }
-        }
-    }
-    return out;
-}
-
-constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
-
-// crc32.ChecksumIEEE of a small value by one lane (lanes run different
-// values): aligned dwords, 64 bytes of loads in flight per round, slicing-by-4
-// per word, the last 0..3 bytes one at a time.
-__device__ uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
-    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
-    const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
-    const uint32_t nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
-    uint32_t c = 0xFFFFFFFFu, pos = 0;
-    for (uint32_t b = 0; __ballot(b < nw); b += 16) {
-        uint32_t d[17];
-#pragma unroll
-        for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-            if (pos + 4 <= L) {
-                c = slice4x(t.S, lb0, lb1, c ^ w, 0u);
-            } else {
-                for (uint32_t k = 0; pos + k < L; ++k) c = byte1x(t.S, lb1, c, w >> (8 * k));
-            }
-            pos = pos + 4 <= L ? pos + 4 : L;
-        }
-    }
-    return ~c;
-}
 
 // k_get_lookup: one lane per query key (keys: a blob padded by 8 bytes, koff:
 // n+1 offsets).  Probes the keydir table like k_kd_insert; a key whose winning
@@ -307,7 +118,7 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
             if (small) crc = c;
         }
         if (todo) {
-            const uint32_t c = wave_crcs(todo, arena, off, len, kl, T, lb0, lb1);
+            const uint32_t c = wave_crcs(todo, [&](int it) { return arena + __shfl(off, it); }, len, kl, T, lb0, lb1);
             if ((todo >> lane) & 1) crc = c;
         }
         if (dst) {  // the values that passed, copied by the whole wave

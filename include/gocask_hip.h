@@ -293,13 +293,15 @@ void gck_encode_zipf_table(uint32_t *thr);
  * Put of key i / value i, or, when tomb[i] != 0, a Delete of key i
  * (header{CRC32(key), ts, 0, len(key)} || key), written back to back into out
  * in order.  keys/vals are concatenated bytes with n+1 offsets
- * (key_off/val_off); every pointer except total is DEVICE memory; out_off
- * (n+1) receives each record's offset in out; *total = bytes written (or
- * needed: GCK_EINVAL with nothing written when out_cap < *total; GCK_EINVALID_KEY
- * and nothing written when a key is empty, as DB.Put / DB.Delete refuse it,
- * core/db.go:186-188, :294-297).  stream:
- * a hipStream_t, NULL for the default stream; returns after the bytes are
- * written. */
+ * (key_off/val_off); every pointer except total is DEVICE memory, keys and
+ * vals 4-byte aligned and readable 4 bytes past their last byte (the kernel
+ * reads whole dwords); out_off (n+1) receives each record's offset in out;
+ * *total = bytes written (or needed: GCK_EINVAL with nothing written to out
+ * when out_cap < *total; GCK_EINVALID_KEY and nothing written to out when a
+ * key is empty, as DB.Put / DB.Delete refuse it, core/db.go:186-188,
+ * :294-297).  Offsets, CRCs and bytes are all computed on the device (16 B of
+ * results cross PCIe).  stream: a hipStream_t, NULL for the default stream;
+ * returns after the bytes are written. */
 int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, const uint8_t *vals,
                      const uint64_t *val_off, const uint32_t *ts, const uint8_t *tomb, uint64_t n,
                      uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *total, void *stream);
