@@ -47,10 +47,28 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // (Pointer arithmetic only, never an integer cast back to a pointer: that
 // would make the loads flat, and flat loads also count on lgkmcnt, so every
 // LDS table wait would wait for HBM too.)
-__device__ __forceinline__ void stripe_load(const uint8_t *p, uint64_t v, uint64_t pad, uint32_t d[5]) {
-    const uint8_t *q = p + v - pad;
-    q = v + 16 <= pad ? p : q;
-    const uint8_t *a = q - (reinterpret_cast<uintptr_t>(q) & 3);
+// Start of a value's CRC: J = ceil(L / 1 KiB) stripes, pad = J KiB - L; all
+// wave-uniform, so the byte shift sh and the dword-aligned base b of the
+// virtual buffer (b + v = the dword holding virtual byte v, sh its offset)
+// are scalars.
+struct CrcJob {
+    const uint8_t *p, *b;
+    uint64_t L, J, pad;
+    uint32_t sh;
+    __device__ CrcJob(const uint8_t *p_, uint64_t L_)
+        : p(p_), L(L_), J((L_ + 1023) >> 10), pad((J << 10) - L_),
+          sh((uint32_t)((reinterpret_cast<uintptr_t>(p_) - pad) & 3)) {
+        b = p - pad - sh;
+    }
+};
+__device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32_t d[5]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t v = (j << 10) + 16ull * lane;
+    const uint8_t *a = jb.b + v;
+    if ((j << 10) < jb.pad + 16) {  // (uniform) the value's first stripe(s): lanes wholly in the padding
+        const uint8_t *p0 = jb.p - (reinterpret_cast<uintptr_t>(jb.p) & 3);
+        a = v + 16 <= jb.pad ? p0 : a;
+    }
     const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
     d[0] = x.x;
     d[1] = x.y;
@@ -58,13 +76,6 @@ __device__ __forceinline__ void stripe_load(const uint8_t *p, uint64_t v, uint64
     d[3] = x.w;
     d[4] = *reinterpret_cast<const uint32_t *>(a + 16);
 }
-
-// Start of a value's CRC: J = ceil(L / 1 KiB) stripes, pad = J KiB - L.
-struct CrcJob {
-    const uint8_t *p;
-    uint64_t L, J, pad;
-    __device__ CrcJob(const uint8_t *p_, uint64_t L_) : p(p_), L(L_), J((L_ + 1023) >> 10), pad((J << 10) - L_) {}
-};
 
 // crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
 // virtual buffer of J stripes of 1 KiB, zero-padded at the FRONT (F(0, .)
@@ -80,11 +91,12 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
                                                 const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
-    const uint32_t sh = (uint32_t)((reinterpret_cast<uintptr_t>(jb.p) + v - jb.pad) & 3);
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
-    if (v < jb.pad + 4) {  // chunks at the value's start: bytes before it are zero, its first 4 complemented
+    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], jb.sh);
+    // (uniform) the stripes that hold the value's first 4 bytes; then per lane:
+    // bytes before the value are zero, its first 4 complemented
+    if ((j << 10) < jb.pad + 4 && v < jb.pad + 4) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
@@ -124,7 +136,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, uint32_
     CrcJob lj = job(lt);
     uint64_t ls = 0;
     auto load_next = [&](uint32_t d[5]) {
-        stripe_load(lj.p, (ls << 10) + 16ull * lane, lj.pad, d);
+        stripe_load(lj, ls, d);
         if (lrem && ++ls == lj.J) {  // the next value (or stay on the last stripe: dummy reloads)
             lrem &= lrem - 1;
             if (lrem) {
