@@ -276,6 +276,7 @@ def main():
     ap.add_argument("--no-merge", action="store_true",
                     help="N>1: skip the keydir merge across ranks that follows the timed replays")
     ap.add_argument("--spec-kib", type=int, default=0, help="speculation window per chunk (KiB, 0: default)")
+    ap.add_argument("--chunk-cap", type=int, default=0, help="record slots staged per chunk (0: default)")
     ap.add_argument("--merge", action="store_true",
                     help="N=1: time the keydir merge too (a one-rank RCCL group)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
@@ -305,7 +306,8 @@ def main():
     if args.config is None:
         args.config = "c3" if world == 1 else "c4"
     t_setup = time.perf_counter()
-    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10, spec_window=args.spec_kib << 10)
+    ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10, spec_window=args.spec_kib << 10,
+                          chunk_cap=args.chunk_cap)
     info = encode_workload(ctx, args.config, world, rank)
     setup_s = time.perf_counter() - t_setup
 
