@@ -718,7 +718,7 @@ constexpr int kBlock = 16;       // capture granularity inside a slab (4 per sla
 constexpr int kBlockRows = 64;   // rows per plan block = per k_crc_rows work item
 // cache policy of k_crc_rows' arena loads (buffer aux bits: 1 sc0, 2 nt, 16 sc1)
 #ifndef GCK_ARENA_AUX
-#define GCK_ARENA_AUX 0
+#define GCK_ARENA_AUX 2
 #endif
 #ifndef GCK_CLAIM
 #define GCK_CLAIM 2
@@ -820,7 +820,7 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 //
 // MODE (ablation, gck_diag_crc_variant): 2 = no LDS table chain, 4 = no row
 // shift / wave scan, 8 = synthetic bytes instead of loads, 16 = no (c, pre)
-// stores.
+// stores, 32 = the default cache policy instead of non-temporal loads.
 template <int MODE, int NR>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
                                                    const uint4 *__restrict__ plan,
@@ -837,7 +837,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     const uint32_t nbyte = (kNibBase + (lane >> 5) * 4096 + l31) * 4;  // the lane's shift table (bytes)
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
-    const uint32_t s_rel = lane * kSlab;
+    // load k of a row: lane p + 16 b reads the 16 B at 1024 k + 64 p + 16 b,
+    // so each load instruction is one contiguous KiB of the row (whole cache
+    // lines, which the non-temporal hint needs); two permlane swap stages then
+    // give lane L the four blocks of its slab [64 L, 64 L + 64)
+    const uint32_t s_rel = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint64_t n_blocks = (n_rows + kBlockRows - 1) / kBlockRows;
     // (c, pre) stores go through a buffer resource based at the block's first
     // record: lanes without a record end store at an out-of-range offset, which
@@ -886,10 +890,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         for (int i = 0; i < NR; ++i) {
             const uint64_t r = min(row0 + i, n_rows - 1);
             const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
-            bs[i].x[0] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel, 0, GCK_ARENA_AUX);
-            bs[i].x[1] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 16, 0, GCK_ARENA_AUX);
-            bs[i].x[2] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 32, 0, GCK_ARENA_AUX);
-            bs[i].x[3] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 48, 0, GCK_ARENA_AUX);
+            constexpr int kAux = (MODE & 32) ? 0 : GCK_ARENA_AUX;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
         }
     };
     // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
@@ -899,12 +902,35 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         uint32_t w[NR][16];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
+            // w[i][4 k + c] = dword c of load k; M[b][k] = lane (p + 16 b)'s load k
+            // (= row bytes 1024 k + 64 p + 16 b).  permlane32_swap on (k, k+2)
+            // then permlane16_swap on (k, k+1) transpose M over each lane group
+            // {p, p+16, p+32, p+48}: lane p + 16 r ends with M[0..3][r] = the
+            // bytes 1024 r + 64 p + 16 b, b = 0..3, i.e. slab 16 r + p.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 w[i][4 * k] = bs[i].x[k].x;
                 w[i][4 * k + 1] = bs[i].x[k].y;
                 w[i][4 * k + 2] = bs[i].x[k].z;
                 w[i][4 * k + 3] = bs[i].x[k].w;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(w[i][4 * k + c], w[i][4 * (k + 2) + c], false, false);
+                    w[i][4 * k + c] = r[0];
+                    w[i][4 * (k + 2) + c] = r[1];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+#pragma unroll
+                for (int k = 0; k < 4; k += 2) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(w[i][4 * k + c], w[i][4 * (k + 1) + c], false, false);
+                    w[i][4 * k + c] = r[0];
+                    w[i][4 * (k + 1) + c] = r[1];
+                }
             }
             if constexpr ((MODE & 8) != 0) {
 #pragma unroll
@@ -2490,7 +2516,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
         break;
         switch (mode) {
             GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(6) GCK_VARIANT(8) GCK_VARIANT(12)
-            GCK_VARIANT(16) GCK_VARIANT(22)
+            GCK_VARIANT(16) GCK_VARIANT(22) GCK_VARIANT(32)
             default: return GCK_EINVAL;
         }
 #undef GCK_VARIANT
