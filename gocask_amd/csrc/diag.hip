@@ -1,7 +1,8 @@
 // diag.hip — measurement helpers (not on the replay path).
 //
 // gck_diag_stream_read: a plain streaming read of the resident arena (16 B per
-// lane, grid-stride, XOR-reduced so nothing is dead-code eliminated).  It is
+// lane, grid-stride, non-temporal loads — the faster of the two policies, as
+// k_crc_rows uses — XOR-reduced so nothing is dead-code eliminated).  It is
 // the practical HBM read ceiling that k_crc_rows is compared against in
 // bench.py / DESIGN.md (SURVEY.md §8d asks for the fraction of a measured
 // streaming-read kernel besides the spec peak).
@@ -154,9 +155,9 @@ extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
-    k_stream_read<false><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);  // warm-up
+    k_stream_read<true><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);  // warm-up
     GCK_HIP(hipEventRecord(a, c->stream));
-    for (int i = 0; i < iters; ++i) k_stream_read<false><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
+    for (int i = 0; i < iters; ++i) k_stream_read<true><<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
     GCK_HIP(hipEventRecord(b, c->stream));
     GCK_HIP(hipEventSynchronize(b));
     float ms = 0;
