@@ -37,7 +37,7 @@ enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 #ifndef GCK_NR
-#define GCK_NR 2
+#define GCK_NR 1
 #endif
 constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes at once
 constexpr uint32_t kNibBase = 32768;
