@@ -1262,14 +1262,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
 #endif
         const uint4 vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)rs, (uint32_t)bsp, V, f)
                                           : *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
-        uint32_t pw[11];
+        // header + keys up to 24 B as three 16 B loads (dword aligned; the
+        // arena is padded): every load instruction of a wave touches 64
+        // records' lines, so the count of instructions, not bytes, is the cost
+        uint32_t pw[12];
 #pragma unroll
-        for (int i = 0; i < 11; ++i) pw[i] = (GCK_FIN_XP & 1) ? (uint32_t)rs * (i + 3) : wp[i];  // header + keys up to 24 B (the arena is padded)
+        for (int i = 0; i < 3; ++i) {
+            const u32x4_a4 v = (GCK_FIN_XP & 1) ? u32x4_a4{(uint32_t)rs * (i + 3), 1u, 2u, 3u}
+                                                : reinterpret_cast<const u32x4_a4 *>(wp)[i];
+            pw[4 * i] = v.x;
+            pw[4 * i + 1] = v.y;
+            pw[4 * i + 2] = v.z;
+            pw[4 * i + 3] = v.w;
+        }
         uint4 vend = make_uint4(0, 0, 0, 0);
         if (!have) vend = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)bse, 1, 2, 3) : *reinterpret_cast<const uint4 *>(arena + bse);
-        uint32_t rr[9];  // row sums rend[fr .. fr + 8] the record crosses
+        uint32_t rr[12];  // row sums rend[fr .. fr + 11] the record crosses (three 16 B loads; rend is padded)
 #pragma unroll
-        for (int j = 0; j < 9; ++j) rr[j] = fr + j < lr ? ((GCK_FIN_XP & 8) ? (uint32_t)fr * 7 + j : rend[fr + j]) : 0u;
+        for (int i = 0; i < 3; ++i) {
+            const u32x4_a4 v = (GCK_FIN_XP & 8) ? u32x4_a4{(uint32_t)fr * 7 + i, 1u, 2u, 3u}
+                                                : reinterpret_cast<const u32x4_a4 *>(rend + fr)[i];
+            rr[4 * i] = v.x;
+            rr[4 * i + 1] = v.y;
+            rr[4 * i + 2] = v.z;
+            rr[4 * i + 3] = v.w;
+        }
         const uint32_t xi = (GCK_FIN_XP & 2) ? d * 0x9E3779B9u : xinv[d];
         const uint32_t xv0 = (GCK_FIN_XP & 2) ? V * 0x85EBCA6Bu : xb[V & 0xFFFF];
         const uint32_t xhi = (GCK_FIN_XP & 2) ? (V >> 16) + 1 : xa[V >> 16];
@@ -1297,9 +1314,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         } else {
             uint32_t h_acc = rr[0] ^ a_rs;
 #pragma unroll
-            for (int j = 1; j < 9; ++j)
+            for (int j = 1; j < 12; ++j)
                 if (fr + j < lr) h_acc = z4096(Tz, h_acc) ^ rr[j];
-            for (uint64_t row = fr + 9; row < lr; ++row) h_acc = z4096(Tz, h_acc) ^ rend[row];  // records over 36 KiB
+            for (uint64_t row = fr + 12; row < lr; ++row) h_acc = z4096(Tz, h_acc) ^ rend[row];  // records over 48 KiB
             acc ^= z4096(Tz, h_acc);
         }
         // F(s, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
@@ -1316,12 +1333,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint32_t nw = L / 4;
         uint32_t y = 0;
 #pragma unroll
-        for (uint32_t i = 1; i < 11; ++i) {
+        for (uint32_t i = 1; i < 12; ++i) {
             if (i < nw) p = slice4t(T, p ^ pw[i]);
             y = i == nw ? pw[i] : y;
         }
-        for (uint32_t i = 11; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
-        if (nw >= 11) y = wp[nw];
+        for (uint32_t i = 12; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
+        if (nw >= 12) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
         // x^(8V) = xa[V >> 16] * xb[V & 0xFFFF]; crc32(0^V) from zl below 2^17
         const uint32_t xv = V < 65536 ? xv0 : gf_mul_lds(ldsb, mw, rxb, xhi, xv0);
