@@ -59,6 +59,45 @@ __global__ __launch_bounds__(1024) void k_stream_rows(const uint8_t *__restrict_
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// The same with non-temporal loads in k_crc_rows' current geometry (lane
+// p + 16 b at 1024 j + 64 p + 16 b, one row per step, the next row issued
+// before the current one is consumed): BLOCKS = each wavefront streams whole
+// 64-row blocks (256 KiB, block index strided over the wavefronts), as
+// k_crc_rows' work items; otherwise rows are strided over the wavefronts
+// (neighbouring wavefronts read neighbouring rows).
+template <bool BLOCKS>
+__global__ __launch_bounds__(1024) void k_stream_rows_nt(const uint8_t *__restrict__ arena, uint64_t n_rows,
+                                                         uint32_t *sink) {
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63, off = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint64_t wv = (uint64_t)blockIdx.x * 16 + (threadIdx.x >> 6), nw = (uint64_t)gridDim.x * 16;
+    auto row_of = [&](uint64_t k) -> uint64_t {  // the wave's k-th row
+        return BLOCKS ? ((k / 64) * nw + wv) * 64 + (k % 64) : k * nw + wv;
+    };
+    auto ld = [&](uint64_t row, v4u (&v)[4]) {
+        const uint64_t r = min(row, n_rows - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(arena + r * 4096 + off + 1024 * j));
+    };
+    uint32_t acc = 0;
+    v4u A[4], B[4];
+    uint64_t k = 0;
+    if (row_of(0) >= n_rows) return;
+    ld(row_of(0), A);
+    for (;;) {
+        ld(row_of(k + 1), B);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc ^= A[j].x ^ A[j].y ^ A[j].z ^ A[j].w;
+        if (row_of(k + 1) >= n_rows) break;
+        ld(row_of(k + 2), A);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc ^= B[j].x ^ B[j].y ^ B[j].z ^ B[j].w;
+        if (row_of(k + 2) >= n_rows) break;
+        k += 2;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 // Random-access probes with k_walk's access shape (a 16 B load per hop):
 // DEP = each lane's next address depends on the bytes it just loaded (a chain
 // walk); otherwise the lane's hops are independent (8 loads in flight).
@@ -99,11 +138,12 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t *__restrict__ arena
 using namespace gck;
 
 // pattern 0: k_stream_read; 15: the same with non-temporal loads; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>;
+// 16: k_stream_rows_nt, rows strided over the wavefronts; 17: the same in 64-row blocks;
 // 3..8: k_chase<dependent> with 8 Ki << (pattern-3) lanes; 9..14: the same
 // lane counts, independent loads.  The chase patterns make 10,240,000 hops in
 // all (C3's record count); *gbs reports hops per ns (G hops/s) for them.
 extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs) {
-    if (!ctx || iters <= 0 || pattern < 0 || pattern > 15) return GCK_EINVAL;
+    if (!ctx || iters <= 0 || pattern < 0 || pattern > 17) return GCK_EINVAL;
     Ctx *c = &ctx->c;
     GCK_HIP(hipSetDevice(c->device));
     if (!c->n_rows) return GCK_EINVAL;
@@ -111,7 +151,11 @@ extern "C" int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, dou
     const uint32_t lanes = pattern >= 3 && pattern <= 14 ? 8192u << ((pattern - 3) % 6) : 0u;
     const uint32_t hops = lanes ? ((10240000u / lanes + 7) & ~7u) : 0u;
     auto launch = [&]() {
-        if (pattern == 15)
+        if (pattern == 16)
+            k_stream_rows_nt<false><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
+        else if (pattern == 17)
+            k_stream_rows_nt<true><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink);
+        else if (pattern == 15)
             k_stream_read<true><<<(uint32_t)c->n_cu * 8, 256, 0, c->stream>>>(c->arena.as<uint4>(), c->arena_len / 16, sink);
         else if (pattern >= 9)
             k_chase<false><<<(lanes + 255) / 256, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), c->arena_len, lanes, hops,

@@ -1076,6 +1076,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 // the next step's rows: this block, or the next block's first
                 const uint64_t nrow = st + 1 < kSteps ? row_b + (uint64_t)(st + 1) * NR : qn * kBlockRows;
                 issue(nrow, buf[(u + 1) & 1]);
+                // keep the next row's loads here, ahead of this row's compute:
+                // left alone, the scheduler sinks them past most of the chain
+                // (reusing the current row's registers), so only one row was
+                // in flight while the wave computed
+                __builtin_amdgcn_sched_barrier(0);
                 process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u & 1],
                         rend_buf);
             }

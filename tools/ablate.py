@@ -16,7 +16,7 @@ for mode in [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else "
     out[f"mode{mode}_ms"] = round(ms.value, 3)
     out[f"mode{mode}_gbs"] = round(st["bytes"] / ms.value / 1e6, 1)
 gbs = ctypes.c_double()
-for pat in [0, 1, 2, 15]:
+for pat in [0, 1, 2, 15, 16, 17]:
     g._lib.check(ctx._L.gck_diag_stream_pattern(ctx._h, pat, 5, ctypes.byref(ms), ctypes.byref(gbs)))
     out[f"stream_pattern{pat}_ms"] = round(ms.value, 3)
 print(json.dumps(out))
