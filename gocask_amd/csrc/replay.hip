@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
         // ---- every dependent load of this iteration
 #ifndef GCK_FIN_XP
-#define GCK_FIN_XP 0  // ablation (timing only, wrong results): 1 no arena loads, 2 no table loads, 4 no stores, 8 no row sums
+#define GCK_FIN_XP 0  // ablation (timing only, wrong results): 1 no arena loads, 2 no table loads, 4 no stores, 8 no row sums, 32 no header + key loads
 #endif
         const uint4 vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)rs, (uint32_t)bsp, V, f)
                                           : *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
@@ -1287,7 +1287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         uint32_t pw[12];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = (GCK_FIN_XP & 1) ? u32x4_a4{(uint32_t)rs * (i + 3), 1u, 2u, 3u}
+            const u32x4_a4 v = (GCK_FIN_XP & 33) ? u32x4_a4{(uint32_t)rs * (i + 3), 1u, 2u, 3u}
                                                 : reinterpret_cast<const u32x4_a4 *>(wp)[i];
             pw[4 * i] = v.x;
             pw[4 * i + 1] = v.y;

@@ -54,7 +54,7 @@ def main():
         stats[short(r["Name"])] = float(r["AverageNs"])
     crc_key = next((k for k in summary if k.startswith("k_crc_rows<")), None)
     crc = summary.get(crc_key, {})
-    sr = summary.get("k_stream_read", {})
+    sr = next((v for k, v in summary.items() if k.startswith("k_stream_read")), {})
     out = {
         "config": cfg,
         "source": f"profiles/{tag}/pmc_summary.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)",
