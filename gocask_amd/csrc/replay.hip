@@ -1147,7 +1147,9 @@ __device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
 // byte mw + 256 v + 4 l: each lane of a 32-lane group on its own bank), then
 // Horner from the highest-degree nibble with y * x^4 = (y >> 4) ^ R[y & 15].
 // About 60 VALU + 15 LDS writes + 15 LDS reads, against 160 VALU for gf_mul.
-// M[0] must be zero (written once per kernel); mw = the wave's region + 4 lane.
+// M[0] must be zero (written once per kernel); mw = the wave's region + 4 lane;
+// rb = the lane's copy of R (32 copies, entry e of copy l at + 128 e + 4 l:
+// conflict-free, where one 16-entry copy put 32 lanes on 16 banks).
 __device__ __forceinline__ uint32_t mulx(uint32_t v) {
     return (v >> 1) ^ (kPoly & (uint32_t)(-(int32_t)(v & 1u)));
 }
@@ -1165,7 +1167,7 @@ __device__ __forceinline__ uint32_t gf_mul_lds(char *lds, uint32_t mw, uint32_t 
     uint32_t y = ent(7);
 #pragma unroll
     for (int t = 6; t >= 0; --t) {
-        const uint32_t r = *reinterpret_cast<const uint32_t *>(lds + (rb | ((y << 2) & 0x3Cu)));
+        const uint32_t r = *reinterpret_cast<const uint32_t *>(lds + (rb | ((y << 7) & 0x780u)));
         y = xor3(y >> 4, r, ent(t));
     }
     return y;
@@ -1211,20 +1213,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                                                   uint32_t *counters) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
-    // gf_mul_lds: one 4 KiB table region per wave, then y * x^4 = (y >> 4) ^ R[y & 15]
-    __shared__ uint32_t Gm[4 * 1024 + 16];
-    // output staging: a wave's 64 gck_rec (2560 B), stored back as 16 B per lane
-    __shared__ uint4 Ost[4][64 * sizeof(gck_rec) / 16];
+    // gf_mul_lds: one 4 KiB table region per wave, then R (y * x^4 = (y >> 4) ^
+    // R[y & 15]) in 32 copies.  A wave's output staging (64 gck_rec = 2560 B)
+    // reuses bytes 256.. of its region (the M entries 1..15, rewritten by every
+    // gf_mul_lds; LDS operations of one wave execute in order)
+    __shared__ uint32_t Gm[4 * 1024 + 512];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
         Tz[i] = zrow[i];
         T[i] = g_slice[i];
     }
-    if (threadIdx.x < 16) Gm[4096 + threadIdx.x] = mulx(mulx(mulx(mulx(threadIdx.x))));
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) Gm[4096 + i] = mulx(mulx(mulx(mulx(i >> 5))));
     Gm[(threadIdx.x >> 6) * 1024 + (threadIdx.x & 63)] = 0;  // entry 0 of every lane
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     char *const ldsb = reinterpret_cast<char *>(Gm);  // byte offsets into Gm
-    const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = 4096 * 4;
+    const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = 4096 * 4 + (lane & 31) * 4;
+    uint4 *const Ost = reinterpret_cast<uint4 *>(ldsb + (threadIdx.x >> 6) * 4096 + 256);
     const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
     uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
     // wave-uniform loop: the 64 lanes hold 64 consecutive records.  Loads in
@@ -1370,7 +1374,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
             // (three 8/16 B stores per lane at a 40 B stride write partial lines)
             const uint64_t fo = rs - fb;
             const bool tomb = kv.x == 0;
-            uint2 *sl = reinterpret_cast<uint2 *>(reinterpret_cast<char *>(Ost[threadIdx.x >> 6]) + lane * sizeof(gck_rec));
+            uint2 *sl = reinterpret_cast<uint2 *>(reinterpret_cast<char *>(Ost) + lane * sizeof(gck_rec));
             sl[0] = make_uint2((uint32_t)fo, (uint32_t)(fo >> 32));                    // rec_off
             sl[1] = make_uint2(f, tomb ? kv.y : kv.x);                                 // file, key_len
             sl[2] = make_uint2(cf + (uint32_t)fo + 16u + kv.x, kv.y);                  // value_pos, value_size
@@ -1382,7 +1386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
 #pragma unroll
             for (uint32_t k = 0; k < 3; ++k) {
                 const uint32_t off = k * 1024 + lane * 16;
-                const uint4 v = Ost[threadIdx.x >> 6][off / 16];
+                const uint4 v = Ost[off / 16];
                 if (off + 16 <= nbytes) {
                     if (!(GCK_FIN_XP & 4)) *reinterpret_cast<u32x4_a4 *>(dst + off) = u32x4_a4{v.x, v.y, v.z, v.w};
                 } else if (off < nbytes) {  // an odd record count ends mid-chunk
