@@ -470,20 +470,62 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 
+// Lane l owns the 64 consecutive counts at b0 + 64 l: all of them are loaded
+// at once (one memory round trip per block; a loop of 64-wide steps waited
+// for each step's load: 25 us for C3's 64 Ki chunks), summed per lane, the
+// lane totals scanned over the wave (64-bit: split in 24-bit halves, as
+// k_scan_top), and the lane writes its 64 bases.  Vector loads and stores
+// where the group's chunk offset leaves them 16 B aligned.
 __global__ __launch_bounds__(64) void k_scan_local(const uint32_t *__restrict__ ch_count,
                                                    uint64_t *__restrict__ rec_base, uint64_t *__restrict__ bsum,
                                                    uint32_t n) {
+    static_assert(kScanBlock == 64 * 64, "a lane owns 64 counts");
     const uint32_t lane = threadIdx.x;
-    const uint32_t b0 = blockIdx.x * kScanBlock;
-    uint64_t run = 0;
-    for (uint32_t i0 = b0; i0 < min(b0 + kScanBlock, n); i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t v = i < n ? ch_count[i] : 0u;
-        const uint32_t inc = wave_incl_sum(v);
-        if (i < n) rec_base[i] = run + inc - v;
-        run += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    const uint32_t i0 = blockIdx.x * kScanBlock + lane * 64;
+    uint32_t v[64];
+    const bool vec_in = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(ch_count + i0) & 15) == 0;
+    const bool vec_out = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(rec_base + i0) & 15) == 0;
+    if (vec_in) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(ch_count + i0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint4 x = src[k];
+            v[4 * k] = x.x;
+            v[4 * k + 1] = x.y;
+            v[4 * k + 2] = x.z;
+            v[4 * k + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) v[k] = i0 + k < n ? ch_count[i0 + k] : 0u;
     }
-    if (lane == 0) bsum[blockIdx.x] = run;
+    uint64_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) tot += v[k];
+    const uint32_t lo = wave_incl_sum((uint32_t)(tot & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(tot >> 24));
+    const uint64_t inc = ((uint64_t)hi << 24) + lo;
+    uint64_t run = inc - tot;  // this lane's first base within the block
+    if (vec_out) {
+        u32x4 *dst = reinterpret_cast<u32x4 *>(rec_base + i0);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const uint64_t a = run, b = run + v[2 * k];
+            run = b + v[2 * k + 1];
+            u32x4 o;
+            o.x = (uint32_t)a;
+            o.y = (uint32_t)(a >> 32);
+            o.z = (uint32_t)b;
+            o.w = (uint32_t)(b >> 32);
+            dst[k] = o;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            if (i0 + k < n) rec_base[i0 + k] = run;
+            run += v[k];
+        }
+    }
+    if (lane == 63) bsum[blockIdx.x] = inc;
 }
 
 __global__ __launch_bounds__(64) void k_scan_top(uint64_t *__restrict__ bsum, uint32_t nb,
