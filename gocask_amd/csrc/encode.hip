@@ -483,6 +483,25 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
                 if (X >= sk) r = k;
             }
             rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
+            // (uniform) the whole row inside one record's value: most rows
+            // of large records; its fields by readlane, no permutes
+            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr && R + 1024 <= O1 && !(GCK_ENC_XP & 2)) {
+                const int src = (int)rr;
+                const uint64_t s0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oo >> 32), src) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oo, src);
+                const uint64_t kl0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(kl >> 32), src) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kl, src);
+                const uint64_t vl0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(vl >> 32), src) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vl, src);
+                const uint64_t vs0 = s0 + 16 + kl0;  // the value's first output byte
+                if (R >= vs0 && R + 1024 <= vs0 + vl0) {
+                    const uint64_t vo0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(vo >> 32), src) << 32) |
+                                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vo, src);
+                    const uint4 v = load16u(vals + vo0 + (X - vs0));
+                    *reinterpret_cast<uint4 *>(out + X) = v;
+                    continue;
+                }
+            }
             // at most two records meet in a chunk: r, and r + 1 from its end on
             uint32_t w[4] = {0u, 0u, 0u, 0u};
             uint32_t mask = 0;  // bytes of the chunk written from this group's records
