@@ -401,6 +401,7 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0 = 0, lb1 = 0, kl_shift = 0;
     CrcTabs *T = nullptr;  // MODE 1 only (static LDS of the one kernel that uses it)
+    const uint64_t key_total = key_off[n], val_total = val_off[n];  // blob sizes (readable + 4 bytes)
     if constexpr (MODE == 1) T = &enc_tabs();
     // the slicing tables, built here (no context): T0..T3 into Zs, expanded
     // into the conflict-free image, then Zs itself
@@ -529,16 +530,36 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
                 } else if (GCK_ENC_XP & 1) {
                     mask = 0xFFFFu;  // ablation: no byte path (wrong bytes)
                 } else {
-                    // byte by byte, the 16 source bytes loaded at once (addresses
-                    // clamped into the key / value, so every load is in range)
+                    // byte by byte.  The key / value bytes come from 16 B
+                    // windows aligned to the chunk (chunk byte i = key byte
+                    // kst + i, value byte vst + i: one unaligned load each
+                    // instead of 16 byte loads); where a window would leave
+                    // its blob (the batch's first and last records), from byte
+                    // loads clamped into the key / value
                     uint32_t by[16];
+                    const int64_t kst = (int64_t)(X - s) - 16, vst = kst - (int64_t)k_l;
+                    const bool need_k = k_l && b0 < s + 16 + k_l && b1 > s + 16;
+                    const bool need_v = v_l && b1 > s + 16 + k_l;
+                    const bool win = (!need_k || ((int64_t)k_o + kst >= 0 && k_o + kst + 16 <= key_total)) &&
+                                     (!need_v || ((int64_t)v_o + vst >= 0 && v_o + vst + 16 <= val_total));
+                    if (win) {
+                        const uint4 kw = need_k ? load16u(kp + kst) : make_uint4(0, 0, 0, 0);
+                        const uint4 vw = need_v ? load16u(vp + vst) : make_uint4(0, 0, 0, 0);
+                        const uint32_t kd[4] = {kw.x, kw.y, kw.z, kw.w}, vd[4] = {vw.x, vw.y, vw.z, vw.w};
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const uint64_t q = X + i - s;  // may be past the record: clamped, unused
-                        const bool in_key = q < 16 + k_l || v_l == 0;
-                        const uint64_t kq = q < 16 ? 0 : min(q - 16, k_l - 1);
-                        const uint64_t vq = q < 16 + k_l ? 0 : min(q - 16 - k_l, v_l - 1);
-                        by[i] = in_key ? kp[kq] : vp[vq];
+                        for (int i = 0; i < 16; ++i) {
+                            const uint64_t q = X + i - s;
+                            by[i] = ((q < 16 + k_l || v_l == 0) ? kd[i >> 2] : vd[i >> 2]) >> (8 * (i & 3)) & 0xFFu;
+                        }
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 16; ++i) {
+                            const uint64_t q = X + i - s;  // may be past the record: clamped, unused
+                            const bool in_key = q < 16 + k_l || v_l == 0;
+                            const uint64_t kq = q < 16 ? 0 : min(q - 16, k_l - 1);
+                            const uint64_t vq = q < 16 + k_l ? 0 : min(q - 16 - k_l, v_l - 1);
+                            by[i] = in_key ? kp[kq] : vp[vq];
+                        }
                     }
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
