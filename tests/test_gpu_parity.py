@@ -516,12 +516,15 @@ def test_keys_longer_than_speculation_bound(g, orc):
 
 
 # ------------------------------------- pipelined host-in/host-out replay ---
-def test_replay_grouped_equals_oracle(g, orc, monkeypatch):
+@pytest.mark.parametrize("fsize", [200 << 20, (215 << 20) + (100 << 10)])
+def test_replay_grouped_equals_oracle(g, orc, monkeypatch, fsize):
     # gck_replay / gck_replay_into cut the files into >= 1 GiB groups after
     # files that reset lastOffset; with 12 x ~200 MiB files and the active
-    # file in the middle, groups must neither split a carry nor reorder
+    # file in the middle, groups must neither split a carry nor reorder.
+    # (~215.1 MiB files: 431 chunks each, so a later group's first chunk is
+    # not a multiple of 4 and k_scan_local takes its unaligned path)
     kw = dict(seed=46, val_fixed=0, key_min=8, key_max=24, key_universe=200000, tomb_permille=10,
-              flip_permille=10, max_file_size=200 << 20, n_files=12)
+              flip_permille=10, max_file_size=fsize, n_files=12)
     files, names = orc.gen_corpus(**kw)
     wf, _ = walk_sorted(files, names)
     reset = [True] * len(wf)
