@@ -423,8 +423,7 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
         __syncthreads();
         fill_slice_lds(T->S, t4);
         __syncthreads();
-        const uint32_t z = xpow8n(1008);
-        for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) T->Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
+        fill_zs(*T);
         __syncthreads();
         slice_bases(lane, lb0, lb1);
         kl_shift = xpow8n(16ull * (63 - lane));
@@ -461,8 +460,8 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
             const uint64_t todo = __ballot(have && !small);
             if (todo) {
                 const uint32_t c = wave_crcs(
-                    todo, [&](int it) { return (__shfl((int)del, it) ? keys : vals) + __shfl(po, it); }, L,
-                    kl_shift, *T, lb0, lb1);
+                    todo, [&](int it) { return (__shfl((int)del, it) ? keys : vals) + __shfl(po, it); }, L, *T,
+                    lb0, lb1, [&](uint32_t A) { return lanes_combine_gmul(kl_shift, A); });
                 if ((todo >> lane) & 1) crc = c;
             }
             if (have) crcs[mine] = crc;

@@ -8,17 +8,34 @@
 namespace gck {
 
 // LDS tables: the conflict-free slicing-by-4 image (gck_crc_lds.h, 128 KiB,
-// from the context's global tables) and multiplication by the constant Z_1008
-// as four byte tables: Z(A) = XOR_k Zs[k][byte k of A] (Z is linear in A).
+// from the context's global tables); multiplication by the constant Z_1008
+// as four byte tables, Z(A) = XOR_k Zs[k][byte k of A] (Z is linear in A);
+// the lane shifts Z_{16 (31 - (l & 31))} as eight nibble tables per lane
+// (entry (q, v) of lane l at word 512 q + 32 v + (l & 31): each lane of a
+// 32-lane LDS group on its own bank, 16 KiB); Z_512 as four byte tables
+// (lanes 0..31 are a further 512 bytes from the stripe end; read with a
+// wave-uniform address only, so one copy has no conflicts).  152 KiB.  Ls and
+// Z512 follow the slicing tables in the context's global table (built once
+// per process on the host, replay.hip make_tables): kGLs, kGZ512 words in.
+constexpr uint32_t kLaneShiftWords = 8 * 16 * 32;
+constexpr uint32_t kGLs = 1024, kGZ512 = kGLs + kLaneShiftWords, kGTabWords = kGZ512 + 1024;
 struct CrcTabs {
     uint32_t S[kSliceLdsWords];
     uint32_t Zs[4][256];
+    uint32_t Ls[kLaneShiftWords];
+    uint32_t Z512[4][256];
 };
-
-__device__ inline void crc_tables(CrcTabs &t, const uint32_t *__restrict__ g_slice) {
-    fill_slice_lds(t.S, g_slice);
+__device__ inline void fill_zs(CrcTabs &t) {
     const uint32_t z = xpow8n(1008);
     for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) t.Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
+}
+
+// All of CrcTabs from the context's global table.
+__device__ inline void crc_tables(CrcTabs &t, const uint32_t *__restrict__ g_tab) {
+    fill_slice_lds(t.S, g_tab);
+    fill_zs(t);
+    for (uint32_t e = threadIdx.x; e < kLaneShiftWords; e += blockDim.x) t.Ls[e] = g_tab[kGLs + e];
+    for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) (&t.Z512[0][0])[e] = g_tab[kGZ512 + e];
     __syncthreads();
 }
 
@@ -35,6 +52,34 @@ __device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b) {
 
 __device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
     return Z[0][a & 0xFF] ^ Z[1][(a >> 8) & 0xFF] ^ Z[2][(a >> 16) & 0xFF] ^ Z[3][a >> 24];
+}
+
+// crc32.ChecksumIEEE from the lanes' stripe registers A (lane l's chunk is
+// followed by 16 (63 - l) bytes of the value): Z_{16 (31 - (l & 31))}(A) by
+// the lane's nibble tables (address: nibble at bits 7..10 merged with the
+// lane's bank offset lb0 in one v_bitop3, table q at + 2048 q bytes), XOR over
+// each half-wave, then Z_512 of the lower half's sum (uniform), complemented.
+// Replaces a 32-step branch-free multiply by the lane constant (~160 VALU per
+// value; lanes_combine_gmul, for kernels without the tables).
+__device__ __forceinline__ uint32_t lanes_combine(const CrcTabs &t, uint32_t lb0, uint32_t A) {
+    uint32_t x8[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int sh = 4 * q;
+        const uint32_t x = sh >= 7 ? A >> (sh - 7) : A << (7 - sh);
+        x8[q] = lds_at(t.Ls + q * 512, __builtin_amdgcn_bitop3_b32(x, 0x780u, lb0, 0xEA));
+    }
+    uint32_t f = xor3(xor3(x8[0], x8[1], x8[2]), xor3(x8[3], x8[4], x8[5]), x8[6] ^ x8[7]);
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)f, 0), hi = (uint32_t)__builtin_amdgcn_readlane((int)f, 32);
+    return ~(zmul(t.Z512, lo) ^ hi);
+}
+__device__ __forceinline__ uint32_t lanes_combine_gmul(uint32_t kl, uint32_t A) {
+    uint32_t f = gmul(kl, A);  // kl = x^(8 * 16 (63 - lane))
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
+    return ~f;
 }
 
 // The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
@@ -90,8 +135,8 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32
 // (coalesced loads).  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner over
 // the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement of the
 // value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).  Lane l's
-// part is finally shifted past the 16 (63-l) bytes after it (kl = x^(8 * 16
-// (63-l))) and the lanes XOR-reduced: F(~0, V); crc = ~that.
+// part is finally shifted past the 16 (63-l) bytes after it and the lanes
+// XOR-reduced (lanes_combine): F(~0, V); crc = ~that.
 //
 // One stripe of the value at virtual stripe j into A:
 __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, const uint32_t d[5], uint32_t A,
@@ -131,9 +176,9 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
 #define GCK_RING 4
 #endif
 constexpr int kRing = GCK_RING;
-template <class PtrOf>
-__device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, uint32_t kl, const CrcTabs &t, uint32_t lb0,
-                              uint32_t lb1) {
+template <class PtrOf, class Combine>
+__device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const CrcTabs &t, uint32_t lb0,
+                              uint32_t lb1, Combine combine) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t out = 0;
     auto job = [&](int it) { return CrcJob(ptr_of(it), __shfl(len, it)); };
@@ -171,10 +216,8 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, uint32_
                 A = fold_stripe(cj, cs, ring[k], A, t, lb0, lb1);
                 load_next(ring[k]);
                 if (++cs == cj.J) {  // value done
-                    uint32_t f = gmul(kl, A);
-#pragma unroll
-                    for (int m = 32; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
-                    if (lane == (uint32_t)ct) out = ~f;
+                    const uint32_t f = combine(A);
+                    if (lane == (uint32_t)ct) out = f;
                     A = 0;
                     cs = 0;
                     crem &= crem - 1;

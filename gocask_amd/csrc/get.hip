@@ -101,7 +101,6 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0, lb1;
     slice_bases(lane, lb0, lb1);
-    const uint32_t kl = xpow8n(16ull * (63 - lane));  // lane l's chunk is followed by 16 (63-l) bytes of its stripe
     const uint64_t groups = (n + 63) >> 6, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); gi < groups; gi += waves) {
         const uint64_t mine = (gi << 6) + lane;
@@ -118,7 +117,8 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
             if (small) crc = c;
         }
         if (todo) {
-            const uint32_t c = wave_crcs(todo, [&](int it) { return arena + __shfl(off, it); }, len, kl, T, lb0, lb1);
+            const uint32_t c = wave_crcs(todo, [&](int it) { return arena + __shfl(off, it); }, len, T, lb0, lb1,
+                                         [&](uint32_t A) { return lanes_combine(T, lb0, A); });
             if ((todo >> lane) & 1) crc = c;
         }
         if (dst) {  // the values that passed, copied by the whole wave

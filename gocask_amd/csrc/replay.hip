@@ -22,6 +22,7 @@
 
 #include "gck_internal.h"
 #include "gck_crc_lds.h"
+#include "gck_crc_wave.h"
 
 namespace gck {
 
@@ -1497,6 +1498,17 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
     for (int t = 1; t < 4; ++t)
         for (uint32_t n = 0; n < 256; ++n)
             slice[t * 256 + n] = (slice[(t - 1) * 256 + n] >> 8) ^ slice[slice[(t - 1) * 256 + n] & 0xff];
+    // the wave CRC's lane shifts and Z_512 after the slicing tables
+    // (gck_crc_wave.h: kGLs, kGZ512)
+    slice.resize(kGTabWords, 0);
+    for (uint32_t l = 0; l < 32; ++l) {
+        const uint32_t K = xpow8n(16ull * (31 - l));
+        for (uint32_t q = 0; q < 8; ++q)
+            for (uint32_t v = 0; v < 16; ++v) slice[kGLs + q * 512 + v * 32 + l] = multmodp(K, v << (4 * q));
+    }
+    const uint32_t z5 = xpow8n(512);
+    for (int k = 0; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) slice[kGZ512 + k * 256 + b] = multmodp(z5, b << (8 * k));
     nib.assign(64 * 8 * 16, 0);
     for (int l = 0; l < 64; ++l) {
         const uint32_t K = xpow8n((uint64_t)kSlab * (63 - l));
