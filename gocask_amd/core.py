@@ -368,6 +368,31 @@ class ReplayContext:
                                            ctypes.byref(got)))
         return recs, ms.value
 
+    # -- merge (compaction) and hint files (include/gocask_hip.h) --
+    def compact(self, max_file_size, fetch=True):
+        """Merge the live records of the device keydir (keydir() first, without
+        tombstones) into new data files + hint files (gck_ctx_compact): with
+        fetch, (list of data-file bytes, list of hint-file bytes, device ms);
+        else (files, data bytes, hint bytes, device ms), outputs on the device."""
+        nf, nd, nh, ms = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_double()
+        check(self._L.gck_ctx_compact(self._h, int(max_file_size), ctypes.byref(nf), ctypes.byref(nd),
+                                      ctypes.byref(nh), ctypes.byref(ms)))
+        if not fetch:
+            return nf.value, nd.value, nh.value, ms.value
+        data = np.zeros(max(nd.value, 1), dtype=np.uint8)
+        hints = np.zeros(max(nh.value, 1), dtype=np.uint8)
+        fsz = np.zeros(max(nf.value, 1), dtype=np.uint64)
+        hsz = np.zeros(max(nf.value, 1), dtype=np.uint64)
+        check(self._L.gck_ctx_fetch_compact(self._h, data.ctypes.data, fsz.ctypes.data, hints.ctypes.data,
+                                            hsz.ctypes.data))
+        files, hfiles, a, b = [], [], 0, 0
+        for k in range(nf.value):
+            files.append(data[a:a + int(fsz[k])].copy())
+            hfiles.append(hints[b:b + int(hsz[k])].copy())
+            a += int(fsz[k])
+            b += int(hsz[k])
+        return files, hfiles, ms.value
+
     # -- batched Get / scrub (include/gocask_hip.h, SURVEY.md §8f f3) --
     def get_batch(self, keys, values=True):
         """DB.Get for every key against the device keydir (keydir() first):

@@ -1,0 +1,366 @@
+// compact.hip — merge (compaction) and hint files on the device (SURVEY.md
+// §8f f4: "merging and hint files", the reference's roadmap item README.md:60).
+//
+// After gck_ctx_keydir (live Puts only), the live records, in walk order, are
+// written as new data files exactly as DB.Put would write them into a fresh
+// database with MaxDataFileSize M (core/db.go:185-231: an entry that does not
+// fit rotates first, rotateDataFile:214-231), each record's bytes verbatim
+// (header, key, value: CRCs and timestamps unchanged).  One hint file per data
+// file lists its records as Bitcask hint entries, little-endian
+//   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
+// (ValuePos = the value's offset in the merged file mod 2^32, as
+// core/keydir.go:25 would set it), so a later start can fill the keydir
+// without reading values.
+//
+// Kernels: sizes and two-level exclusive scans of record and hint-entry
+// sizes; the rotation points (one wavefront, a 64-way search per file); the
+// data bytes (a wavefront per group of 64 records, 16 B output chunks, each
+// from one or two chunk-aligned windows of the resident arena); the hint
+// entries (a lane per record).
+#include "gck_internal.h"
+
+namespace gck {
+
+typedef uint32_t u32x4_a4c __attribute__((ext_vector_type(4), aligned(4)));
+
+constexpr uint32_t kCmpBlock = 1024;  // records per first-level scan block
+
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(v, d);
+        if ((threadIdx.x & 63) >= (uint32_t)d) v += o;
+    }
+    return v;
+}
+
+// Per record: data size 16 + KeySize + ValueSize and hint size 16 + KeySize;
+// exclusive scans within blocks of kCmpBlock, block totals to bsum / hbsum.
+__global__ __launch_bounds__(kCmpBlock) void k_cmp_sizes(const gck_rec *__restrict__ kd, uint64_t n,
+                                                         uint64_t *__restrict__ pos, uint64_t *__restrict__ hpos,
+                                                         uint64_t *__restrict__ bsum, uint64_t *__restrict__ hbsum) {
+    __shared__ uint64_t wt[2][kCmpBlock / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * kCmpBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint64_t sz = 0, hs = 0;
+    if (i < n) {
+        const gck_rec r = kd[i];
+        sz = 16ull + r.key_len + r.value_size;
+        hs = 16ull + r.key_len;
+    }
+    const uint64_t a = wave_incl_sum64(sz), b = wave_incl_sum64(hs);
+    if (lane == 63) {
+        wt[0][w] = a;
+        wt[1][w] = b;
+    }
+    __syncthreads();
+    uint64_t pa = 0, pb = 0;
+    for (uint32_t k = 0; k < w; ++k) {
+        pa += wt[0][k];
+        pb += wt[1][k];
+    }
+    if (i < n) {
+        pos[i] = pa + a - sz;
+        hpos[i] = pb + b - hs;
+    }
+    if (threadIdx.x == kCmpBlock - 1) {
+        bsum[blockIdx.x] = pa + a;
+        hbsum[blockIdx.x] = pb + b;
+    }
+}
+
+// One wavefront: exclusive scan of the block totals (in place), totals at [nb].
+__global__ __launch_bounds__(64) void k_cmp_top(uint64_t *__restrict__ bsum, uint64_t *__restrict__ hbsum, uint64_t nb) {
+    uint64_t ra = 0, rb = 0;
+    for (uint64_t i0 = 0; i0 < nb; i0 += 64) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t va = i < nb ? bsum[i] : 0, vb = i < nb ? hbsum[i] : 0;
+        const uint64_t a = wave_incl_sum64(va), b = wave_incl_sum64(vb);
+        if (i < nb) {
+            bsum[i] = ra + a - va;
+            hbsum[i] = rb + b - vb;
+        }
+        ra += __shfl(a, 63);
+        rb += __shfl(b, 63);
+    }
+    if (threadIdx.x == 0) {
+        bsum[nb] = ra;
+        hbsum[nb] = rb;
+    }
+}
+
+__global__ void k_cmp_add(uint64_t *__restrict__ pos, uint64_t *__restrict__ hpos, const uint64_t *__restrict__ bsum,
+                          const uint64_t *__restrict__ hbsum, uint64_t n, uint64_t nb) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        pos[i] += bsum[i / kCmpBlock];
+        hpos[i] += hbsum[i / kCmpBlock];
+    }
+    if (i == n) {
+        pos[n] = bsum[nb];
+        hpos[n] = hbsum[nb];
+    }
+}
+
+// Rotation points (core/db.go:214-231 applied record by record): fstart[k] is
+// the first record of merged file k, fstart[nf] = n.  A file takes records
+// while its size + the next entry <= M; the first file is empty when the
+// first record alone exceeds M (the fresh database's active file is rotated
+// away before anything is written).  One wavefront; per file a 64-way search
+// of pos for the first record that does not fit.
+__global__ __launch_bounds__(64) void k_cmp_breaks(const uint64_t *__restrict__ pos, uint64_t n, uint64_t M,
+                                                   uint32_t *__restrict__ fstart, uint32_t cap,
+                                                   uint32_t *__restrict__ n_files) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t k = 0;
+    uint64_t b = 0;
+    if (n == 0) {  // nothing live: the fresh database's one (empty) file
+        if (lane == 0) {
+            fstart[0] = 0;
+            fstart[1] = 0;
+            *n_files = 1;
+        }
+        return;
+    }
+    if (pos[1] - pos[0] > M) {
+        if (lane == 0) fstart[0] = 0;
+        k = 1;
+    }
+    while (b < n && k < cap) {
+        if (lane == 0) fstart[k] = (uint32_t)b;
+        ++k;
+        // the smallest j in (b, n) with pos[j + 1] - pos[b] > M, else n
+        const uint64_t lim = pos[b] + M;
+        uint64_t lo = b + 1, hi = n;  // answer in [lo, hi]
+        while (lo < hi) {
+            const uint64_t span = hi - lo, step = (span + 63) / 64;
+            const uint64_t j = lo + (uint64_t)lane * step;
+            const bool over = j < hi && pos[j + 1] > lim;
+            const uint64_t m = __ballot(over);
+            if (m) {  // the first probe over the limit bounds the answer
+                const uint32_t f = (uint32_t)__builtin_ctzll(m);
+                const uint64_t jf = lo + (uint64_t)f * step;
+                hi = jf;
+                lo = f ? lo + (uint64_t)(f - 1) * step + 1 : lo;
+            } else {
+                lo = lo + 63 * step + 1 > hi ? hi : lo + 63 * step + 1;
+            }
+        }
+        b = lo;
+    }
+    if (lane == 0) {
+        fstart[k < cap ? k : cap - 1] = (uint32_t)n;
+        *n_files = k;
+    }
+}
+
+// The 16 bytes at p (any alignment): two dword-aligned loads and a byte shift.
+__device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
+    const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+    const uint8_t *a = p - sh;
+    const u32x4_a4c x = *reinterpret_cast<const u32x4_a4c *>(a);
+    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + 16);
+    return make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
+                      __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
+}
+
+// Data bytes: a wavefront per group of 64 consecutive live records; output
+// rows of 1 KiB, lane l the 16 B chunk at 16 l.  A chunk holds bytes of at
+// most two records (a live record is >= 17 bytes: the key is not empty);
+// each record's part comes from the arena window aligned to the chunk (chunk
+// byte i = record byte X + i - P), so a chunk is one or two unaligned 16 B
+// loads and a byte select.  Bytes outside the group's range are another
+// group's: those chunks are stored byte by byte.  A row inside one record
+// takes a uniform path (fields by readlane, one load, one store per lane).
+__global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ arena,
+                                                  const uint64_t *__restrict__ fbase,
+                                                  const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
+                                                  uint64_t n, uint8_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t groups = (n + 63) / 64, waves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); g < groups; g += waves) {
+        const uint64_t g0 = g * 64, mine = g0 + lane;
+        const uint32_t cnt = (uint32_t)min<uint64_t>(64, n - g0);
+        const bool have = lane < cnt;
+        uint64_t src = 0, len = 0, P = 0;
+        if (have) {
+            const gck_rec r = kd[mine];
+            src = fbase[r.file] + r.rec_off;
+            len = 16ull + r.key_len + r.value_size;
+            P = pos[mine];
+        }
+        const uint64_t O0 = __shfl(P, 0), O1 = pos[g0 + cnt];
+        auto rl64 = [](uint64_t v, uint32_t k) {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), (int)k) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)k);
+        };
+        uint32_t rr = 0;
+        for (uint64_t R = O0 & ~15ull; R < O1; R += 1024) {
+            const uint64_t X = R + 16ull * lane;
+            uint32_t r = rr;
+            for (uint32_t k = rr + 1; k < cnt; ++k) {
+                const uint64_t pk = rl64(P, k);
+                if (pk >= R + 1024) break;
+                if (X >= pk) r = k;
+            }
+            rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
+            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr) {
+                const uint64_t p0 = rl64(P, rr), l0 = rl64(len, rr);
+                if (R >= p0 && R + 1024 <= p0 + l0) {  // (uniform) the row inside one record
+                    const uint64_t s0 = rl64(src, rr);
+                    *reinterpret_cast<uint4 *>(out + X) = ld16u(arena + s0 + (X - p0));
+                    continue;
+                }
+            }
+            // (no early exit for lanes past O1: the permutes below read the
+            // record fields from other lanes, and ds_bpermute returns 0 from
+            // lanes that are not active; their chunks get an empty mask)
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            uint32_t mask = 0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint32_t sidx = min<uint32_t>(r + j, cnt - 1);
+                const uint64_t ps = __shfl(P, (int)sidx), ls = __shfl(len, (int)sidx), ss = __shfl(src, (int)sidx);
+                const uint64_t b0 = max(max(X, ps), O0), b1 = min(min(X + 16, ps + ls), O1);
+                if (r + j >= cnt || b0 >= b1) continue;
+                uint4 v;
+                if ((int64_t)(ss + X) - (int64_t)ps >= 0) {
+                    v = ld16u(arena + ss + X - ps);
+                } else {  // a window starting before the arena: bytes one by one
+                    uint32_t by[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) by[i] = X + i >= ps && X + i < ps + ls ? arena[ss + (X + i - ps)] : 0u;
+                    v = make_uint4(by[0] | by[1] << 8 | by[2] << 16 | by[3] << 24, by[4] | by[5] << 8 | by[6] << 16 | by[7] << 24,
+                                   by[8] | by[9] << 8 | by[10] << 16 | by[11] << 24,
+                                   by[12] | by[13] << 8 | by[14] << 16 | by[15] << 24);
+                }
+                const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t m = ((1u << (uint32_t)(b1 - X)) - 1u) & ~((1u << (uint32_t)(b0 - X)) - 1u);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t bm = (m >> (4 * q)) & 15u;
+                    const uint32_t km = (bm & 1u ? 0xFFu : 0u) | (bm & 2u ? 0xFF00u : 0u) | (bm & 4u ? 0xFF0000u : 0u) |
+                                        (bm & 8u ? 0xFF000000u : 0u);
+                    w[q] = (w[q] & ~km) | (vv[q] & km);
+                }
+                mask |= m;
+            }
+            if (mask == 0xFFFFu) {
+                *reinterpret_cast<uint4 *>(out + X) = make_uint4(w[0], w[1], w[2], w[3]);
+            } else if (mask) {  // the group's first or last chunk: its bytes only
+                for (uint32_t i = 0; i < 16; ++i)
+                    if ((mask >> i) & 1) out[X + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+    }
+}
+
+// Hint entries: a lane per record, byte stores (16 + KeySize bytes each).
+__global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
+                            const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
+                            const uint64_t *__restrict__ hpos, const uint32_t *__restrict__ fstart, uint32_t nf,
+                            uint64_t n, uint8_t *__restrict__ hints) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const gck_rec r = kd[i];
+    // the merged file of record i: the last k with fstart[k] <= i
+    uint32_t lo = 0, hi = nf - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (fstart[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t fo = pos[i] - pos[fstart[lo]];  // the record's offset in its merged file
+    const uint32_t h[4] = {r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)};
+    uint8_t *d = hints + hpos[i];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) d[k] = (uint8_t)(h[k >> 2] >> (8 * (k & 3)));
+    const uint8_t *key = arena + fbase[r.file] + r.rec_off + 16;
+    for (uint32_t k = 0; k < r.key_len; ++k) d[16 + k] = key[k];
+}
+
+}  // namespace gck
+
+using namespace gck;
+
+extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n_files, uint64_t *data_bytes,
+                               uint64_t *hint_bytes, double *ms) {
+    if (!ctx || !n_files || !data_bytes || !hint_bytes || max_file_size == 0) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    if (c->kd_flags & GCK_KD_KEEP_TOMBSTONES) return GCK_EINVAL;  // a merge keeps Puts only
+    GCK_HIP(hipSetDevice(c->device));
+    const uint64_t n = c->n_live;
+    if (n > 0xFFFFFFF0ull) return GCK_EINVAL;
+    const uint64_t nb = (n + kCmpBlock - 1) / kCmpBlock;
+    const uint32_t cap = (uint32_t)n + 2;  // files: at most one per record, plus an empty first one
+    int rc;
+    if ((rc = c->d_cpos.ensure((n + 1) * 8)) || (rc = c->d_chpos.ensure((n + 1) * 8)) ||
+        (rc = c->d_cbsum.ensure((nb + 1) * 16)) || (rc = c->d_cfstart.ensure((uint64_t)(cap + 1) * 4)) ||
+        (rc = c->d_cnf.ensure(16)))
+        return rc;
+    hipStream_t s = c->stream;
+    hipEvent_t e0, e1;
+    GCK_HIP(hipEventCreate(&e0));
+    GCK_HIP(hipEventCreate(&e1));
+    GCK_HIP(hipEventRecord(e0, s));
+    uint64_t *pos = c->d_cpos.as<uint64_t>(), *hpos = c->d_chpos.as<uint64_t>();
+    uint64_t *bsum = c->d_cbsum.as<uint64_t>(), *hbsum = bsum + nb + 1;
+    if (nb) k_cmp_sizes<<<(uint32_t)nb, kCmpBlock, 0, s>>>(c->d_kdout.as<gck_rec>(), n, pos, hpos, bsum, hbsum);
+    k_cmp_top<<<1, 64, 0, s>>>(bsum, hbsum, nb);
+    k_cmp_add<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(pos, hpos, bsum, hbsum, n, nb);
+    k_cmp_breaks<<<1, 64, 0, s>>>(pos, n, max_file_size, c->d_cfstart.as<uint32_t>(), cap + 1, c->d_cnf.as<uint32_t>());
+    uint64_t tot[2] = {0, 0};
+    uint32_t nf = 0;
+    GCK_HIP(hipMemcpyAsync(&tot[0], pos + n, 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(&tot[1], hpos + n, 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipMemcpyAsync(&nf, c->d_cnf.p, 4, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16))) return rc;
+    if (n) {
+        const uint64_t groups = (n + 63) / 64;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((groups + 3) / 4, (uint64_t)c->n_cu * 8);
+        k_cmp_copy<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_kdout.as<gck_rec>(), pos, n,
+                                        c->d_cdata.as<uint8_t>());
+        k_cmp_hints<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
+                                                               c->d_kdout.as<gck_rec>(), pos, hpos,
+                                                               c->d_cfstart.as<uint32_t>(), nf, n,
+                                                               c->d_chint.as<uint8_t>());
+    }
+    GCK_HIP(hipGetLastError());
+    GCK_HIP(hipEventRecord(e1, s));
+    GCK_HIP(hipEventSynchronize(e1));
+    float t = 0;
+    GCK_HIP(hipEventElapsedTime(&t, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ms) *ms = t;
+    c->cmp_files = nf;
+    c->cmp_data = tot[0];
+    c->cmp_hint = tot[1];
+    *n_files = nf;
+    *data_bytes = tot[0];
+    *hint_bytes = tot[1];
+    return GCK_OK;
+}
+
+extern "C" int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file_sizes, uint8_t *hints,
+                                     uint64_t *hint_sizes) {
+    if (!ctx) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    const uint32_t nf = c->cmp_files;
+    const uint64_t n = c->n_live;
+    std::vector<uint32_t> fs(nf + 1);
+    if (nf) GCK_HIP(hipMemcpy(fs.data(), c->d_cfstart.p, (nf + 1) * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> pos(n + 1), hpos(n + 1);
+    if (file_sizes || hint_sizes) {
+        GCK_HIP(hipMemcpy(pos.data(), c->d_cpos.p, (n + 1) * 8, hipMemcpyDeviceToHost));
+        GCK_HIP(hipMemcpy(hpos.data(), c->d_chpos.p, (n + 1) * 8, hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < nf; ++k) {
+            if (file_sizes) file_sizes[k] = pos[fs[k + 1]] - pos[fs[k]];
+            if (hint_sizes) hint_sizes[k] = hpos[fs[k + 1]] - hpos[fs[k]];
+        }
+    }
+    if (data && c->cmp_data) GCK_HIP(hipMemcpy(data, c->d_cdata.p, c->cmp_data, hipMemcpyDeviceToHost));
+    if (hints && c->cmp_hint) GCK_HIP(hipMemcpy(hints, c->d_chint.p, c->cmp_hint, hipMemcpyDeviceToHost));
+    return GCK_OK;
+}

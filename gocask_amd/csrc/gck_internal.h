@@ -103,6 +103,12 @@ struct Ctx {
     // ranks, the live records
     DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout, d_kdidx;
     uint64_t n_live = 0;
+    uint32_t kd_flags = 0;                                // flags of the last gck_ctx_keydir
+    // compaction (compact.hip): record / hint-entry offsets, block sums, file
+    // starts, file count, merged data and hint bytes
+    DBuf d_cpos, d_chpos, d_cbsum, d_cfstart, d_cnf, d_cdata, d_chint;
+    uint32_t cmp_files = 0;
+    uint64_t cmp_data = 0, cmp_hint = 0;
     // keydir merge across shards: pack partition of each live entry, the
     // merged headers / keys of the entries this rank owns
     DBuf d_kpart, d_kcrank, d_kbrank, d_kpsum, d_kptot;  // pack: partition, in-tile ranks, tile sums

@@ -335,6 +335,8 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     Ctx *c = &ctx->c;
     *n_live = 0;
     c->n_live = 0;
+    c->kd_flags = flags;
+    c->cmp_files = 0;
     c->kd_valid = false;
     const uint64_t n = c->n_recs;
     if (!n) {

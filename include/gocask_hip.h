@@ -166,6 +166,26 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
 int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 
+/* ---- merge (compaction) and hint files ------------------
+ * The reference lists "merging and hint files" as future work (README.md:60);
+ * this is the device form of that roadmap item.  After gck_ctx_keydir (without
+ * GCK_KD_KEEP_TOMBSTONES: a merge keeps live Puts only), the live records in
+ * walk order are written as new data files exactly as DB.Put would write them
+ * into a fresh database with MaxDataFileSize = max_file_size (an entry that does
+ * not fit rotates first, core/db.go:214-231; a first record larger than the
+ * limit leaves the first file empty), each record's bytes verbatim (header,
+ * key, value: CRCs and timestamps unchanged).  One hint file per data file
+ * lists its records as little-endian Bitcask hint entries
+ *   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
+ * (ValuePos = the value's offset in its merged file mod 2^32, as
+ * core/keydir.go:25 sets it on a replay of the merged files).  The outputs stay
+ * on the device: *n_files, *data_bytes (all files back to back), *hint_bytes;
+ * gck_ctx_fetch_compact copies them and the per-file sizes out (any pointer
+ * may be NULL).  *ms (optional) = device time. */
+int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n_files, uint64_t *data_bytes,
+                    uint64_t *hint_bytes, double *ms);
+int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file_sizes, uint8_t *hints, uint64_t *hint_sizes);
+
 /* ---- batched Get / keydir scrub -------------------------
  * DB.Get (core/db.go:287-316) for n keys against the device keydir of the last
  * run (call gck_ctx_keydir first, any flags): keys[key_off[i], key_off[i+1]) is

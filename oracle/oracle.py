@@ -277,3 +277,41 @@ def entry(now: int, key: bytes, val: bytes) -> bytes:
 def tombstone(now: int, key: bytes) -> bytes:
     """core/db.go:245-247 — Delete writes header{CRC(key), t, 0, len(key)} || key."""
     return struct.pack("<IIII", zlib.crc32(key), now & 0xFFFFFFFF, 0, len(key)) + key
+
+
+def compact(files, recs, reset_after, max_file_size):
+    """Merge (compaction) restated — the reference's roadmap item "merging and
+    hint files" (README.md:60), defined as: the live records of the keydir
+    (orc_keydir: last writer wins, Puts only, core/keydir.go:22-49) in walk
+    order, Put into a fresh database with MaxDataFileSize = max_file_size —
+    DB.Put (core/db.go:185-212) rotates when the active file's size + the
+    entry > MaxDataFileSize (rotateDataFile, :214-231; the fresh database's
+    first file starts empty) — each record's bytes verbatim.  Per merged file
+    its hint entries, little-endian [Timestamp][KeySize][ValueSize][ValuePos]
+    u32 + key (Bitcask's hint layout; ValuePos = the value's offset in the
+    merged file mod 2^32, as core/keydir.go:25 sets it).
+    Returns (list of data-file bytes, list of hint-file bytes)."""
+    kd = keydir(files, recs, reset_after)
+    live = sorted(kd.values(), key=lambda r: (int(r["file"]), int(r["rec_off"])))
+    data, hints = [bytearray()], [bytearray()]
+    for r in live:
+        f, o = files[int(r["file"])], int(r["rec_off"])
+        kl, vs = int(r["key_len"]), int(r["value_size"])
+        b = bytes(f[o:o + 16 + kl + vs])
+        if len(data[-1]) + len(b) > max_file_size:
+            data.append(bytearray())
+            hints.append(bytearray())
+        vpos = (len(data[-1]) + 16 + kl) & 0xFFFFFFFF
+        hints[-1] += struct.pack("<IIII", int(r["ts"]), kl, vs, vpos) + b[16:16 + kl]
+        data[-1] += b
+    return [bytes(d) for d in data], [bytes(h) for h in hints]
+
+
+def parse_hints(h):
+    """Hint entries of one hint file: [(timestamp, key, value_size, value_pos)]."""
+    out, p = [], 0
+    while p < len(h):
+        ts, kl, vs, vpos = struct.unpack_from("<IIII", h, p)
+        out.append((ts, bytes(h[p + 16:p + 16 + kl]), vs, vpos))
+        p += 16 + kl
+    return out
