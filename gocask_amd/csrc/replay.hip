@@ -198,23 +198,54 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         // it, so the next windows' loads stay in flight: windows A/B/C rotate,
         // unrolled so none is copied); a window with candidates leaves the
         // loop for the chain tests and the scan resumes after it if none holds.
+        // Lane L scans positions [64 L, 64 L + 64) of a 4 KiB window and
+        // needs bytes [64 L, 64 L + 80).  Loads as k_crc_rows': lane p + 16 b
+        // reads 1024 k + 64 p + 16 b (k < 4: each instruction one contiguous
+        // KiB, whole lines, non-temporal), the permlane transpose gives lane L
+        // its 64 bytes, lane L + 1's first block (DPP) its last 16, and lane
+        // 63 the window's next 16 bytes from a fifth load (one line, every
+        // lane the same address).
+        const uint32_t s_rel = 64 * (lane & 15) + 16 * (lane >> 4);
         auto load = [&](uint64_t b0, u32x4 (&v)[5]) {
-            // bytes [p0, p0+80): the 64 positions plus their header bytes (the
-            // arena is padded 3 windows past every file).  Buffer loads: the
-            // compiler keeps them where they are issued (ahead of their use).
+            // (the arena is padded 3 windows past every file).  Buffer loads:
+            // the compiler keeps them where they are issued (ahead of their use).
             const __amdgpu_buffer_rsrc_t rw = make_rsrc(arena + base + b0, 4096 + 80);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, lane * 64 + 16 * k, 0, 0);
+            for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rw, s_rel + 1024 * k, 0, 2);
+            v[4] = __builtin_amdgcn_raw_buffer_load_b128(rw, 4096, 0, 0);
         };
         auto cands = [&](const u32x4 (&v)[5]) -> uint64_t {  // bit t: bytes p0+t+10, p0+t+11 both zero
             uint32_t w[20];
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
+            for (int k = 0; k < 4; ++k) {
                 w[4 * k] = v[k].x;
                 w[4 * k + 1] = v[k].y;
                 w[4 * k + 2] = v[k].z;
                 w[4 * k + 3] = v[k].w;
             }
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(w[4 * k + c4], w[4 * (k + 2) + c4], false, false);
+                    w[4 * k + c4] = r[0];
+                    w[4 * (k + 2) + c4] = r[1];
+                }
+            }
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+#pragma unroll
+                for (int k = 0; k < 4; k += 2) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(w[4 * k + c4], w[4 * (k + 1) + c4], false, false);
+                    w[4 * k + c4] = r[0];
+                    w[4 * (k + 1) + c4] = r[1];
+                }
+            }
+            // bytes 64 L + 64 .. 79: lane L + 1's first block (wave_shl:1), lane 63 the fifth load
+            w[16] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].x, (int)w[0], 0x130, 0xF, 0xF, false);
+            w[17] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].y, (int)w[1], 0x130, 0xF, 0xF, false);
+            w[18] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].z, (int)w[2], 0x130, 0xF, 0xF, false);
+            w[19] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].w, (int)w[3], 0x130, 0xF, 0xF, false);
             uint32_t zf[20];
 #pragma unroll
             for (int k = 2; k < 20; ++k) zf[k] = zero_bytes(w[k]);
