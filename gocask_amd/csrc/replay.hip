@@ -41,6 +41,10 @@ constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 #define GCK_NR 1
 #endif
 constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes at once
+#ifndef GCK_PF
+#define GCK_PF 1
+#endif
+constexpr int kPrefetch = GCK_PF;  // k_crc_rows: steps between a row's loads and its processing
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -863,8 +867,11 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
 __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__restrict__ g_slice,
                                              const uint32_t *__restrict__ g_nib) {
     fill_slice_lds(lds, g_slice);
+    // lane-shift tables: nibble q (from bit 0 of G), value v, lane l at byte
+    // 4 kNibBase + 4096 q + 256 v + 4 l (every lane on its own bank); the
+    // lookup address is one v_perm_b32 (see k_crc_rows)
     for (uint32_t i = threadIdx.x; i < 8192; i += blockDim.x) {
-        const uint32_t l = (i >> 12) * 32 + (i & 31), v = (i >> 5) & 15, q = (i >> 9) & 7;
+        const uint32_t l = i & 63, v = (i >> 6) & 15, q = i >> 10;
         lds[kNibBase + i] = g_nib[(l * 8 + q) * 16 + v];
     }
     __syncthreads();
@@ -918,7 +925,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     if constexpr ((MODE & 64) == 0) fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
-    const uint32_t nbyte = (kNibBase + (lane >> 5) * 4096 + l31) * 4;  // the lane's shift table (bytes)
+    static_assert(kNibBase * 4 == 0x20000, "shift-table addresses: byte 2 of the v_perm base");
+    const uint32_t nbase = kNibBase * 4 + lane * 4;  // byte 0: the lane's bank, byte 2: the region
     const uint32_t lb0 = l31 * 4, lb1 = 65536 + l31 * 4;
     // load k of a row: lane p + 16 b reads the 16 B at 1024 k + 64 p + 16 b,
     // so each load instruction is one contiguous KiB of the row (whole cache
@@ -980,8 +988,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         if constexpr ((MODE & 8) != 0) return;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            const uint64_t r = min(row0 + i, n_rows - 1);
-            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + r * kRow, kRow);
+            // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
+            const uint32_t r = min((uint32_t)(row0 + i), (uint32_t)(n_rows - 1));
+            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
             constexpr int kAux = (MODE & 32) ? 0 : GCK_ARENA_AUX;
 #pragma unroll
             for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
@@ -1058,19 +1067,25 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             }
         }
         // Z_{64(63-lane)}(G) of every row (8 nibble lookups in the lane's
-        // table; address = (nibble << 7) | base, the base's bits 7..10 are
-        // zero), then the NR wave scans interleaved so each DPP read finds
-        // its source written a few instructions earlier (no s_nop hazards)
+        // table), then the NR wave scans interleaved so each DPP read finds
+        // its source written a few instructions earlier (no s_nop hazards).
+        // Lookup addresses: byte k of ge / go holds nibble 2k / 2k+1 of G
+        // with the nibble's index in its high half, which makes byte 1 of the
+        // address (table q, entry v): one v_perm_b32 per lookup, 3 VALU to
+        // split G (was a shift, an and and an add per lookup)
         uint32_t P[NR], pre[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             if constexpr ((MODE & 4) == 0) {
+                // (x & m) | q in one v_bitop3_b32 (truth table 0xEA; the two
+                // constants live in registers set up outside the loop)
+                const uint32_t ge = __builtin_amdgcn_bitop3_b32(G[i], 0x0F0F0F0Fu, 0x60402000u, 0xEA);
+                const uint32_t go = __builtin_amdgcn_bitop3_b32(G[i] >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
                 uint32_t t[8];
 #pragma unroll
-                for (int qn = 0; qn < 8; ++qn) {
-                    const uint32_t sh = 4 * qn;
-                    const uint32_t x = sh >= 7 ? G[i] >> (sh - 7) : G[i] << (7 - sh);
-                    t[qn] = lds_at(lds, (x & 0x780u) | (nbyte + qn * 2048));
+                for (int k = 0; k < 4; ++k) {
+                    t[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
+                    t[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
                 }
                 P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
             } else {
@@ -1141,8 +1156,14 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     uint64_t qn = grab();
     Plan pc, pn;
     load_plan(q, pc);
-    RowBuf buf[2][NR];
-    issue(q * kBlockRows, buf[0]);
+    // kPrefetch rows in flight per wavefront (row buffers rotate with period
+    // NB, which divides the 4 steps of a quad, so every buffer has fixed
+    // registers)
+    static_assert(kPrefetch == 1 || (NR == 1 && kPrefetch <= 3), "prefetch depth > 1 needs one row per step");
+    constexpr int NB = kPrefetch == 1 ? 2 : 4;
+    RowBuf buf[NB][NR];
+#pragma unroll
+    for (int d = 0; d < kPrefetch; ++d) issue(q * kBlockRows + (uint64_t)d * NR, buf[d]);
     for (;;) {
         // block q: plan pc is resident; fetch the next block's plan and claim
         // the one after it (both land during this block)
@@ -1165,15 +1186,17 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
-                // the next step's rows: this block, or the next block's first
-                const uint64_t nrow = st + 1 < kSteps ? row_b + (uint64_t)(st + 1) * NR : qn * kBlockRows;
-                issue(nrow, buf[(u + 1) & 1]);
+                // the rows kPrefetch steps ahead: this block, or the next block's first
+                const int ahead = st + kPrefetch;
+                const uint64_t nrow =
+                    ahead < kSteps ? row_b + (uint64_t)ahead * NR : qn * kBlockRows + (uint64_t)(ahead - kSteps) * NR;
+                issue(nrow, buf[(u + kPrefetch) % NB]);
                 // keep the next row's loads here, ahead of this row's compute:
                 // left alone, the scheduler sinks them past most of the chain
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u & 1],
+                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u % NB],
                         rend_buf);
             }
         }
@@ -1286,7 +1309,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                                                   const uint32_t *__restrict__ g_slice,
                                                   const uint32_t *__restrict__ xinv,
                                                   const uint32_t *__restrict__ zrow,
-                                                  const uint32_t *__restrict__ zl, const uint32_t *__restrict__ xa,
+                                                  const uint32_t *__restrict__ /*zl: unused*/, const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
@@ -1391,7 +1414,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const uint32_t xi = (GCK_FIN_XP & 2) ? d * 0x9E3779B9u : xinv[d];
         const uint32_t xv0 = (GCK_FIN_XP & 2) ? V * 0x85EBCA6Bu : xb[V & 0xFFFF];
         const uint32_t xhi = (GCK_FIN_XP & 2) ? (V >> 16) + 1 : xa[V >> 16];
-        const uint32_t zlv = (GCK_FIN_XP & 2) ? V ^ 0xC2B2AE35u : zl[min(V, (1u << 17) - 1)];
         const uint32_t cf = carry[f];
         const uint64_t fb = fbase[f];
         // ---- the next iteration's record table
@@ -1441,11 +1463,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         for (uint32_t i = 12; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
         if (nw >= 12) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
-        // x^(8V) = xa[V >> 16] * xb[V & 0xFFFF]; crc32(0^V) from zl below 2^17
+        // x^(8V) = xa[V >> 16] * xb[V & 0xFFFF]
         const uint32_t xv = V < 65536 ? xv0 : gf_mul_lds(ldsb, mw, rxb, xhi, xv0);
-        const uint32_t raw0 = chain ^ gf_mul_lds(ldsb, mw, rxb, xv, p);
-        const uint32_t z = V < (1u << 17) ? zlv : gf_mul_lds(ldsb, mw, rxb, xv, 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
-        const uint32_t calc = raw0 ^ z;
+        // crc = F(0, value) ^ crc32(0^V), crc32(0^V) = Z_V(~0) ^ ~0, and Z_V is
+        // linear: one multiply covers the prefix and the init term (no
+        // crc32(0^V) table load)
+        const uint32_t calc = chain ^ gf_mul_lds(ldsb, mw, rxb, xv, p ^ 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         {
             // The wave's records are consecutive gck_recs (40 B each): staged in
             // LDS, then stored as 16 B per lane, 1 KiB contiguous per instruction

@@ -196,7 +196,14 @@ int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file_sizes, uin
  * on the device from the resident file bytes at (File, ValuePos).  With values
  * != NULL the values of the GCK_OK keys are copied back to back, val_off[i]
  * their offsets (UINT64_MAX for the others); GCK_EINVAL if they exceed
- * values_cap (status / value_size are then filled, for a retry). */
+ * values_cap (status / value_size are then filled, for a retry).
+ * File resolution: the device reads the value from the walked file the entry's
+ * record came from (its index in walk order).  Disk.ReadFileAt opens
+ * <path>/<Name()>.csk instead (internal/fs/disk.go:147-148), which is the same
+ * file for every .csk directly in the DB directory (the layout Disk writes);
+ * for a .csk nested in a subdirectory (Disk.Walk recurses, disk.go:122-145) the
+ * reference would read the top-level file of that name, or fail: not mirrored
+ * here.  gck_db_get (the host mirror) opens by name as the reference does. */
 int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off, uint32_t n, int32_t *status,
                       uint32_t *value_size, uint32_t *crc_calc, uint8_t *values, uint64_t values_cap,
                       uint64_t *val_off, double *ms);
