@@ -97,7 +97,7 @@ struct Ctx {
     DBuf d_row_first, d_rend, d_plan, d_queue;
 
     // constant tables
-    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow, d_zl;
+    DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow;
 
     // device keydir (keydir.hip): key hashes, slot table, live flags, tile
     // ranks, the live records

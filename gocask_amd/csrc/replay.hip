@@ -1309,7 +1309,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                                                   const uint32_t *__restrict__ g_slice,
                                                   const uint32_t *__restrict__ xinv,
                                                   const uint32_t *__restrict__ zrow,
-                                                  const uint32_t *__restrict__ /*zl: unused*/, const uint32_t *__restrict__ xa,
+                                                  const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
@@ -1545,8 +1545,7 @@ __global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ are
 
 // ------------------------------------------------------------- host side ---
 static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib, std::vector<uint32_t> &xinv,
-                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow,
-                        std::vector<uint32_t> &zl) {
+                        std::vector<uint32_t> &xa, std::vector<uint32_t> &xb, std::vector<uint32_t> &zrow) {
     slice.assign(4 * 256, 0);
     for (uint32_t n = 0; n < 256; ++n) {
         uint32_t c = n;
@@ -1590,12 +1589,6 @@ static void make_tables(std::vector<uint32_t> &slice, std::vector<uint32_t> &nib
     zrow.assign(1024, 0);
     for (int k = 0; k < 4; ++k)
         for (uint32_t b = 1; b < 256; ++b) zrow[k * 256 + b] = multmodp(x_row, b << (8 * k));
-    zl.assign(1u << 17, 0);  // crc32 of L zero bytes
-    uint32_t st = 0xFFFFFFFFu;
-    for (uint32_t L = 0; L < (1u << 17); ++L) {
-        zl[L] = st ^ 0xFFFFFFFFu;
-        st = slice[st & 0xff] ^ (st >> 8);
-    }
 }
 
 static int ctx_init(Ctx *c, const gck_opts *o) {
@@ -1640,17 +1633,17 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     // the constant tables are the same for every context: built once per process
     struct Tables {
-        std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow, zl;
-        Tables() { make_tables(slice, nib, xinv, xa, xb, zrow, zl); }
+        std::vector<uint32_t> slice, nib, xinv, xa, xb, zrow;
+        Tables() { make_tables(slice, nib, xinv, xa, xb, zrow); }
     };
     static const Tables tabs;
     const std::vector<uint32_t> &slice = tabs.slice, &nib = tabs.nib, &xinv = tabs.xinv,
-                                &xa = tabs.xa, &xb = tabs.xb, &zrow = tabs.zrow, &zl = tabs.zl;
+                                &xa = tabs.xa, &xb = tabs.xb, &zrow = tabs.zrow;
     int rc;
     if ((rc = c->d_slice.ensure(slice.size() * 4)) || (rc = c->d_nib.ensure(nib.size() * 4)) ||
         (rc = c->d_xinv.ensure(xinv.size() * 4)) || (rc = c->d_xa.ensure(xa.size() * 4)) ||
         (rc = c->d_xb.ensure(xb.size() * 4)) || (rc = c->d_zrow.ensure(zrow.size() * 4)) ||
-        (rc = c->d_zl.ensure(zl.size() * 4)) || (rc = c->d_counters.ensure(128)))
+        (rc = c->d_counters.ensure(128)))
         return rc;
     {
         void *hp = nullptr, *dp = nullptr;
@@ -1660,7 +1653,6 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
         c->d_mbox = static_cast<uint32_t *>(dp);
     }
     GCK_HIP(hipMemcpy(c->d_zrow.p, zrow.data(), zrow.size() * 4, hipMemcpyHostToDevice));
-    GCK_HIP(hipMemcpy(c->d_zl.p, zl.data(), zl.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_slice.p, slice.data(), slice.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_nib.p, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     GCK_HIP(hipMemcpy(c->d_xinv.p, xinv.data(), xinv.size() * 4, hipMemcpyHostToDevice));
@@ -1675,7 +1667,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
-                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow, &c->d_zl,
+                   &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
@@ -1877,7 +1869,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
                                     c->d_zrow.as<uint32_t>(),
-                                    c->d_zl.as<uint32_t>(), c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
+                                    c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
 }
 
