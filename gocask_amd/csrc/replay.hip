@@ -1296,8 +1296,11 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, con
     return c;
 }
 
+#ifndef GCK_FIN_PIPE
+#define GCK_FIN_PIPE 0
+#endif
 #ifndef GCK_FIN_WPE
-#define GCK_FIN_WPE 4
+#define GCK_FIN_WPE (GCK_FIN_PIPE ? 3 : 4)
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
@@ -1355,70 +1358,96 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         o.f0 = base ? rec_file[r0] : 0xFFFFFFFFu;
         o.ep0 = ep[r0];
     };
-    uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
-    Rec cur;
-    if (base < re) load_rec(base, cur);
-    for (; base < re; base += G) {
-        const uint64_t r_ = base + lane;
-        const bool valid = r_ < re;
-        const uint64_t rs = cur.rs;
-        const uint2 kv = cur.kv;
-        const uint32_t f = cur.f, V = kv.y;
-        const uint64_t vs = rs + 16 + kv.x, ve = vs + V;
+    // Per-iteration geometry of a wave's 64 records (recomputed where needed:
+    // a few VALU, fewer registers than carrying it)
+    struct Geo {
+        bool valid, prev_same, have;
+        uint32_t f, V, e_prev, pre_prev, d;
+        uint64_t rs, vs, ve, bsp, bse, fr, lr, w0;
+        uint2 kv;
+    };
+    auto geo = [&](const Rec &c, uint64_t b) {
+        Geo g;
+        g.valid = b + lane < re;
+        g.rs = c.rs;
+        g.kv = c.kv;
+        g.f = c.f;
+        g.V = c.kv.y;
+        g.vs = g.rs + 16 + g.kv.x;
+        g.ve = g.vs + g.V;
         // the previous record (r - 1): lane - 1's, or the wave's extra one
-        const uint32_t f_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.f0, (int)f, 0x138, 0xF, 0xF, false);
-        const uint32_t e_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.ep0.x, (int)cur.ep.x, 0x138, 0xF, 0xF, false);
-        const uint32_t pre_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)cur.ep0.y, (int)cur.ep.y, 0x138, 0xF, 0xF, false);
+        const uint32_t f_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)c.f0, (int)c.f, 0x138, 0xF, 0xF, false);
+        g.e_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)c.ep0.x, (int)c.ep.x, 0x138, 0xF, 0xF, false);
+        g.pre_prev = (uint32_t)__builtin_amdgcn_update_dpp((int)c.ep0.y, (int)c.ep.y, 0x138, 0xF, 0xF, false);
         // records of a file are contiguous in walk order; lanes past the range
         // repeat the last record and have no predecessor
-        const bool prev_same = valid && f_prev == f;
+        g.prev_same = g.valid && f_prev == g.f;
         // ft of this record comes from lane + 1 if that lane holds record r + 1 of the same file
-        const uint64_t nb_same = __ballot(valid && prev_same);
-        const bool have = lane < 63 && ((nb_same >> (lane + 1)) & 1);
-        const uint64_t bsp = prev_same ? (rs - 1) & ~15ull : rs, bse = (ve - 1) & ~15ull;
-        const uint64_t fr = rs / kRow, lr = (ve - 1) / kRow;
-        const uint32_t d = (uint32_t)((lr + 1) * kRow - ve);
-        const uint64_t w0 = rs & ~3ull;
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
-        // ---- every dependent load of this iteration
+        const uint64_t nb_same = __ballot(g.valid && g.prev_same);
+        g.have = lane < 63 && ((nb_same >> (lane + 1)) & 1);
+        g.bsp = g.prev_same ? (g.rs - 1) & ~15ull : g.rs;
+        g.bse = (g.ve - 1) & ~15ull;
+        g.fr = g.rs / kRow;
+        g.lr = (g.ve - 1) / kRow;
+        g.d = (uint32_t)((g.lr + 1) * kRow - g.ve);
+        g.w0 = g.rs & ~3ull;
+        return g;
+    };
 #ifndef GCK_FIN_XP
 #define GCK_FIN_XP 0  // ablation (timing only, wrong results): 1 no arena loads, 2 no table loads, 4 no stores, 8 no row sums, 32 no header + key loads
 #endif
-        const uint4 vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)rs, (uint32_t)bsp, V, f)
-                                          : *reinterpret_cast<const uint4 *>(arena + bsp);  // block holding byte rs - 1
+    // every load that depends on the record table
+    struct Dep {
+        uint4 vp, vend;
+        uint32_t pw[12], rr[12];
+        uint32_t xi, xv0, xhi, cf;
+        uint64_t fb;
+    };
+    auto issue = [&](const Geo &g, Dep &o) {
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + g.w0);
+        o.vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)g.rs, (uint32_t)g.bsp, g.V, g.f)
+                                : *reinterpret_cast<const uint4 *>(arena + g.bsp);  // block holding byte rs - 1
         // header + keys up to 24 B as three 16 B loads (dword aligned; the
         // arena is padded): every load instruction of a wave touches 64
         // records' lines, so the count of instructions, not bytes, is the cost
-        uint32_t pw[12];
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = (GCK_FIN_XP & 33) ? u32x4_a4{(uint32_t)rs * (i + 3), 1u, 2u, 3u}
+            const u32x4_a4 v = (GCK_FIN_XP & 33) ? u32x4_a4{(uint32_t)g.rs * (i + 3), 1u, 2u, 3u}
                                                 : reinterpret_cast<const u32x4_a4 *>(wp)[i];
-            pw[4 * i] = v.x;
-            pw[4 * i + 1] = v.y;
-            pw[4 * i + 2] = v.z;
-            pw[4 * i + 3] = v.w;
+            o.pw[4 * i] = v.x;
+            o.pw[4 * i + 1] = v.y;
+            o.pw[4 * i + 2] = v.z;
+            o.pw[4 * i + 3] = v.w;
         }
-        uint4 vend = make_uint4(0, 0, 0, 0);
-        if (!have) vend = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)bse, 1, 2, 3) : *reinterpret_cast<const uint4 *>(arena + bse);
-        uint32_t rr[12];  // row sums rend[fr .. fr + 11] the record crosses (three 16 B loads; rend is padded)
+        o.vend = make_uint4(0, 0, 0, 0);
+        if (!g.have)
+            o.vend = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)g.bse, 1, 2, 3) : *reinterpret_cast<const uint4 *>(arena + g.bse);
+        // row sums rend[fr .. fr + 11] the record crosses (three 16 B loads; rend is padded)
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = (GCK_FIN_XP & 8) ? u32x4_a4{(uint32_t)fr * 7 + i, 1u, 2u, 3u}
-                                                : reinterpret_cast<const u32x4_a4 *>(rend + fr)[i];
-            rr[4 * i] = v.x;
-            rr[4 * i + 1] = v.y;
-            rr[4 * i + 2] = v.z;
-            rr[4 * i + 3] = v.w;
+            const u32x4_a4 v = (GCK_FIN_XP & 8) ? u32x4_a4{(uint32_t)g.fr * 7 + i, 1u, 2u, 3u}
+                                                : reinterpret_cast<const u32x4_a4 *>(rend + g.fr)[i];
+            o.rr[4 * i] = v.x;
+            o.rr[4 * i + 1] = v.y;
+            o.rr[4 * i + 2] = v.z;
+            o.rr[4 * i + 3] = v.w;
         }
-        const uint32_t xi = (GCK_FIN_XP & 2) ? d * 0x9E3779B9u : xinv[d];
-        const uint32_t xv0 = (GCK_FIN_XP & 2) ? V * 0x85EBCA6Bu : xb[V & 0xFFFF];
-        const uint32_t xhi = (GCK_FIN_XP & 2) ? (V >> 16) + 1 : xa[V >> 16];
-        const uint32_t cf = carry[f];
-        const uint64_t fb = fbase[f];
-        // ---- the next iteration's record table
-        Rec nxt;
-        if (base + G < re) load_rec(base + G, nxt);
+        o.xi = (GCK_FIN_XP & 2) ? g.d * 0x9E3779B9u : xinv[g.d];
+        o.xv0 = (GCK_FIN_XP & 2) ? g.V * 0x85EBCA6Bu : xb[g.V & 0xFFFF];
+        o.xhi = (GCK_FIN_XP & 2) ? (g.V >> 16) + 1 : xa[g.V >> 16];
+        o.cf = carry[g.f];
+        o.fb = fbase[g.f];
+    };
+    auto compute = [&](const Rec &c, const Geo &g, const Dep &o, uint64_t base) {
+        const bool valid = g.valid, prev_same = g.prev_same, have = g.have;
+        const uint64_t rs = g.rs, vs = g.vs, ve = g.ve, bsp = g.bsp, bse = g.bse, fr = g.fr, lr = g.lr, w0 = g.w0;
+        const uint2 kv = g.kv;
+        const uint32_t f = g.f, V = g.V, e_prev = g.e_prev, pre_prev = g.pre_prev;
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
+        const uint4 vp = o.vp, vend = o.vend;
+        const uint32_t *pw = o.pw, *rr = o.rr;
+        const uint32_t xi = o.xi, xv0 = o.xv0, xhi = o.xhi, cf = o.cf;
+        const uint64_t fb = o.fb;
         // ---- compute
         const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
         // A(rs) = pre_prev ^ Z_{E-rs}(ft_prev) (0 when rs starts a row).  Only
@@ -1428,10 +1457,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         const bool mid = prev_same && (rs & (kRow - 1)) != 0;
         const uint32_t a_rs = mid ? pre_prev : 0u, s0 = mid ? ft_prev : 0u;
         const uint32_t ft_next = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ft_prev, 0x130, 0xF, 0xF, false);  // wave_shl:1
-        const uint32_t ft = have ? ft_next : crc_block(T, cur.ep.x, vend, (uint32_t)(ve - bse));
+        const uint32_t ft = have ? ft_next : crc_block(T, c.ep.x, vend, (uint32_t)(ve - bse));
         // acc = the record's bytes of its rows, referenced to the end row's
         // end, without the last block's ft (added back unshifted below)
-        uint32_t acc = cur.ep.y;
+        uint32_t acc = c.ep.y;
         if (fr == lr) {
             acc ^= a_rs;
         } else {
@@ -1497,8 +1526,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
             __builtin_amdgcn_wave_barrier();
             n_rej += valid && calc != hcrc;
         }
+    };
+    // Software pipeline (GCK_FIN_PIPE): the record table two iterations ahead,
+    // its dependent loads one iteration ahead, so an iteration's compute
+    // overlaps the next one's memory round trip (≈40 more VGPRs: 3 waves/SIMD).
+    // Without it: the table one iteration ahead, the dependent loads issued
+    // together and waited for, then the compute.
+    uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    Rec cur, nxt;
+    if (base < re) load_rec(base, cur);
+#if GCK_FIN_PIPE
+    Dep dc;
+    if (base < re) issue(geo(cur, base), dc);
+    if (base + G < re) load_rec(base + G, nxt);
+    for (; base < re; base += G) {
+        Dep dn;
+        Rec nn;
+        if (base + G < re) issue(geo(nxt, base + G), dn);
+        if (base + 2 * G < re) load_rec(base + 2 * G, nn);
+        compute(cur, geo(cur, base), dc, base);
+        cur = nxt;
+        nxt = nn;
+        dc = dn;
+    }
+#else
+    for (; base < re; base += G) {
+        const Geo g = geo(cur, base);
+        Dep dc;
+        issue(g, dc);
+        if (base + G < re) load_rec(base + G, nxt);
+        compute(cur, g, dc, base);
         cur = nxt;
     }
+#endif
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
     __shared__ uint32_t blk_rej;
