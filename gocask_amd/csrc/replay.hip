@@ -44,6 +44,9 @@ constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes a
 #ifndef GCK_PF
 #define GCK_PF 1
 #endif
+#ifndef GCK_SPLAN
+#define GCK_SPLAN 0  // k_crc_rows builds each block's plan from the record table (no k_row_plan)
+#endif
 constexpr int kPrefetch = GCK_PF;  // k_crc_rows: steps between a row's loads and its processing
 constexpr uint32_t kNibBase = 32768;
 
@@ -919,7 +922,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
                                                    uint32_t *__restrict__ out_rend,
                                                    uint32_t *__restrict__ rend_scratch,
-                                                   uint32_t *__restrict__ queue) {
+                                                   uint32_t *__restrict__ queue,
+                                                   const uint64_t *__restrict__ rec_off,
+                                                   const uint2 *__restrict__ rec_kv, uint64_t row0) {
     static_assert(kBlockRows % (4 * NR) == 0, "a block is whole quads of steps");
     constexpr int kSteps = kBlockRows / NR;  // steps per block
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
@@ -971,16 +976,70 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         return last;
     };
     struct Plan {
+#if !GCK_SPLAN
         uint4 a, b;  // the lane's 64 row nibbles
+#endif
         uint32_t ra; // row_first of row lane
+        uint32_t re; // row_first of the block's end (GCK_SPLAN)
     };
     auto load_plan = [&](uint64_t q, Plan &p) {
         const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
+#if !GCK_SPLAN
         const uint4 *src = plan + qc * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
         p.a = src[0];
         p.b = src[1];
+#else
+        p.re = row_first[min(qc * kBlockRows + kBlockRows, n_rows)];
+#endif
         p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
     };
+#if GCK_SPLAN
+    // The block's plan nibbles from its record ends (records [ra0, re) end in
+    // its rows, in offset order), instead of k_row_plan's dense 32 B per row:
+    // a lane per record computes (row, slab, block) of its last byte, then a
+    // uniform loop hands each end to the slab's lane (nibble dword chosen by
+    // a uniform index).
+    // GCK_SPLAN 2: the first 64 record ends of a block are loaded one block
+    // ahead (Batch); later ones (blocks with more than 64 ends) on the spot
+    struct Batch {
+        uint64_t off;
+        uint2 kv;
+    };
+    auto load_batch = [&](const Plan &p, Batch &b) {
+        const uint32_t r = min((uint32_t)__builtin_amdgcn_readlane((int)p.ra, 0) + lane, (uint32_t)(n_total - 1));
+        b.off = rec_off[r];
+        b.kv = rec_kv[r];
+    };
+    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch *first, uint32_t (&nb)[8]) {
+#pragma unroll
+        for (int d = 0; d < 8; ++d) nb[d] = 0;
+        const uint64_t base = (row0 + row_b) * kRow;
+        for (uint32_t b0 = ra0_; b0 < re_; b0 += 64) {
+            const uint32_t r = b0 + lane;
+            uint32_t code = 0;
+            if (r < re_) {
+                const uint64_t end = first && b0 == ra0_ ? first->off + 16 + (uint64_t)first->kv.x + first->kv.y
+                                                         : value_end(rec_off, rec_kv, r);
+                const uint64_t rel = end - 1 - base;  // < 64 rows
+                code = ((uint32_t)(rel >> 12) << 8) | ((uint32_t)(rel >> 6) & 63u) << 2 | ((uint32_t)(rel >> 4) & 3u);
+            }
+            // ends in offset order, so each nibble dword's ends are a run:
+            // per dword d a uniform loop over its ends (static register index)
+            const uint32_t dd = r < re_ ? code >> 11 : 8u;
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                uint64_t act = __ballot(dd == (uint32_t)d);
+                while (act) {
+                    const int i = __builtin_ctzll(act);
+                    act &= act - 1;
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)code, i);
+                    const uint32_t k = (c >> 2) & 63u, bit = (1u << (c & 3u)) << (4 * ((c >> 8) & 7u));
+                    nb[d] |= lane == k ? bit : 0u;
+                }
+            }
+        }
+    };
+#endif
     struct RowBuf {
         u32x4 x[4];
     };
@@ -1156,6 +1215,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     uint64_t qn = grab();
     Plan pc, pn;
     load_plan(q, pc);
+#if GCK_SPLAN == 2
+    Batch bc, bn;
+    load_plan(qn, pn);
+    load_batch(pc, bc);
+#endif
     // kPrefetch rows in flight per wavefront (row buffers rotate with period
     // NB, which divides the 4 steps of a quad, so every buffer has fixed
     // registers)
@@ -1167,13 +1231,32 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     for (;;) {
         // block q: plan pc is resident; fetch the next block's plan and claim
         // the one after it (both land during this block)
+#if GCK_SPLAN == 2
+        // pn (block qn) landed during the previous block: its record ends now,
+        // the plan of the block after it next
+        const uint64_t qnn = grab();
+        Plan pnn;
+        load_batch(pn, bn);
+        load_plan(qnn, pnn);
+#else
         load_plan(qn, pn);
         const uint64_t qnn = grab();
+#endif
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
+#if !GCK_SPLAN
         const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
+#else
+        uint32_t nibs[8];
+#if GCK_SPLAN == 2
+        build_nibs(row_b, ra0, pc.re, &bc, nibs);
+#else
+        (void)load_batch;
+        build_nibs(row_b, ra0, pc.re, nullptr, nibs);
+#endif
+#endif
         // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
         // lane; the two row buffers alternate, so each has fixed registers
         for (int qd = 0; qd < kSteps / 4; ++qd) {
@@ -1207,6 +1290,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         q = qn;
         qn = qnn;
         pc = pn;
+#if GCK_SPLAN == 2
+        pn = pnn;
+        bc = bn;
+#endif
     }
 }
 
@@ -1896,7 +1983,7 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
                                              c->d_fnrec.as<uint64_t>(), c->nfiles, c->n_rows, rng,
                                              c->d_row_first.as<uint32_t>());
-    if (r1 > r0)
+    if (r1 > r0 && !GCK_SPLAN)
         k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
             c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
             c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16);
@@ -1914,7 +2001,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
         c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16,
         c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
-        c->d_rend.as<uint32_t>() + c->n_rows, queue);
+        c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0);
     return GCK_OK;
 }
 
@@ -2717,7 +2804,7 @@ int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter)
         k_crc_rows<M, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(                                                  \
             c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint4>(), c->d_row_first.as<uint32_t>(), c->n_recs,      \
             c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),      \
-            c->d_rend.as<uint32_t>() + c->n_rows, queue);                                                           \
+            c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), 0); \
         break;
         switch (mode) {
             GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(6) GCK_VARIANT(8) GCK_VARIANT(12)
