@@ -44,8 +44,13 @@ constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes a
 #ifndef GCK_PF
 #define GCK_PF 1
 #endif
+// Row plan source for k_crc_rows: 0 = k_row_plan's dense 32 B per row; 1 = each
+// block's nibbles built in k_crc_rows from the record table; 2 = the same with
+// the block's first 64 record ends loaded one block ahead (shipped: C3 step
+// 7.11-7.13 -> 6.76-6.94 ms on one box, records phase 0.20 -> 0.11 ms, and
+// k_crc_rows no longer reads 268 MB of plan)
 #ifndef GCK_SPLAN
-#define GCK_SPLAN 0  // k_crc_rows builds each block's plan from the record table (no k_row_plan)
+#define GCK_SPLAN 2
 #endif
 constexpr int kPrefetch = GCK_PF;  // k_crc_rows: steps between a row's loads and its processing
 constexpr uint32_t kNibBase = 32768;
@@ -1882,7 +1887,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
-        (rc = c->d_plan.ensure((c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
+        (rc = c->d_plan.ensure(GCK_SPLAN ? 16 : (c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
