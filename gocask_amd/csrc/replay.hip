@@ -52,6 +52,9 @@ constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes a
 #ifndef GCK_SPLAN
 #define GCK_SPLAN 2
 #endif
+#ifndef GCK_EPACC
+#define GCK_EPACC 0  // k_crc_rows: (c, pre) gathered per block and stored 64 slots at a time
+#endif
 constexpr int kPrefetch = GCK_PF;  // k_crc_rows: steps between a row's loads and its processing
 constexpr uint32_t kNibBase = 32768;
 
@@ -1060,6 +1063,15 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
         }
     };
+    // GCK_EPACC: (c, pre) of consecutive record slots gathered in two
+    // registers (lane l = slot acc_base + l) and stored 64 at a time, at the
+    // block end or when full, instead of one 64-lane store per row
+    uint32_t acc_c = 0, acc_p = 0, acc_n = 0, acc_base = 0;
+    auto acc_flush = [&]() {
+        store_ep(lane < acc_n ? (acc_base + lane - ra0) * 8u : kDrop, acc_c, acc_p);
+        acc_base += acc_n;
+        acc_n = 0;
+    };
     // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
     // nib holds their plan nibbles from bit 0 up
     auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t ra_reg, const RowBuf (&bs)[NR],
@@ -1190,6 +1202,36 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             };
             if constexpr ((MODE & 16) != 0) {
                 asm volatile("" ::"v"(m), "v"(pre[i]), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
+            } else if (GCK_EPACC) {
+                // the row's ends in slot order (lane, then block), each into
+                // lane acc_n of the accumulator: a uniform loop over the
+                // lanes with ends (about 1.2 per row on C3)
+                (void)ra;
+                // each lane's first end's capture, selected on the vector unit
+                const uint32_t cap0 = cap((uint32_t)__builtin_ctz(m | 16u));
+                auto push = [&](uint32_t cv, uint32_t pv) {
+                    if (acc_n == 64) acc_flush();
+                    acc_c = lane == acc_n ? cv : acc_c;
+                    acc_p = lane == acc_n ? pv : acc_p;
+                    ++acc_n;
+                };
+                uint64_t C = __ballot(m != 0);
+                while (C) {
+                    const int L = __builtin_ctzll(C);
+                    C &= C - 1;
+                    const uint32_t mL = (uint32_t)__builtin_amdgcn_readlane((int)m, L);
+                    const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)pre[i], L);
+                    push((uint32_t)__builtin_amdgcn_readlane((int)cap0, L), pv);
+                    if (mL & (mL - 1)) {  // rare: a slab with 2..4 ends (records under 64 B)
+                        const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)c1[i], L);
+                        const uint32_t v2 = (uint32_t)__builtin_amdgcn_readlane((int)c2[i], L);
+                        const uint32_t v3 = (uint32_t)__builtin_amdgcn_readlane((int)c3[i], L);
+                        for (uint32_t mm = mL & (mL - 1); mm; mm &= mm - 1) {
+                            const uint32_t b = (uint32_t)__builtin_ctz(mm);
+                            push(b == 1 ? v1 : b == 2 ? v2 : v3, pv);
+                        }
+                    }
+                }
             } else if (__ballot(m & (m - 1)) == 0) {
                 // common case: at most one record end per slab, its slot is
                 // ra + (cut lanes before)
@@ -1251,6 +1293,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
+        acc_base = ra0;
+        acc_n = 0;
 #if !GCK_SPLAN
         const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
 #else
@@ -1288,6 +1332,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                         rend_buf);
             }
         }
+        if (GCK_EPACC) acc_flush();
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
         *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
