@@ -1032,16 +1032,19 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 code = ((uint32_t)(rel >> 12) << 8) | ((uint32_t)(rel >> 6) & 63u) << 2 | ((uint32_t)(rel >> 4) & 3u);
             }
             // ends in offset order, so each nibble dword's ends are a run:
-            // per dword d a uniform loop over its ends (static register index)
+            // per dword d a uniform loop over its ends (static register index).
+            // Target lane and bit decoded by every lane at once; the loop only
+            // reads them (two readlanes) and ORs the bit into lane k.
             const uint32_t dd = r < re_ ? code >> 11 : 8u;
+            const uint32_t tk = (code >> 2) & 63u, tbit = (1u << (code & 3u)) << (4 * ((code >> 8) & 7u));
 #pragma unroll
             for (int d = 0; d < 8; ++d) {
                 uint64_t act = __ballot(dd == (uint32_t)d);
                 while (act) {
                     const int i = __builtin_ctzll(act);
-                    act &= act - 1;
-                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)code, i);
-                    const uint32_t k = (c >> 2) & 63u, bit = (1u << (c & 3u)) << (4 * ((c >> 8) & 7u));
+                    act ^= 1ull << i;
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)tk, i);
+                    const uint32_t bit = (uint32_t)__builtin_amdgcn_readlane((int)tbit, i);
                     nb[d] |= lane == k ? bit : 0u;
                 }
             }
