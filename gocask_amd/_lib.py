@@ -53,7 +53,7 @@ assert KD_ENTRY_DTYPE.itemsize == 64
 EXPORTED = [
     "gck_replay", "gck_replay_into", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
     "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_ctx_compact", "gck_ctx_fetch_compact", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
-    "gck_ctx_read_file", "gck_diag_stream_read", "gck_diag_stream_pattern", "gck_diag_crc_variant", "gck_diag_walk_variant", "gck_diag_spec_entries", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
+    "gck_ctx_read_file", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
     "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count", "gck_host_register", "gck_host_unregister",
     "gck_version", "gck_last_error",
@@ -131,6 +131,8 @@ class GckConfig(ctypes.Structure):
 
 
 _lib = None
+_diag = None
+DIAG_PATH = os.path.join(os.path.dirname(LIB_PATH), "libgocask_diag.so")
 
 
 def _torch_runtime_first():
@@ -193,12 +195,6 @@ def load():
         "gck_ctx_device_recs": (ctypes.c_int, [vp, P(vp), P(ctypes.c_uint64)]),
         "gck_ctx_stream": (vp, [vp]),
         "gck_ctx_read_file": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint64, vp, ctypes.c_uint64]),
-        "gck_diag_stream_read": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]),
-        "gck_diag_stream_pattern": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double),
-                                                   P(ctypes.c_double)]),
-        "gck_diag_crc_variant": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double)]),
-        "gck_diag_walk_variant": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double)]),
-        "gck_diag_spec_entries": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
         "gck_encode_corpus": (ctypes.c_int, [vp, P(GckCorpusCfg), P(ctypes.c_uint32), P(ctypes.c_uint64), vp,
                                              ctypes.c_uint32]),
         "gck_encode_files": (ctypes.c_int, [vp, P(GckCorpusCfg), vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp]),
@@ -228,13 +224,31 @@ def load():
         "gck_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
-        if name.startswith("gck_diag_") and not hasattr(L, name):
-            continue  # measurement helpers only (an older build under GCK_LIB_PATH)
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
     _lib = L
     return L
+
+
+def load_diag():
+    """The measurement helpers (gocask_amd/csrc/gck_diag.h), a separate
+    library linked against libgocask_hip.so; not part of the product ABI."""
+    global _diag
+    if _diag is not None:
+        return _diag
+    load()
+    if not os.path.exists(DIAG_PATH):
+        raise ImportError(f"{DIAG_PATH} missing: run __graft_entry__.build()")
+    D = ctypes.CDLL(DIAG_PATH)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    D.gck_diag_stream_read.restype = ctypes.c_int
+    D.gck_diag_stream_read.argtypes = [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
+    D.gck_diag_stream_pattern.restype = ctypes.c_int
+    D.gck_diag_stream_pattern.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
+    _diag = D
+    return D
 
 
 class GckError(RuntimeError):

@@ -485,10 +485,11 @@ class ReplayContext:
                     n_files=s.n_files)
 
     def stream_read_ceiling(self, iters=10):
-        """Plain streaming read of the resident arena: (ms per pass, GB/s)."""
+        """Plain streaming read of the resident arena (measurement helper,
+        libgocask_diag.so): (ms per pass, GB/s)."""
         ms = ctypes.c_double()
         gbs = ctypes.c_double()
-        check(self._L.gck_diag_stream_read(self._h, iters, ctypes.byref(ms), ctypes.byref(gbs)))
+        check(_lib.load_diag().gck_diag_stream_read(self._h, iters, ctypes.byref(ms), ctypes.byref(gbs)))
         return ms.value, gbs.value
 
     def read_file(self, file, off=0, length=None, out=None):

@@ -13,7 +13,9 @@
 // without reading values.
 //
 // Kernels: sizes and two-level exclusive scans of record and hint-entry
-// sizes; the rotation points (one wavefront, a 64-way search per file); the
+// sizes; the rotation points (few files: one wavefront, a 64-way search per
+// file; many: each record's successor file start, then the chain from record
+// 0 by pointer doubling); the
 // data bytes (a wavefront per group of 64 records, 16 B output chunks, each
 // from one or two chunk-aligned windows of the resident arena); the hint
 // entries (a lane per record).
@@ -154,12 +156,95 @@ __global__ __launch_bounds__(64) void k_cmp_breaks(const uint64_t *__restrict__ 
     }
 }
 
+// Rotation points for many merged files (a small max_file_size): the chain of
+// file starts 0 -> next[0] -> next[next[0]] ... with next[b] = the smallest j
+// in (b, n] with j == n or pos[j + 1] - pos[b] > M (a lane per record, binary
+// search), marked by pointer doubling: round k marks jmp[i] for every marked
+// i, then jmp[i] = jmp[jmp[i]] (= next^(2^(k+1))(i)), so after R rounds every
+// start within 2^R steps of record 0 is marked.  A mark that lands during its
+// own round only marks true starts earlier (images of starts are starts).
+__global__ void k_cmp_next(const uint64_t *__restrict__ pos, uint64_t n, uint64_t M, uint32_t *__restrict__ jmp,
+                           uint32_t *__restrict__ on) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > n) return;
+    if (i == n) {
+        jmp[n] = (uint32_t)n;
+        return;
+    }
+    const uint64_t lim = pos[i] + M;
+    uint64_t lo = i + 1, hi = n;  // answer in [lo, hi]
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (pos[mid + 1] > lim) hi = mid; else lo = mid + 1;
+    }
+    jmp[i] = (uint32_t)lo;
+    on[i] = i == 0 ? 1u : 0u;
+}
+__global__ void k_cmp_mark(const uint32_t *__restrict__ jmp, uint32_t *on, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && on[i]) {
+        const uint32_t j = jmp[i];
+        if (j < n) on[j] = 1u;
+    }
+}
+__global__ void k_cmp_jump(const uint32_t *__restrict__ jmp, uint32_t *__restrict__ jmp2, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) jmp2[i] = jmp[jmp[i]];
+}
+// fstart from the marks: per block of kCmpBlock records the marked count
+// (wave ballots), one wavefront scans the block counts, then each block
+// writes its starts in order after `lead` (1 when the first file is empty).
+__global__ __launch_bounds__(kCmpBlock) void k_cmp_fcount(const uint32_t *__restrict__ on, uint64_t n,
+                                                          uint64_t *__restrict__ bcnt) {
+    __shared__ uint32_t wc[kCmpBlock / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * kCmpBlock + threadIdx.x;
+    const uint64_t m = __ballot(i < n && on[i]);
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t k = 0; k < kCmpBlock / 64; ++k) t += wc[k];
+        bcnt[blockIdx.x] = t;
+    }
+}
+__global__ __launch_bounds__(64) void k_cmp_ftop(uint64_t *__restrict__ bcnt, uint64_t nb, uint32_t lead,
+                                                 uint32_t *__restrict__ fstart, uint64_t n, uint32_t *__restrict__ n_files) {
+    uint64_t run = lead;
+    for (uint64_t i0 = 0; i0 < nb; i0 += 64) {
+        const uint64_t i = i0 + threadIdx.x;
+        const uint64_t v = i < nb ? bcnt[i] : 0;
+        const uint64_t a = wave_incl_sum64(v);
+        if (i < nb) bcnt[i] = run + a - v;
+        run += __shfl(a, 63);
+    }
+    if (threadIdx.x == 0) {
+        if (lead) fstart[0] = 0;  // the empty first file
+        fstart[run] = (uint32_t)n;
+        *n_files = (uint32_t)run;
+    }
+}
+__global__ __launch_bounds__(kCmpBlock) void k_cmp_fscatter(const uint32_t *__restrict__ on, uint64_t n,
+                                                            const uint64_t *__restrict__ bcnt,
+                                                            uint32_t *__restrict__ fstart) {
+    __shared__ uint32_t wc[kCmpBlock / 64];
+    const uint64_t i = (uint64_t)blockIdx.x * kCmpBlock + threadIdx.x;
+    const bool mk = i < n && on[i];
+    const uint64_t m = __ballot(mk);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) wc[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t k = 0; k < w; ++k) before += wc[k];
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (mk) fstart[bcnt[blockIdx.x] + before + r] = (uint32_t)i;
+}
+
 // The 16 bytes at p (any alignment): two dword-aligned loads and a byte shift.
 __device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint8_t *a = p - sh;
     const u32x4_a4c x = *reinterpret_cast<const u32x4_a4c *>(a);
-    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + 16);
+    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + (sh ? 16 : 12));  // (as encode.hip load16u)
     return make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
                       __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
 }
@@ -282,10 +367,26 @@ __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *_
 
 using namespace gck;
 
+namespace {
+// hipEvents destroyed on every return path
+struct EvPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    ~EvPair() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+constexpr uint64_t kSerialBreakFiles = 256;  // up to this many merged files: the one-wavefront search
+}  // namespace
+
 extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n_files, uint64_t *data_bytes,
                                uint64_t *hint_bytes, double *ms) {
     if (!ctx || !n_files || !data_bytes || !hint_bytes || max_file_size == 0) return GCK_EINVAL;
     Ctx *c = &ctx->c;
+    // the keydir must describe the last run (gck_ctx_run invalidates it), and
+    // that run must have opened: the reference refuses a database whose replay
+    // hit a startup error (core/db.go:134-138), so there is nothing to merge
+    if (!c->kd_valid || c->status != GCK_OK) return GCK_EINVAL;
     if (c->kd_flags & GCK_KD_KEEP_TOMBSTONES) return GCK_EINVAL;  // a merge keeps Puts only
     GCK_HIP(hipSetDevice(c->device));
     const uint64_t n = c->n_live;
@@ -298,20 +399,43 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
         (rc = c->d_cnf.ensure(16)))
         return rc;
     hipStream_t s = c->stream;
-    hipEvent_t e0, e1;
-    GCK_HIP(hipEventCreate(&e0));
-    GCK_HIP(hipEventCreate(&e1));
-    GCK_HIP(hipEventRecord(e0, s));
+    EvPair ev;
+    GCK_HIP(hipEventCreate(&ev.a));
+    GCK_HIP(hipEventCreate(&ev.b));
+    GCK_HIP(hipEventRecord(ev.a, s));
     uint64_t *pos = c->d_cpos.as<uint64_t>(), *hpos = c->d_chpos.as<uint64_t>();
     uint64_t *bsum = c->d_cbsum.as<uint64_t>(), *hbsum = bsum + nb + 1;
     if (nb) k_cmp_sizes<<<(uint32_t)nb, kCmpBlock, 0, s>>>(c->d_kdout.as<gck_rec>(), n, pos, hpos, bsum, hbsum);
     k_cmp_top<<<1, 64, 0, s>>>(bsum, hbsum, nb);
     k_cmp_add<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(pos, hpos, bsum, hbsum, n, nb);
-    k_cmp_breaks<<<1, 64, 0, s>>>(pos, n, max_file_size, c->d_cfstart.as<uint32_t>(), cap + 1, c->d_cnf.as<uint32_t>());
-    uint64_t tot[2] = {0, 0};
+    uint64_t tot[3] = {0, 0, 0};  // data bytes, hint bytes, pos[1]
     uint32_t nf = 0;
     GCK_HIP(hipMemcpyAsync(&tot[0], pos + n, 8, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipMemcpyAsync(&tot[1], hpos + n, 8, hipMemcpyDeviceToHost, s));
+    if (n) GCK_HIP(hipMemcpyAsync(&tot[2], pos + 1, 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    // consecutive merged files hold more than M together (a file closes when
+    // the next entry does not fit), so there are at most 2 bytes / M + 2
+    const uint64_t est = std::min<uint64_t>(2 * (tot[0] / max_file_size) + 2, (uint64_t)cap);
+    if (n == 0 || est <= kSerialBreakFiles) {
+        k_cmp_breaks<<<1, 64, 0, s>>>(pos, n, max_file_size, c->d_cfstart.as<uint32_t>(), cap + 1, c->d_cnf.as<uint32_t>());
+    } else {
+        if ((rc = c->d_cjmp.ensure((n + 1) * 8 + (n + 1) * 4)) || (rc = c->d_con.ensure(n * 4 + 16))) return rc;
+        uint32_t *jmp = c->d_cjmp.as<uint32_t>(), *jmp2 = jmp + (n + 1), *on = c->d_con.as<uint32_t>();
+        const uint32_t g1 = (uint32_t)((n + 1 + 255) / 256);
+        k_cmp_next<<<g1, 256, 0, s>>>(pos, n, max_file_size, jmp, on);
+        for (uint64_t reach = 1; reach < est; reach <<= 1) {  // starts within `reach` steps of record 0 are marked
+            k_cmp_mark<<<g1, 256, 0, s>>>(jmp, on, n);
+            if (reach * 2 < est) {
+                k_cmp_jump<<<g1, 256, 0, s>>>(jmp, jmp2, n);
+                std::swap(jmp, jmp2);
+            }
+        }
+        k_cmp_fcount<<<(uint32_t)nb, kCmpBlock, 0, s>>>(on, n, bsum);
+        const uint32_t lead = tot[2] > max_file_size ? 1u : 0u;  // pos[1] - pos[0] (= 0) > M: an empty first file
+        k_cmp_ftop<<<1, 64, 0, s>>>(bsum, nb, lead, c->d_cfstart.as<uint32_t>(), n, c->d_cnf.as<uint32_t>());
+        k_cmp_fscatter<<<(uint32_t)nb, kCmpBlock, 0, s>>>(on, n, bsum, c->d_cfstart.as<uint32_t>() + lead);
+    }
     GCK_HIP(hipMemcpyAsync(&nf, c->d_cnf.p, 4, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
     if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16))) return rc;
@@ -326,12 +450,10 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
                                                                c->d_chint.as<uint8_t>());
     }
     GCK_HIP(hipGetLastError());
-    GCK_HIP(hipEventRecord(e1, s));
-    GCK_HIP(hipEventSynchronize(e1));
+    GCK_HIP(hipEventRecord(ev.b, s));
+    GCK_HIP(hipEventSynchronize(ev.b));
     float t = 0;
-    GCK_HIP(hipEventElapsedTime(&t, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
+    GCK_HIP(hipEventElapsedTime(&t, ev.a, ev.b));
     if (ms) *ms = t;
     c->cmp_files = nf;
     c->cmp_data = tot[0];

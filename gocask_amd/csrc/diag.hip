@@ -1,4 +1,5 @@
-// diag.hip — measurement helpers (not on the replay path).
+// diag.hip — measurement helpers (not on the replay path), built as the
+// separate libgocask_diag.so (gck_diag.h), linked against libgocask_hip.so.
 //
 // gck_diag_stream_read: a plain streaming read of the resident arena (16 B per
 // lane, grid-stride, non-temporal loads — the faster of the two policies, as
@@ -7,6 +8,7 @@
 // bench.py / DESIGN.md (SURVEY.md §8d asks for the fraction of a measured
 // streaming-read kernel besides the spec peak).
 #include "gck_internal.h"
+#include "gck_diag.h"
 
 namespace gck {
 

@@ -282,9 +282,6 @@ int gck_encode_walk_order(gck_ctx *ctx, uint32_t *creation_index, uint32_t n) {
 namespace gck {
 
 constexpr uint32_t kEncScanBlock = 1024;
-#ifndef GCK_ENC_XP
-#define GCK_ENC_XP 0  // ablation (timing only): 1 no byte path, 2 no stores
-#endif
 
 // 1a. sizes, block-local exclusive prefix (into out_off), block sums, refusals
 __global__ __launch_bounds__(1024) void k_enc_sizes(const uint64_t *__restrict__ key_off,
@@ -370,13 +367,17 @@ __global__ void k_enc_units(const uint64_t *__restrict__ out_off, uint64_t n, ui
     }
 }
 
-// The 16 bytes at src (any alignment): two dword-aligned loads, a byte shift
-// (reads up to 3 bytes before src and 4 after the 16).
+// The 16 bytes at src (any alignment): two dword-aligned loads, a byte shift.
+// Reads the dwords holding [src, src + 16) only: the second load is the dword
+// after the first 16 B when src is unaligned (it holds bytes of the window),
+// else a dword inside them (alignbyte by 0 ignores it).  With a 4-byte aligned
+// blob base nothing outside the blob's dwords is read (gck_encode_batch checks
+// the alignment).
 __device__ __forceinline__ uint4 load16u(const uint8_t *src) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(src) & 3);
     const uint8_t *a = src - sh;
     const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
-    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + 16);
+    const uint32_t y = *reinterpret_cast<const uint32_t *>(a + (sh ? 16 : 12));
     return make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, sh), __builtin_amdgcn_alignbyte(x.z, x.y, sh),
                       __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
 }
@@ -485,7 +486,7 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
             rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
             // (uniform) the whole row inside one record's value: most rows
             // of large records; its fields by readlane, no permutes
-            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr && R + 1024 <= O1 && !(GCK_ENC_XP & 2)) {
+            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr && R + 1024 <= O1) {
                 const int src = (int)rr;
                 const uint64_t s0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oo >> 32), src) << 32) |
                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oo, src);
@@ -526,8 +527,6 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
                     w[2] = v.z;
                     w[3] = v.w;
                     mask = 0xFFFFu;
-                } else if (GCK_ENC_XP & 1) {
-                    mask = 0xFFFFu;  // ablation: no byte path (wrong bytes)
                 } else {
                     // byte by byte.  The key / value bytes come from 16 B
                     // windows aligned to the chunk (chunk byte i = key byte
@@ -571,9 +570,7 @@ __global__ __launch_bounds__(MODE == 1 ? 1024 : 256) void k_encode_batch(const u
                     }
                 }
             }
-            if (GCK_ENC_XP & 2) {
-                if (w[0] == 0x12345678u && w[1] == mask) out[X] = 1;  // keep the work live
-            } else if (mask == 0xFFFFu) {
+            if (mask == 0xFFFFu) {
                 *reinterpret_cast<uint4 *>(out + X) = make_uint4(w[0], w[1], w[2], w[3]);
             } else if (mask) {  // the group's first or last chunk: its bytes only
                 for (uint32_t i = 0; i < 16; ++i)
@@ -591,6 +588,8 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
                                 uint8_t *out, uint64_t out_cap, uint64_t *out_off, uint64_t *total,
                                 void *stream) {
     if (!key_off || !val_off || !out_off || !total || (n && (!keys || !out || !ts || !tomb))) return GCK_EINVAL;
+    // the kernels read whole dwords of the key / value blobs from their base
+    if ((reinterpret_cast<uintptr_t>(keys) | reinterpret_cast<uintptr_t>(vals)) & 3) return GCK_EINVAL;
     int ndev = 0, dev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0 || hipGetDevice(&dev) != hipSuccess) return GCK_EDEVICE;
     hipStream_t s = (hipStream_t)stream;

@@ -50,6 +50,20 @@ __device__ __forceinline__ uint32_t gmul(uint32_t a, uint32_t b) {
     return p;
 }
 
+// Inclusive XOR prefix within each 16-lane row (DPP row shifts), then row 0's
+// total into row 1 and row 2's into row 3 (row_bcast:15): lane 31 = XOR of
+// lanes 0..31, lane 63 = XOR of lanes 32..63.  DPP moves data in the VALU;
+// __shfl_xor compiles to ds_bpermute through the LDS crossbar.  All lanes
+// must be active (callers run it in wave-uniform control flow).
+__device__ __forceinline__ uint32_t half_xor(uint32_t f) {
+    f ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x111, 0xF, 0xF, false);  // row_shr:1
+    f ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x112, 0xF, 0xF, false);  // row_shr:2
+    f ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x114, 0xF, 0xF, false);  // row_shr:4
+    f ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x118, 0xF, 0xF, false);  // row_shr:8
+    f ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    return f;
+}
+
 __device__ __forceinline__ uint32_t zmul(const uint32_t (*Z)[256], uint32_t a) {
     return Z[0][a & 0xFF] ^ Z[1][(a >> 8) & 0xFF] ^ Z[2][(a >> 16) & 0xFF] ^ Z[3][a >> 24];
 }
@@ -70,16 +84,15 @@ __device__ __forceinline__ uint32_t lanes_combine(const CrcTabs &t, uint32_t lb0
         x8[q] = lds_at(t.Ls + q * 512, __builtin_amdgcn_bitop3_b32(x, 0x780u, lb0, 0xEA));
     }
     uint32_t f = xor3(xor3(x8[0], x8[1], x8[2]), xor3(x8[3], x8[4], x8[5]), x8[6] ^ x8[7]);
-#pragma unroll
-    for (int m = 16; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)f, 0), hi = (uint32_t)__builtin_amdgcn_readlane((int)f, 32);
+    // XOR over each half-wave by DPP (row prefixes, then row 0 into row 1 and
+    // row 2 into row 3): lane 31 holds lanes 0..31, lane 63 lanes 32..63
+    f = half_xor(f);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)f, 31), hi = (uint32_t)__builtin_amdgcn_readlane((int)f, 63);
     return ~(zmul(t.Z512, lo) ^ hi);
 }
 __device__ __forceinline__ uint32_t lanes_combine_gmul(uint32_t kl, uint32_t A) {
-    uint32_t f = gmul(kl, A);  // kl = x^(8 * 16 (63 - lane))
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) f ^= __shfl_xor(f, m);
-    return ~f;
+    uint32_t f = half_xor(gmul(kl, A));  // kl = x^(8 * 16 (63 - lane))
+    return ~((uint32_t)__builtin_amdgcn_readlane((int)f, 31) ^ (uint32_t)__builtin_amdgcn_readlane((int)f, 63));
 }
 
 // The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
@@ -89,9 +102,6 @@ __device__ __forceinline__ uint32_t lanes_combine_gmul(uint32_t kl, uint32_t A) 
 // bytes); a lane straddling the value start reads up to 15 bytes before it
 // (the record's header and key: inside the arena).
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-#ifndef GCK_CRC_NT
-#define GCK_CRC_NT 1  // non-temporal stripe loads (scrub 4.92 -> 4.76-4.90 ms)
-#endif
 // (Pointer arithmetic only, never an integer cast back to a pointer: that
 // would make the loads flat, and flat loads also count on lgkmcnt, so every
 // LDS table wait would wait for HBM too.)
@@ -117,16 +127,15 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32
         const uint8_t *p0 = jb.p - (reinterpret_cast<uintptr_t>(jb.p) & 3);
         a = v + 16 <= jb.pad ? p0 : a;
     }
-#if GCK_CRC_NT
+    // non-temporal stripe loads (scrub 4.92 -> 4.76-4.90 ms)
     const u32x4_a4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(a));
-#else
-    const u32x4_a4 x = *reinterpret_cast<const u32x4_a4 *>(a);
-#endif
     d[0] = x.x;
     d[1] = x.y;
     d[2] = x.z;
     d[3] = x.w;
-    d[4] = *reinterpret_cast<const uint32_t *>(a + 16);
+    // the dword after the chunk when the shift needs it, else one inside it
+    // (alignbyte by 0 ignores d[4]): nothing past a value's last dword is read
+    d[4] = *reinterpret_cast<const uint32_t *>(a + (jb.sh ? 16 : 12));
 }
 
 // crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
@@ -172,10 +181,7 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
 // ahead is far below what HBM latency needs).  All control is wave-uniform;
 // every load is issued unconditionally (a dummy reload past the last stripe),
 // so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
-#ifndef GCK_RING
-#define GCK_RING 4
-#endif
-constexpr int kRing = GCK_RING;
+constexpr int kRing = 4;  // ring depths 2, 4 and 8 measured the same
 template <class PtrOf, class Combine>
 __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const CrcTabs &t, uint32_t lb0,
                               uint32_t lb1, Combine combine) {

@@ -49,7 +49,7 @@ enum Phase {
     PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
     PH_SCAN,          // record slots per chunk, per-file summary
     PH_HOST,          // D2H summary + host bookkeeping
-    PH_RECORDS,       // k_compact, k_row_fill / k_row_index, k_row_plan
+    PH_RECORDS,       // k_row_fill, k_compact, k_row_tail
     PH_CRC,           // k_crc_rows: the HBM-bound kernel
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
@@ -94,7 +94,7 @@ struct Ctx {
     DBuf d_rec_off, d_rec_kv, d_rec_file, d_ep, d_out;  // record table: arena offset, (KeySize, ValueSize), file
     // rows
     uint64_t n_rows = 0;
-    DBuf d_row_first, d_rend, d_plan, d_queue;
+    DBuf d_row_first, d_rend, d_queue;
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow;
@@ -107,6 +107,7 @@ struct Ctx {
     // compaction (compact.hip): record / hint-entry offsets, block sums, file
     // starts, file count, merged data and hint bytes
     DBuf d_cpos, d_chpos, d_cbsum, d_cfstart, d_cnf, d_cdata, d_chint;
+    DBuf d_cjmp, d_con;  // many-file rotation points: jump pointers (two copies), start marks
     uint32_t cmp_files = 0;
     uint64_t cmp_data = 0, cmp_hint = 0;
     // keydir merge across shards: pack partition of each live entry, the

@@ -37,25 +37,6 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
-#ifndef GCK_NR
-#define GCK_NR 1
-#endif
-constexpr int kRowsPerStep = GCK_NR;  // rows a k_crc_rows wavefront processes at once
-#ifndef GCK_PF
-#define GCK_PF 1
-#endif
-// Row plan source for k_crc_rows: 0 = k_row_plan's dense 32 B per row; 1 = each
-// block's nibbles built in k_crc_rows from the record table; 2 = the same with
-// the block's first 64 record ends loaded one block ahead (shipped: C3 step
-// 7.11-7.13 -> 6.76-6.94 ms on one box, records phase 0.20 -> 0.11 ms, and
-// k_crc_rows no longer reads 268 MB of plan)
-#ifndef GCK_SPLAN
-#define GCK_SPLAN 2
-#endif
-#ifndef GCK_EPACC
-#define GCK_EPACC 0  // k_crc_rows: (c, pre) gathered per block and stored 64 slots at a time
-#endif
-constexpr int kPrefetch = GCK_PF;  // k_crc_rows: steps between a row's loads and its processing
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -90,21 +71,6 @@ __device__ __forceinline__ Hdr ld_hdr(const uint8_t *__restrict__ arena, uint64_
     return h;
 }
 
-// The same 16 bytes with two loads (16 B + 4 B, dword aligned) instead of five.
-typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ Hdr ld_hdr2(const uint8_t *__restrict__ arena, uint64_t o) {
-    const uint8_t *p = arena + (o & ~3ull);
-    const u32x4_a4 v = *reinterpret_cast<const u32x4_a4 *>(p);
-    const uint32_t w4 = *reinterpret_cast<const uint32_t *>(p + 16);
-    const uint32_t sh = (uint32_t)o & 3u;
-    Hdr h;
-    h.crc = ab(v.y, v.x, sh);
-    h.ts = ab(v.z, v.y, sh);
-    h.ks = ab(v.w, v.z, sh);
-    h.vs = ab(w4, v.w, sh);
-    return h;
-}
-
 // Follow the header chain from q for kHops+1 headers: key length in
 // [1, max_key] and every record inside the file.  A chain may only end exactly
 // at the file end.  (A record straddling the file end is rejected: that only
@@ -127,11 +93,11 @@ __device__ bool chain_ok(const uint8_t *__restrict__ arena, uint64_t base, uint6
 // The reference's readEntry loop (core/db.go:131-178) over one chunk: decode
 // headers from p while p < ce.  EOF classes follow Go's io.ReadFull /
 // bufio.Reader.Discard semantics.  emit(i, p, hdr) per record.
-template <class Emit, bool H2 = false>
+template <class Emit>
 __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uint64_t len, uint64_t ce,
                            uint64_t p, Emit emit, uint32_t &count, uint64_t &exit, uint32_t &term,
                            uint64_t &tpos) {
-    auto ld = [&](uint64_t o) { return H2 ? ld_hdr2(arena, o) : ld_hdr(arena, o); };
+    auto ld = [&](uint64_t o) { return ld_hdr(arena, o); };
     uint32_t n = 0;
     term = T_NONE;
     tpos = 0;
@@ -355,10 +321,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
 // writes 64 / kStageIl runs of kStageIl consecutive elements (whole lines)
 // instead of 64 scattered partial lines (measured: those cost half of the
 // walk), and k_compact still reads a chunk's slots at a short stride.
-#ifndef GCK_STAGE_IL
-#define GCK_STAGE_IL 8
-#endif
-constexpr uint32_t kStageIl = GCK_STAGE_IL;
+constexpr uint32_t kStageIl = 8;
 __host__ __device__ __forceinline__ uint64_t stage_slot(uint32_t c, uint32_t i, uint32_t cap) {
     return ((uint64_t)(c / kStageIl) * (cap + 1) + (i < cap ? i : cap)) * kStageIl + (c % kStageIl);
 }
@@ -807,67 +770,11 @@ __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *_
     for (uint64_t row = (end + kRow - 1) / kRow + threadIdx.x; row < r1; row += blockDim.x) row_first[row] = v;
 }
 
-constexpr int kBlock = 16;       // capture granularity inside a slab (4 per slab)
-constexpr int kBlockRows = 64;   // rows per plan block = per k_crc_rows work item
-// cache policy of k_crc_rows' arena loads (buffer aux bits: 1 sc0, 2 nt, 16 sc1)
-#ifndef GCK_ARENA_AUX
-#define GCK_ARENA_AUX 2
-#endif
-#ifndef GCK_CLAIM
-#define GCK_CLAIM 2
-#endif
-constexpr uint32_t kClaim = GCK_CLAIM;  // consecutive blocks per k_crc_rows queue claim
-#ifndef GCK_STATIC8
-#define GCK_STATIC8 4
-#endif
-constexpr uint32_t kStaticEighths = GCK_STATIC8;  // eighths of k_crc_rows' full rounds assigned statically
-constexpr int kPlanLaneBytes = 32;  // plan bytes per lane per block (64 rows x 4 bits)
-constexpr int kPlanRowBytes = kPlanLaneBytes * 64 / kBlockRows;  // = 32: plan bytes per row
+constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
+constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
+constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue claim
+constexpr uint32_t kStaticEighths = 4;     // eighths of k_crc_rows' full rounds assigned statically
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
-
-// Row plan for k_crc_rows, lane-major per block of 64 rows so that a
-// wavefront loads the plan of a whole block with two 16 B loads per lane:
-//   block q, lane k (slab k): 32 B = 8 dwords; dword d, nibble n belongs to
-//   row 64q + 8d + n; its bit b is set iff a record's last byte lies in block b
-//   of slab k, i.e. in row bytes [64k + 16b, 64k + 16b + 16).  A 16 B block
-//   holds at most one record end: records are at least 16 B (a bare header).
-// The first record whose end lies past a row's start is row_first[row]
-// (k_compact, k_row_tail); record ids of the ends follow from it and a count over the
-// lanes, so the plan carries no ids.
-//
-// One wavefront per block: the records ending in its rows are a contiguous
-// range, read 64 at a time (coalesced); each lane ORs its record's bit into
-// an LDS image of the block, then each lane writes its 32 B (2 KiB contiguous
-// per wavefront).
-constexpr int kPlanWaves = 4;
-
-__global__ __launch_bounds__(64 * kPlanWaves) void k_row_plan(const uint64_t *__restrict__ rec_off,
-                                                              const uint2 *__restrict__ rec_kv,
-                                                              uint64_t r0, uint64_t nr,
-                                                              const uint32_t *__restrict__ row_first,
-                                                              uint4 *__restrict__ plan) {
-    __shared__ uint32_t cut_lds[kPlanWaves][64 * 9];  // lane stride 9 dwords: conflict-free row reads
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t R0 = r0 + ((uint64_t)blockIdx.x * kPlanWaves + wv) * kBlockRows, r1 = r0 + nr;
-    if (R0 >= r1) return;
-    uint32_t *cw = cut_lds[wv];
-    for (uint32_t i = lane; i < 64 * 9; i += 64) cw[i] = 0;
-    const uint64_t Re = min(R0 + kBlockRows, r1);           // rows [R0, Re)
-    const uint64_t lo = row_first[R0], hi = row_first[Re];  // records ending in rows [R0, Re)
-    for (uint64_t b = lo; b < hi; b += 64) {
-        const uint64_t r = b + lane;
-        if (r < hi) {
-            const uint64_t last = value_end(rec_off, rec_kv, r) - 1;  // the record's last byte
-            const uint32_t rl = (uint32_t)(last / kRow - R0);          // 0..63
-            const uint32_t o = (uint32_t)(last % kRow), slab = o / kSlab, blk = (o % kSlab) / kBlock;
-            atomicOr(cw + slab * 9 + rl / 8, (1u << blk) << (4 * (rl % 8)));
-        }
-    }
-    // the launch's plan counts blocks from its first row r0
-    uint4 *dst = plan + ((R0 - r0) / kBlockRows) * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
-    dst[0] = make_uint4(cw[lane * 9], cw[lane * 9 + 1], cw[lane * 9 + 2], cw[lane * 9 + 3]);
-    dst[1] = make_uint4(cw[lane * 9 + 4], cw[lane * 9 + 5], cw[lane * 9 + 6], cw[lane * 9 + 7]);
-}
 
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
@@ -897,34 +804,31 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 //     lane's LDS table), and an inclusive prefix XOR over the wave (DPP) gives
 //     rrow = F(0, row) (lane 63) and, per lane, pre = the exclusive prefix =
 //     the slabs before k referenced to the row end;
-//   - per record end (plan: block b of slab k) the lane stores (c_b, pre) at
-//     the record's slot; k_finalize continues c_b over the <= 16 bytes of the
+//   - per record end in block b of slab k the lane stores (c_b, pre) at the
+//     record's slot; k_finalize continues c_b over the <= 16 bytes of the
 //     block up to the record end and stitches rows (see there).
 // Outputs: out_ep (c, pre) per record, out_rend per row (rrow).
 //
-// Work: blocks of 64 consecutive rows from an atomic queue (late-starting or
-// slow wavefronts simply take fewer blocks), NR rows per step.  Per block a
-// lane loads its 32 plan bytes and row_first of one row (3 loads, issued a
-// block ahead) and the block's 64 rrow values leave in one coalesced store,
-// so per row the vector-memory queue holds only the 4 x 16 B row loads and
-// one 8 B (c, pre) store.  Rows are local to the launch: arena, plan,
-// row_first and out_rend point at its first row; n_total is the record-slot
-// scratch base (64 slots per wavefront), rend_scratch 64 row slots.
+// Work: row blocks of 64 consecutive rows, the first half of the full rounds
+// static, the rest from an atomic queue (late-starting or slow wavefronts take
+// fewer).  Per block the record ends of its rows (records [row_first[first
+// row], row_first[first row + 64]), in offset order) become per-lane nibbles
+// (bit b of row j's nibble in lane k: a record's last byte lies in block b of
+// slab k); the first 64 ends are loaded one block ahead.  The block's 64 rrow
+// values leave in one coalesced store, so per row the vector-memory queue
+// holds only the 4 x 16 B row loads and one 8 B (c, pre) store.  Rows are
+// local to the launch: arena, row_first and out_rend point at its first row
+// (row0 in the whole arena); n_total is the record-slot scratch base (64
+// slots per wavefront), rend_scratch 64 row slots.
 //
 // Memory pipeline: the row data are buffer loads (row base in a scalar
-// resource, lane offset in a fixed VGPR) issued one step ahead.  No scalar
+// resource, lane offset in a fixed VGPR) issued one row ahead.  No scalar
 // loads in the loop: an outstanding SMEM load would make every LDS wait
 // (lgkmcnt(0)) wait for HBM too.  Every lane stores on every path (lanes
-// without a record end to their scratch slot), so the compiler's vmcnt waits
-// count the same stores on every path and stay a step behind the loads.
-//
-// MODE (ablation, gck_diag_crc_variant): 2 = no LDS table chain, 4 = no row
-// shift / wave scan, 8 = synthetic bytes instead of loads, 16 = no (c, pre)
-// stores, 32 = the default cache policy instead of non-temporal loads, 64 = no
-// LDS table fill, 128 = static block assignment only.
-template <int MODE, int NR>
+// without a record end to an out-of-range offset, dropped), so the compiler's
+// vmcnt waits count the same stores on every path and stay a row behind the
+// loads.
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint4 *__restrict__ plan,
                                                    const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
@@ -933,10 +837,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    uint32_t *__restrict__ queue,
                                                    const uint64_t *__restrict__ rec_off,
                                                    const uint2 *__restrict__ rec_kv, uint64_t row0) {
-    static_assert(kBlockRows % (4 * NR) == 0, "a block is whole quads of steps");
-    constexpr int kSteps = kBlockRows / NR;  // steps per block
+    constexpr int kSteps = kBlockRows;  // rows per block, one per step
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
-    if constexpr ((MODE & 64) == 0) fill_crc_lds(lds, g_slice, g_nib);
+    fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     static_assert(kNibBase * 4 == 0x20000, "shift-table addresses: byte 2 of the v_perm base");
     const uint32_t nbase = kNibBase * 4 + lane * 4;  // byte 0: the lane's bank, byte 2: the region
@@ -969,7 +872,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     // compute, a fully static split loses to the queue's balance (6.02 vs
     // 5.82 ms), half static / half queue is best (5.77).
     const uint32_t W = gridDim.x * kWaves, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    const uint32_t n_static = (MODE & 128) ? (uint32_t)((n_blocks + W - 1) / W) : (uint32_t)(n_blocks / W) * kStaticEighths / 8;
+    const uint32_t n_static = (uint32_t)(n_blocks / W) * kStaticEighths / 8;
     uint32_t st_k = 0;
     uint32_t last = kClaim - 1;
     auto grab = [&]() -> uint32_t {  // next block index
@@ -984,31 +887,20 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         return last;
     };
     struct Plan {
-#if !GCK_SPLAN
-        uint4 a, b;  // the lane's 64 row nibbles
-#endif
-        uint32_t ra; // row_first of row lane
-        uint32_t re; // row_first of the block's end (GCK_SPLAN)
+        uint32_t ra;  // row_first of row `lane` of the block
+        uint32_t re;  // row_first of the block's end
     };
     auto load_plan = [&](uint64_t q, Plan &p) {
         const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
-#if !GCK_SPLAN
-        const uint4 *src = plan + qc * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
-        p.a = src[0];
-        p.b = src[1];
-#else
         p.re = row_first[min(qc * kBlockRows + kBlockRows, n_rows)];
-#endif
         p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
     };
-#if GCK_SPLAN
-    // The block's plan nibbles from its record ends (records [ra0, re) end in
-    // its rows, in offset order), instead of k_row_plan's dense 32 B per row:
-    // a lane per record computes (row, slab, block) of its last byte, then a
-    // uniform loop hands each end to the slab's lane (nibble dword chosen by
-    // a uniform index).
-    // GCK_SPLAN 2: the first 64 record ends of a block are loaded one block
-    // ahead (Batch); later ones (blocks with more than 64 ends) on the spot
+    // The block's nibbles from its record ends (records [ra0, re) end in its
+    // rows, in offset order): a lane per record computes (row, slab, block) of
+    // its last byte, then a uniform loop hands each end to the slab's lane
+    // (nibble dword chosen by a uniform index).  The first 64 record ends of a
+    // block are loaded one block ahead (Batch); later ones (blocks with more
+    // than 64 ends) on the spot.
     struct Batch {
         uint64_t off;
         uint2 kv;
@@ -1018,7 +910,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         b.off = rec_off[r];
         b.kv = rec_kv[r];
     };
-    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch *first, uint32_t (&nb)[8]) {
+    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch &first, uint32_t (&nb)[8]) {
 #pragma unroll
         for (int d = 0; d < 8; ++d) nb[d] = 0;
         const uint64_t base = (row0 + row_b) * kRow;
@@ -1026,8 +918,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             const uint32_t r = b0 + lane;
             uint32_t code = 0;
             if (r < re_) {
-                const uint64_t end = first && b0 == ra0_ ? first->off + 16 + (uint64_t)first->kv.x + first->kv.y
-                                                         : value_end(rec_off, rec_kv, r);
+                const uint64_t end = b0 == ra0_ ? first.off + 16 + (uint64_t)first.kv.x + first.kv.y
+                                                : value_end(rec_off, rec_kv, r);
                 const uint64_t rel = end - 1 - base;  // < 64 rows
                 code = ((uint32_t)(rel >> 12) << 8) | ((uint32_t)(rel >> 6) & 63u) << 2 | ((uint32_t)(rel >> 4) & 3u);
             }
@@ -1050,292 +942,162 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             }
         }
     };
-#endif
-    struct RowBuf {
-        u32x4 x[4];
+    auto issue = [&](uint64_t row, u32x4 (&x)[4]) {
+        // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
+        const uint32_t r = min((uint32_t)row, (uint32_t)(n_rows - 1));
+        const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kArenaAux);
     };
-    auto issue = [&](uint64_t row0, RowBuf (&bs)[NR]) {
-        if constexpr ((MODE & 8) != 0) return;
+    // one row: row j of the block; m = its nibble in this lane
+    auto process = [&](uint32_t j, uint32_t m, uint32_t ra_reg, const u32x4 (&x)[4], uint32_t &rend_buf) {
+        // w[4 k + c] = dword c of load k; M[b][k] = lane (p + 16 b)'s load k
+        // (= row bytes 1024 k + 64 p + 16 b).  permlane32_swap on (k, k+2)
+        // then permlane16_swap on (k, k+1) transpose M over each lane group
+        // {p, p+16, p+32, p+48}: lane p + 16 r ends with M[0..3][r] = the
+        // bytes 1024 r + 64 p + 16 b, b = 0..3, i.e. slab 16 r + p.
+        uint32_t w[16];
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
-            const uint32_t r = min((uint32_t)(row0 + i), (uint32_t)(n_rows - 1));
-            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
-            constexpr int kAux = (MODE & 32) ? 0 : GCK_ARENA_AUX;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
+        for (int k = 0; k < 4; ++k) {
+            w[4 * k] = x[k].x;
+            w[4 * k + 1] = x[k].y;
+            w[4 * k + 2] = x[k].z;
+            w[4 * k + 3] = x[k].w;
         }
-    };
-    // GCK_EPACC: (c, pre) of consecutive record slots gathered in two
-    // registers (lane l = slot acc_base + l) and stored 64 at a time, at the
-    // block end or when full, instead of one 64-lane store per row
-    uint32_t acc_c = 0, acc_p = 0, acc_n = 0, acc_base = 0;
-    auto acc_flush = [&]() {
-        store_ep(lane < acc_n ? (acc_base + lane - ra0) * 8u : kDrop, acc_c, acc_p);
-        acc_base += acc_n;
-        acc_n = 0;
-    };
-    // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
-    // nib holds their plan nibbles from bit 0 up
-    auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t ra_reg, const RowBuf (&bs)[NR],
-                       uint32_t &rend_buf) {
-        uint32_t w[NR][16];
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            // w[i][4 k + c] = dword c of load k; M[b][k] = lane (p + 16 b)'s load k
-            // (= row bytes 1024 k + 64 p + 16 b).  permlane32_swap on (k, k+2)
-            // then permlane16_swap on (k, k+1) transpose M over each lane group
-            // {p, p+16, p+32, p+48}: lane p + 16 r ends with M[0..3][r] = the
-            // bytes 1024 r + 64 p + 16 b, b = 0..3, i.e. slab 16 r + p.
+        for (int c = 0; c < 4; ++c) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                w[i][4 * k] = bs[i].x[k].x;
-                w[i][4 * k + 1] = bs[i].x[k].y;
-                w[i][4 * k + 2] = bs[i].x[k].z;
-                w[i][4 * k + 3] = bs[i].x[k].w;
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(w[i][4 * k + c], w[i][4 * (k + 2) + c], false, false);
-                    w[i][4 * k + c] = r[0];
-                    w[i][4 * (k + 2) + c] = r[1];
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-#pragma unroll
-                for (int k = 0; k < 4; k += 2) {
-                    const auto r = __builtin_amdgcn_permlane16_swap(w[i][4 * k + c], w[i][4 * (k + 1) + c], false, false);
-                    w[i][4 * k + c] = r[0];
-                    w[i][4 * (k + 1) + c] = r[1];
-                }
-            }
-            if constexpr ((MODE & 8) != 0) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[i][j] = (uint32_t)(row0 + i) * 2654435761u + lane * 97u + j;
+            for (int k = 0; k < 2; ++k) {
+                const auto r = __builtin_amdgcn_permlane32_swap(w[4 * k + c], w[4 * (k + 2) + c], false, false);
+                w[4 * k + c] = r[0];
+                w[4 * (k + 2) + c] = r[1];
             }
         }
-        // NR independent chains interleaved: NR table reads in flight per step
-        uint32_t a[NR], c1[NR], c2[NR], c3[NR], G[NR];
 #pragma unroll
-        for (int i = 0; i < NR; ++i) a[i] = w[i][0];
+        for (int c = 0; c < 4; ++c) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) {
-                const uint32_t nx = j < 15 ? w[i][j < 15 ? j + 1 : 15] : 0u;
-                if constexpr ((MODE & 2) != 0) {
-                    a[i] = (__builtin_amdgcn_alignbit(a[i], a[i], 5) + 0x9E3779B9u) ^ nx;
-                    if (j == 3) c1[i] = a[i];
-                    if (j == 7) c2[i] = a[i];
-                    if (j == 11) c3[i] = a[i];
-                    if (j == 15) G[i] = a[i];
-                } else if (j == 15) {
-                    G[i] = slice4x(lds, lb0, lb1, a[i], 0u);
-                } else if ((j & 3) == 3) {
-                    const uint32_t c = slice4x(lds, lb0, lb1, a[i], 0u);
-                    if (j == 3) c1[i] = c;
-                    if (j == 7) c2[i] = c;
-                    if (j == 11) c3[i] = c;
-                    a[i] = c ^ nx;
-                } else {
-                    a[i] = slice4x(lds, lb0, lb1, a[i], nx);
-                }
+            for (int k = 0; k < 4; k += 2) {
+                const auto r = __builtin_amdgcn_permlane16_swap(w[4 * k + c], w[4 * (k + 1) + c], false, false);
+                w[4 * k + c] = r[0];
+                w[4 * (k + 1) + c] = r[1];
             }
         }
-        // Z_{64(63-lane)}(G) of every row (8 nibble lookups in the lane's
-        // table), then the NR wave scans interleaved so each DPP read finds
-        // its source written a few instructions earlier (no s_nop hazards).
-        // Lookup addresses: byte k of ge / go holds nibble 2k / 2k+1 of G
-        // with the nibble's index in its high half, which makes byte 1 of the
-        // address (table q, entry v): one v_perm_b32 per lookup, 3 VALU to
-        // split G (was a shift, an and and an add per lookup)
-        uint32_t P[NR], pre[NR];
+        uint32_t a = w[0], c1 = 0, c2 = 0, c3 = 0, G = 0;
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            if constexpr ((MODE & 4) == 0) {
-                // (x & m) | q in one v_bitop3_b32 (truth table 0xEA; the two
-                // constants live in registers set up outside the loop)
-                const uint32_t ge = __builtin_amdgcn_bitop3_b32(G[i], 0x0F0F0F0Fu, 0x60402000u, 0xEA);
-                const uint32_t go = __builtin_amdgcn_bitop3_b32(G[i] >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
-                uint32_t t[8];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    t[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
-                    t[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
-                }
-                P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
+        for (int t = 0; t < 16; ++t) {
+            const uint32_t nx = t < 15 ? w[t < 15 ? t + 1 : 15] : 0u;
+            if (t == 15) {
+                G = slice4x(lds, lb0, lb1, a, 0u);
+            } else if ((t & 3) == 3) {
+                const uint32_t c = slice4x(lds, lb0, lb1, a, 0u);
+                if (t == 3) c1 = c;
+                if (t == 7) c2 = c;
+                if (t == 11) c3 = c;
+                a = c ^ nx;
             } else {
-                P[i] = G[i];
+                a = slice4x(lds, lb0, lb1, a, nx);
             }
         }
-        if constexpr ((MODE & 4) == 0) {
+        // Z_{64(63-lane)}(G) (8 nibble lookups in the lane's table), then the
+        // wave scan.  Lookup addresses: byte k of ge / go holds nibble 2k /
+        // 2k+1 of G with the nibble's index in its high half, which makes byte
+        // 1 of the address (table q, entry v): one v_perm_b32 per lookup; the
+        // split is (x & m) | q in one v_bitop3_b32 (truth table 0xEA)
+        const uint32_t ge = __builtin_amdgcn_bitop3_b32(G, 0x0F0F0F0Fu, 0x60402000u, 0xEA);
+        const uint32_t go = __builtin_amdgcn_bitop3_b32(G >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
+        uint32_t t8[8];
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);  // row_shr:1
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);  // row_shr:2
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);  // row_shr:4
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);  // row_shr:8
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);  // row_bcast:15 -> rows 1, 3
-#pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);  // row_bcast:31 -> rows 2, 3
-#pragma unroll
-            for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);  // wave_shr:1 -> exclusive (lane 0: 0)
+        for (int k = 0; k < 4; ++k) {
+            t8[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
+            t8[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
+        }
+        uint32_t P = xor3(xor3(t8[0], t8[1], t8[2]), xor3(t8[3], t8[4], t8[5]), t8[6] ^ t8[7]);
+        P ^= dpp<0x111, 0xF>(P);  // row_shr:1
+        P ^= dpp<0x112, 0xF>(P);  // row_shr:2
+        P ^= dpp<0x114, 0xF>(P);  // row_shr:4
+        P ^= dpp<0x118, 0xF>(P);  // row_shr:8
+        P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
+        P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
+        const uint32_t pre = dpp<0x138, 0xF>(P);  // wave_shr:1 -> exclusive (lane 0: 0)
+        const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
+        // the register at the start of block b, by masks (no branches; a
+        // chain of selects was turned into a lookup in a scratch copy of
+        // c1..c3)
+        auto cap = [&](uint32_t b) {
+            return (c1 & (0u - (uint32_t)(b == 1))) | (c2 & (0u - (uint32_t)(b == 2))) | (c3 & (0u - (uint32_t)(b == 3)));
+        };
+        if (__ballot(m & (m - 1)) == 0) {
+            // common case: at most one record end per slab, its slot is
+            // ra + (lanes with an end before this one)
+            const uint64_t C = __ballot(m != 0);
+            const uint32_t idx =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
+            store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre);
         } else {
+            // a slab with 2..4 record ends (records under 64 B): ids by an
+            // exclusive count over the lanes, four stores per lane
+            const uint32_t n = __builtin_popcount(m);
+            const uint32_t ex = wave_incl_sum(n) - n;
+            uint32_t mm = m;
 #pragma unroll
-            for (int i = 0; i < NR; ++i) pre[i] = 0;
-        }
-#pragma unroll
-        for (int i = 0; i < NR; ++i) {
-            const uint32_t j = j0 + i;
-            // blocks of this slab holding a record end (the plan is zero past
-            // the last row)
-            const uint32_t m = (nib >> (4 * i)) & 15u;
-            const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
-            // the register at the start of block b (selects, no branches)
-            auto cap = [&](uint32_t b) {
-                uint32_t v = b == 3 ? c3[i] : c2[i];
-                v = b == 1 ? c1[i] : v;
-                return b == 0 ? 0u : v;
-            };
-            if constexpr ((MODE & 16) != 0) {
-                asm volatile("" ::"v"(m), "v"(pre[i]), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
-            } else if (GCK_EPACC) {
-                // the row's ends in slot order (lane, then block), each into
-                // lane acc_n of the accumulator: a uniform loop over the
-                // lanes with ends (about 1.2 per row on C3)
-                (void)ra;
-                // each lane's first end's capture, selected on the vector unit
-                const uint32_t cap0 = cap((uint32_t)__builtin_ctz(m | 16u));
-                auto push = [&](uint32_t cv, uint32_t pv) {
-                    if (acc_n == 64) acc_flush();
-                    acc_c = lane == acc_n ? cv : acc_c;
-                    acc_p = lane == acc_n ? pv : acc_p;
-                    ++acc_n;
-                };
-                uint64_t C = __ballot(m != 0);
-                while (C) {
-                    const int L = __builtin_ctzll(C);
-                    C &= C - 1;
-                    const uint32_t mL = (uint32_t)__builtin_amdgcn_readlane((int)m, L);
-                    const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)pre[i], L);
-                    push((uint32_t)__builtin_amdgcn_readlane((int)cap0, L), pv);
-                    if (mL & (mL - 1)) {  // rare: a slab with 2..4 ends (records under 64 B)
-                        const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)c1[i], L);
-                        const uint32_t v2 = (uint32_t)__builtin_amdgcn_readlane((int)c2[i], L);
-                        const uint32_t v3 = (uint32_t)__builtin_amdgcn_readlane((int)c3[i], L);
-                        for (uint32_t mm = mL & (mL - 1); mm; mm &= mm - 1) {
-                            const uint32_t b = (uint32_t)__builtin_ctz(mm);
-                            push(b == 1 ? v1 : b == 2 ? v2 : v3, pv);
-                        }
-                    }
-                }
-            } else if (__ballot(m & (m - 1)) == 0) {
-                // common case: at most one record end per slab, its slot is
-                // ra + (cut lanes before)
-                const uint64_t C = __ballot(m != 0);
-                const uint32_t idx =
-                    __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-                store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
-            } else {
-                // a slab with 2..4 record ends (records under 64 B): ids by
-                // an exclusive count over the lanes, four stores per lane
-                const uint32_t n = __builtin_popcount(m);
-                const uint32_t ex = wave_incl_sum(n) - n;
-                uint32_t mm = m;
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
-                    mm &= mm - 1;
-                }
+            for (uint32_t q = 0; q < 4; ++q) {
+                store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre);
+                mm &= mm - 1;
             }
-            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P[i], 63);  // F(0, row)
-            rend_buf = lane == j ? total : rend_buf;
         }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);  // F(0, row)
+        rend_buf = lane == j ? total : rend_buf;
     };
 
-    // prologue: this wave's first two blocks, the first plan
+    // prologue: this wave's first two blocks, their plans, the first batch
     uint64_t q = grab();
     if (q >= n_blocks) return;
     uint64_t qn = grab();
     Plan pc, pn;
-    load_plan(q, pc);
-#if GCK_SPLAN == 2
     Batch bc, bn;
+    load_plan(q, pc);
     load_plan(qn, pn);
     load_batch(pc, bc);
-#endif
-    // kPrefetch rows in flight per wavefront (row buffers rotate with period
-    // NB, which divides the 4 steps of a quad, so every buffer has fixed
-    // registers)
-    static_assert(kPrefetch == 1 || (NR == 1 && kPrefetch <= 3), "prefetch depth > 1 needs one row per step");
-    constexpr int NB = kPrefetch == 1 ? 2 : 4;
-    RowBuf buf[NB][NR];
-#pragma unroll
-    for (int d = 0; d < kPrefetch; ++d) issue(q * kBlockRows + (uint64_t)d * NR, buf[d]);
+    // one row in flight ahead of the one processed (two buffers alternate, so
+    // each has fixed registers)
+    u32x4 buf[2][4];
+    issue(q * kBlockRows, buf[0]);
     for (;;) {
-        // block q: plan pc is resident; fetch the next block's plan and claim
-        // the one after it (both land during this block)
-#if GCK_SPLAN == 2
-        // pn (block qn) landed during the previous block: its record ends now,
-        // the plan of the block after it next
+        // block q: plan pc and batch bc are resident; pn (block qn) landed
+        // during the previous block: its record ends now, the plan of the
+        // block after it next
         const uint64_t qnn = grab();
         Plan pnn;
         load_batch(pn, bn);
         load_plan(qnn, pnn);
-#else
-        load_plan(qn, pn);
-        const uint64_t qnn = grab();
-#endif
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
-        acc_base = ra0;
-        acc_n = 0;
-#if !GCK_SPLAN
-        const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
-#else
         uint32_t nibs[8];
-#if GCK_SPLAN == 2
-        build_nibs(row_b, ra0, pc.re, &bc, nibs);
-#else
-        (void)load_batch;
-        build_nibs(row_b, ra0, pc.re, nullptr, nibs);
-#endif
-#endif
-        // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
-        // lane; the two row buffers alternate, so each has fixed registers
+        build_nibs(row_b, ra0, pc.re, bc, nibs);
+        // rows in quads: a quad consumes 16 nibble bits per lane
         for (int qd = 0; qd < kSteps / 4; ++qd) {
             // this quad's nibbles (a uniform select: qd is a loop counter)
             uint32_t nib = nibs[0];
 #pragma unroll
             for (int d = 1; d < 8; ++d)
-                if (qd * NR / 2 == d) nib = nibs[d];
-            if constexpr (NR == 1) nib >>= 16 * (qd & 1);
+                if (qd / 2 == d) nib = nibs[d];
+            nib >>= 16 * (qd & 1);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
-                // the rows kPrefetch steps ahead: this block, or the next block's first
-                const int ahead = st + kPrefetch;
-                const uint64_t nrow =
-                    ahead < kSteps ? row_b + (uint64_t)ahead * NR : qn * kBlockRows + (uint64_t)(ahead - kSteps) * NR;
-                issue(nrow, buf[(u + kPrefetch) % NB]);
+                // the next row: this block's, or the next block's first
+                const uint64_t nrow = st + 1 < kSteps ? row_b + (uint64_t)(st + 1) : qn * kBlockRows;
+                issue(nrow, buf[(u + 1) % 2]);
                 // keep the next row's loads here, ahead of this row's compute:
                 // left alone, the scheduler sinks them past most of the chain
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u % NB],
-                        rend_buf);
+                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u % 2], rend_buf);
             }
         }
-        if (GCK_EPACC) acc_flush();
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
         *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
@@ -1343,10 +1105,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         q = qn;
         qn = qnn;
         pc = pn;
-#if GCK_SPLAN == 2
         pn = pnn;
         bc = bn;
-#endif
     }
 }
 
@@ -1436,13 +1196,7 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, con
     return c;
 }
 
-#ifndef GCK_FIN_PIPE
-#define GCK_FIN_PIPE 0
-#endif
-#ifndef GCK_FIN_WPE
-#define GCK_FIN_WPE (GCK_FIN_PIPE ? 3 : 4)
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE))) void k_finalize(const uint8_t *__restrict__ arena,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint2 *__restrict__ rec_kv,
                                                   const uint32_t *__restrict__ rec_file,
@@ -1533,9 +1287,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         g.w0 = g.rs & ~3ull;
         return g;
     };
-#ifndef GCK_FIN_XP
-#define GCK_FIN_XP 0  // ablation (timing only, wrong results): 1 no arena loads, 2 no table loads, 4 no stores, 8 no row sums, 32 no header + key loads
-#endif
     // every load that depends on the record table
     struct Dep {
         uint4 vp, vend;
@@ -1545,15 +1296,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
     };
     auto issue = [&](const Geo &g, Dep &o) {
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + g.w0);
-        o.vp = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)g.rs, (uint32_t)g.bsp, g.V, g.f)
-                                : *reinterpret_cast<const uint4 *>(arena + g.bsp);  // block holding byte rs - 1
+        o.vp = *reinterpret_cast<const uint4 *>(arena + g.bsp);  // block holding byte rs - 1
         // header + keys up to 24 B as three 16 B loads (dword aligned; the
         // arena is padded): every load instruction of a wave touches 64
         // records' lines, so the count of instructions, not bytes, is the cost
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = (GCK_FIN_XP & 33) ? u32x4_a4{(uint32_t)g.rs * (i + 3), 1u, 2u, 3u}
-                                                : reinterpret_cast<const u32x4_a4 *>(wp)[i];
+            const u32x4_a4 v = reinterpret_cast<const u32x4_a4 *>(wp)[i];
             o.pw[4 * i] = v.x;
             o.pw[4 * i + 1] = v.y;
             o.pw[4 * i + 2] = v.z;
@@ -1561,20 +1310,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         }
         o.vend = make_uint4(0, 0, 0, 0);
         if (!g.have)
-            o.vend = (GCK_FIN_XP & 1) ? make_uint4((uint32_t)g.bse, 1, 2, 3) : *reinterpret_cast<const uint4 *>(arena + g.bse);
+            o.vend = *reinterpret_cast<const uint4 *>(arena + g.bse);
         // row sums rend[fr .. fr + 11] the record crosses (three 16 B loads; rend is padded)
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = (GCK_FIN_XP & 8) ? u32x4_a4{(uint32_t)g.fr * 7 + i, 1u, 2u, 3u}
-                                                : reinterpret_cast<const u32x4_a4 *>(rend + g.fr)[i];
+            const u32x4_a4 v = reinterpret_cast<const u32x4_a4 *>(rend + g.fr)[i];
             o.rr[4 * i] = v.x;
             o.rr[4 * i + 1] = v.y;
             o.rr[4 * i + 2] = v.z;
             o.rr[4 * i + 3] = v.w;
         }
-        o.xi = (GCK_FIN_XP & 2) ? g.d * 0x9E3779B9u : xinv[g.d];
-        o.xv0 = (GCK_FIN_XP & 2) ? g.V * 0x85EBCA6Bu : xb[g.V & 0xFFFF];
-        o.xhi = (GCK_FIN_XP & 2) ? (g.V >> 16) + 1 : xa[g.V >> 16];
+        o.xi = xinv[g.d];
+        o.xv0 = xb[g.V & 0xFFFF];
+        o.xhi = xa[g.V >> 16];
         o.cf = carry[g.f];
         o.fb = fbase[g.f];
     };
@@ -1658,38 +1406,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
                 const uint32_t off = k * 1024 + lane * 16;
                 const uint4 v = Ost[off / 16];
                 if (off + 16 <= nbytes) {
-                    if (!(GCK_FIN_XP & 4)) *reinterpret_cast<u32x4_a4 *>(dst + off) = u32x4_a4{v.x, v.y, v.z, v.w};
+                    *reinterpret_cast<u32x4_a4 *>(dst + off) = u32x4_a4{v.x, v.y, v.z, v.w};
                 } else if (off < nbytes) {  // an odd record count ends mid-chunk
-                    if (!(GCK_FIN_XP & 4)) *reinterpret_cast<uint2 *>(dst + off) = make_uint2(v.x, v.y);
+                    *reinterpret_cast<uint2 *>(dst + off) = make_uint2(v.x, v.y);
                 }
             }
             __builtin_amdgcn_wave_barrier();
             n_rej += valid && calc != hcrc;
         }
     };
-    // Software pipeline (GCK_FIN_PIPE): the record table two iterations ahead,
-    // its dependent loads one iteration ahead, so an iteration's compute
-    // overlaps the next one's memory round trip (≈40 more VGPRs: 3 waves/SIMD).
-    // Without it: the table one iteration ahead, the dependent loads issued
-    // together and waited for, then the compute.
+    // The record table one iteration ahead, the loads that depend on it
+    // issued together and waited for, then the compute.  (Loading the table
+    // two iterations ahead and the dependent loads one ahead measured slower:
+    // 0.517-0.520 vs 0.496-0.498 ms)
     uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
     Rec cur, nxt;
     if (base < re) load_rec(base, cur);
-#if GCK_FIN_PIPE
-    Dep dc;
-    if (base < re) issue(geo(cur, base), dc);
-    if (base + G < re) load_rec(base + G, nxt);
-    for (; base < re; base += G) {
-        Dep dn;
-        Rec nn;
-        if (base + G < re) issue(geo(nxt, base + G), dn);
-        if (base + 2 * G < re) load_rec(base + 2 * G, nn);
-        compute(cur, geo(cur, base), dc, base);
-        cur = nxt;
-        nxt = nn;
-        dc = dn;
-    }
-#else
     for (; base < re; base += G) {
         const Geo g = geo(cur, base);
         Dep dc;
@@ -1698,7 +1430,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
         compute(cur, g, dc, base);
         cur = nxt;
     }
-#endif
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
     __shared__ uint32_t blk_rej;
@@ -1708,39 +1439,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GCK_FIN_WPE
     if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&blk_rej, wsum);
     __syncthreads();
     if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[3], blk_rej);
-}
-
-// Measurement variants of k_walk (gck_diag_walk_variant): MODE bit 1 = header
-// by two loads (ld_hdr2; the compiler already merges ld_hdr's), 4 = no stage
-// stores.  Same chains, counts and exits as k_walk.
-struct NoEmit {
-    __device__ void operator()(uint32_t, uint64_t, const Hdr &) const {}
-    __device__ void prime() const {}
-};
-template <int MODE>
-__global__ __launch_bounds__(256) void k_walk_xp(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
-                                                 const uint64_t *__restrict__ flen,
-                                                 const uint32_t *__restrict__ ch_file,
-                                                 const uint64_t *__restrict__ ch_entry,
-                                                 const uint64_t *__restrict__ ch_wend, uint32_t *ch_count,
-                                                 uint64_t *ch_exit, uint2 *s_kv, uint32_t cap,
-                                                 uint32_t n_chunks) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
-    const uint64_t entry = ch_entry[c];
-    if (entry == kNone) return;
-    const uint32_t f = ch_file[c];
-    uint32_t count = 0, term;
-    uint64_t exit = 0, tpos;
-    constexpr bool H2 = (MODE & 1) != 0;
-    if constexpr ((MODE & 4) != 0) {
-        walk_chain<NoEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, NoEmit{}, count, exit, term, tpos);
-    } else {
-        ScratchEmit em{s_kv + stage_slot(c, 0, cap), cap};
-        walk_chain<ScratchEmit, H2>(arena, fbase[f], flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
-    }
-    ch_count[c] = count;
-    ch_exit[c] = exit;
 }
 
 // ------------------------------------------------------------- host side ---
@@ -1866,14 +1564,14 @@ static void ctx_free(Ctx *c) {
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
-                   &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend, &c->d_plan,
+                   &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
                    &c->d_gvoff, &c->d_gvals, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
-                   &c->d_cdata, &c->d_chint};
+                   &c->d_cdata, &c->d_chint, &c->d_cjmp, &c->d_con};
     for (DBuf *b : all) b->release();
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
     c->h_mbox = c->d_mbox = nullptr;
@@ -1935,7 +1633,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(16)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
-        (rc = c->d_plan.ensure(GCK_SPLAN ? 16 : (c->n_rows + kBlockRows) * kPlanRowBytes)) || (rc = c->d_queue.ensure(16)))
+        (rc = c->d_queue.ensure(16)))
         return rc;
     if (nfiles) {
         GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
@@ -2014,9 +1712,7 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
             c->d_fnrec.as<uint64_t>() + f0, f1 - f0);
 }
 
-// Record table of chunks [c0, c1), row index and row plan of rows [r0, r1)
-// (the plan counts blocks from r0).
-
+// Record table of chunks [c0, c1) and row index (row_first) of rows [r0, r1].
 static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
                            const uint64_t *rng, uint64_t cap) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
@@ -2036,10 +1732,6 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
                                              c->d_fnrec.as<uint64_t>(), c->nfiles, c->n_rows, rng,
                                              c->d_row_first.as<uint32_t>());
-    if (r1 > r0 && !GCK_SPLAN)
-        k_row_plan<<<nblk(r1 - r0, kBlockRows * kPlanWaves), 64 * kPlanWaves, 0, s>>>(
-            c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0, r1 - r0, c->d_row_first.as<uint32_t>(),
-            c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16);
 }
 
 // CRC partials of rows [r0, r1) (k_crc_rows).  Record-slot scratch: cap ..
@@ -2050,9 +1742,8 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>();
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
-        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_plan.as<uint4>() + r0 * kPlanRowBytes / 16,
-        c->d_row_first.as<uint32_t>() + r0, cap,
+    k_crc_rows<<<grid, 1024, 0, s>>>(
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0);
     return GCK_OK;
@@ -2768,112 +2459,5 @@ int gck_device_count(void) {
 const char *gck_version(void) { return "gocask_hip 0.1 (gfx950)"; }
 
 const char *gck_last_error(void) { return gck::last_error(); }
-
-// Diagnostic: the speculative entry of every chunk (k_spec_entry again, into
-// a scratch array) next to the final entry of the last run, both copied to
-// host arrays of n_chunks; *n = chunks.
-int gck_diag_spec_entries(gck_ctx *ctx, uint64_t *spec, uint64_t *final_, uint64_t cap, uint64_t *n) {
-    if (!ctx || !n) return GCK_EINVAL;
-    Ctx *c = &ctx->c;
-    *n = c->n_chunks;
-    if (!spec || !final_ || cap < c->n_chunks) return GCK_EINVAL;
-    if (!c->n_chunks) return GCK_OK;
-    GCK_HIP(hipSetDevice(c->device));
-    DBuf tmp;
-    if (tmp.ensure((uint64_t)c->n_chunks * 8)) return GCK_ENOMEM;
-    k_spec_entry<<<nblk(c->n_chunks, 4), 256, 0, c->stream>>>(
-        c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
-        c->d_ch_start.as<uint64_t>(), c->d_ch_end.as<uint64_t>(), tmp.as<uint64_t>(), c->n_chunks, c->opts.max_key,
-        c->opts.spec_window);
-    GCK_HIP(hipMemcpyAsync(spec, tmp.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost, c->stream));
-    GCK_HIP(hipMemcpyAsync(final_, c->d_ch_entry.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost, c->stream));
-    GCK_HIP(hipStreamSynchronize(c->stream));
-    tmp.release();
-    return GCK_OK;
-}
-
-// Measurement helper: time k_walk variants (k_walk_xp MODE) on the chunk
-// entries of the last run; the stage is clobbered (rerun before fetching).
-int gck_diag_walk_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
-    if (!ctx || iters <= 0 || mode < 0 || mode > 7) return GCK_EINVAL;
-    Ctx *c = &ctx->c;
-    if (!c->n_chunks) return GCK_EINVAL;
-    GCK_HIP(hipSetDevice(c->device));
-    hipEvent_t a, b;
-    GCK_HIP(hipEventCreate(&a));
-    GCK_HIP(hipEventCreate(&b));
-    const uint32_t nc = c->n_chunks;
-    GCK_HIP(hipEventRecord(a, c->stream));
-    for (int i = 0; i < iters; ++i) {
-#define GCK_WALK_XP(M)                                                                                             \
-    case M:                                                                                                        \
-        k_walk_xp<M><<<nblk(nc, 256), 256, 0, c->stream>>>(                                                        \
-            c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(), \
-            c->d_ch_entry.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(), c->d_ch_count.as<uint32_t>(),              \
-            c->d_ch_exit.as<uint64_t>(), c->d_stage.as<uint2>(), c->opts.chunk_cap, nc);                         \
-        break;
-        switch (mode) {
-            GCK_WALK_XP(0)
-            GCK_WALK_XP(1)
-            GCK_WALK_XP(2)
-            GCK_WALK_XP(3)
-            GCK_WALK_XP(4)
-            GCK_WALK_XP(5)
-            GCK_WALK_XP(6)
-            GCK_WALK_XP(7)
-        }
-#undef GCK_WALK_XP
-    }
-    GCK_HIP(hipEventRecord(b, c->stream));
-    GCK_HIP(hipEventSynchronize(b));
-    float ms = 0;
-    GCK_HIP(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    *ms_per_iter = ms / iters;
-    return GCK_OK;
-}
-
-// Measurement helper: time ablated variants of k_crc_rows on the state left by
-// the last gck_ctx_run (outputs are clobbered; rerun before fetching).
-// mode bits: 2 = no LDS table chain, 4 = no row shift / wave scan, 8 = no
-// loads (synthetic bytes).
-int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter) {
-    if (!ctx || iters <= 0 || mode < 0 || mode > 255) return GCK_EINVAL;
-    Ctx *c = &ctx->c;
-    if (!c->n_rows || !c->n_recs) return GCK_EINVAL;
-    GCK_HIP(hipSetDevice(c->device));
-    const uint64_t nb = (c->n_rows + kBlockRows - 1) / kBlockRows;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
-    uint32_t *queue = c->d_queue.as<uint32_t>();
-    hipEvent_t a, b;
-    GCK_HIP(hipEventCreate(&a));
-    GCK_HIP(hipEventCreate(&b));
-    GCK_HIP(hipEventRecord(a, c->stream));
-    for (int i = 0; i < iters; ++i) {
-        GCK_HIP(hipMemsetAsync(queue, 0, 4, c->stream));
-#define GCK_VARIANT(M)                                                                                              \
-    case M:                                                                                                         \
-        k_crc_rows<M, kRowsPerStep><<<grid, 1024, 0, c->stream>>>(                                                  \
-            c->arena.as<uint8_t>(), c->n_rows, c->d_plan.as<uint4>(), c->d_row_first.as<uint32_t>(), c->n_recs,      \
-            c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),      \
-            c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), 0); \
-        break;
-        switch (mode) {
-            GCK_VARIANT(0) GCK_VARIANT(2) GCK_VARIANT(4) GCK_VARIANT(6) GCK_VARIANT(8) GCK_VARIANT(12)
-            GCK_VARIANT(16) GCK_VARIANT(22) GCK_VARIANT(32) GCK_VARIANT(86) GCK_VARIANT(128) GCK_VARIANT(150)
-            default: return GCK_EINVAL;
-        }
-#undef GCK_VARIANT
-    }
-    GCK_HIP(hipEventRecord(b, c->stream));
-    GCK_HIP(hipEventSynchronize(b));
-    float ms = 0;
-    GCK_HIP(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    *ms_per_iter = ms / iters;
-    return GCK_OK;
-}
 
 }  // extern "C"

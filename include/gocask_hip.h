@@ -257,28 +257,6 @@ const char *gck_phase_name(int phase);
  * HIP stream the pipeline runs on (hipStream_t, as void*). */
 int gck_ctx_device_recs(gck_ctx *ctx, const gck_rec **recs, uint64_t *n);
 void *gck_ctx_stream(gck_ctx *ctx);
-/* Measurement helper (not on the replay path): time a plain streaming read of
- * the resident arena (16 B per lane, non-temporal loads), the practical HBM
- * read ceiling k_crc_rows is compared to. */
-int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs);
-/* Diagnostic read probes over the arena: 0 = the streaming read with the
- * default cache policy, 15 = with non-temporal loads (gck_diag_stream_read's
- * kernel), 1 = a lane-contiguous 64 B slab layout (lane stride 64 B), 2 = same
- * geometry coalesced, 3..14 = random-access probes. */
-int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs);
-/* Measurement helper: time ablated variants of the CRC kernel on the last run's
- * state (mode bits 2 = no LDS table chain, 4 = no slab shift / wave scan, 8 = no
- * loads, 16 = no record stores, 32 = default cache policy instead of
- * non-temporal loads).  Clobbers the last run's outputs. */
-int gck_diag_crc_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter);
-/* Measurement helper: time variants of the chain walk on the last run's chunk
- * entries (mode bits 1 = header in two loads, 2 = 8-byte stage, 4 = no stage
- * stores).  Clobbers the last run's stage. */
-int gck_diag_walk_variant(gck_ctx *ctx, int mode, int iters, double *ms_per_iter);
-/* Diagnostic: every chunk's speculative entry (recomputed) and its final entry
- * after validation in the last run (host arrays of cap >= chunks; *n = chunks;
- * UINT64_MAX = none). */
-int gck_diag_spec_entries(gck_ctx *ctx, uint64_t *spec, uint64_t *final_, uint64_t cap, uint64_t *n);
 /* Copy `len` bytes of file `file` (as resident in the arena) back to host. */
 int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, uint64_t len);
 

@@ -121,3 +121,60 @@ def test_compact_requires_puts_only(g, orc):
         ctx.keydir(keep_tombstones=True, fetch=False)
         with pytest.raises(Exception):
             ctx.compact(1 << 20)
+
+
+@pytest.mark.parametrize("seed,vmin,max_size", [
+    (81, 0, 64),     # thousands of merged files: the pointer-doubling rotation points
+    (82, 0, 17),     # a file per record
+    (83, 40, 30),    # every record over the limit: an empty first file, then one file per record
+])
+def test_compact_many_files(g, orc, seed, vmin, max_size):
+    rng = np.random.default_rng(seed)
+    ops = []
+    for i in range(3000):
+        k = b"k%d" % int(rng.integers(0, 900))
+        if rng.random() < 0.05:
+            ops.append(orc.tombstone(1_700_000_000 + i, k))
+        else:
+            ops.append(orc.entry(1_700_000_000 + i, k, rng.bytes(int(rng.integers(vmin, vmin + 30)))))
+    files = [np.frombuffer(b"".join(ops), np.uint8)]
+    recs, st = orc.replay(files, [False])
+    assert st["status"] == 0
+    want_d, want_h = orc.compact(files, recs, [False], max_size)
+    assert len(want_d) > 256  # past the one-wavefront search
+    got_d, got_h = _compact(g, files, [False], max_size)
+    assert len(got_d) == len(want_d)
+    assert got_d == want_d
+    assert got_h == want_h
+
+
+def test_compact_refuses_stale_keydir(g, orc):
+    # a run invalidates the keydir: compacting without a fresh gck_ctx_keydir
+    # would merge nothing and report success
+    _, files, reset = load_case(case_names()[0])
+    with g.ReplayContext() as ctx:
+        ctx.load(files, reset)
+        ctx.run()
+        ctx.keydir(fetch=False)
+        ctx.compact(1 << 20)  # fresh keydir: fine
+        ctx.run()
+        with pytest.raises(g._lib.GckError) as e:
+            ctx.compact(1 << 20)
+        assert e.value.code == g._lib.GCK_EINVAL
+
+
+def test_compact_refuses_startup_error(g, orc):
+    # the reference refuses to open a database whose replay hit a startup
+    # error (core/db.go:134-138): there is no keydir to merge
+    good = orc.entry(1, b"user", b"alice")
+    bad = good + orc.entry(2, b"key", b"value")[:17]  # header + 1 of 3 key bytes: ErrUnexpectedEOF
+    files = [np.frombuffer(bad, np.uint8)]
+    _, st = orc.replay(files, [False])
+    assert st["status"] == 1
+    with g.ReplayContext() as ctx:
+        ctx.load(files, [False])
+        assert ctx.run() == 1
+        ctx.keydir(fetch=False)
+        with pytest.raises(g._lib.GckError) as e:
+            ctx.compact(1 << 20)
+        assert e.value.code == g._lib.GCK_EINVAL

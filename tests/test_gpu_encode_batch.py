@@ -76,3 +76,48 @@ def test_encode_batch_replays():
     assert len(recs) == len(orecs) == len(ops)
     assert (recs == orecs).all()
     assert st["n_crc_fail"] == 0
+
+
+def _raw_encode(keys_t, koff, vals_t, voff, ts, tomb, out, out_off):
+    import ctypes
+
+    from gocask_amd import _lib
+
+    total = ctypes.c_uint64(0)
+    return _lib.load().gck_encode_batch(keys_t.data_ptr(), koff.data_ptr(), vals_t.data_ptr(), voff.data_ptr(),
+                                        ts.data_ptr(), tomb.data_ptr(), len(ts), out.data_ptr(), out.numel(),
+                                        out_off.data_ptr(), ctypes.byref(total), None), total.value
+
+
+def test_encode_batch_exact_size_and_alignment():
+    """Exact-size blobs (no padding) encode correctly; blobs that do not start
+    on a 4-byte boundary are refused (the kernel reads dwords)."""
+    import torch
+
+    from gocask_amd import _lib
+
+    ops = [(11, b"abc", b"12345"), (12, b"k" * 37, bytes(range(200)) * 3), (13, b"z", None), (14, b"tail", b"x" * 4097)]
+    keys = b"".join(k for _, k, _ in ops)
+    vals = b"".join(v for _, _, v in ops if v is not None)
+    koff = np.cumsum([0] + [len(k) for _, k, _ in ops]).astype(np.int64)
+    voff = np.cumsum([0] + [0 if v is None else len(v) for _, _, v in ops]).astype(np.int64)
+
+    def dev(b, extra_front=0):
+        t = torch.empty(len(b) + extra_front, dtype=torch.uint8, device="cuda")
+        t[extra_front:] = torch.frombuffer(bytearray(b), dtype=torch.uint8).cuda()
+        return t[extra_front:]
+
+    d_koff, d_voff = torch.from_numpy(koff).cuda(), torch.from_numpy(voff).cuda()
+    ts = torch.tensor([t for t, _, _ in ops], dtype=torch.int32, device="cuda")
+    tomb = torch.tensor([v is None for _, _, v in ops], dtype=torch.uint8, device="cuda")
+    need = sum(16 + len(k) + (0 if v is None else len(v)) for _, k, v in ops)
+    out = torch.zeros(need, dtype=torch.uint8, device="cuda")
+    out_off = torch.zeros(len(ops) + 1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    rc, total = _raw_encode(dev(keys), d_koff, dev(vals), d_voff, ts, tomb, out, out_off)
+    assert rc == _lib.GCK_OK and total == need
+    assert bytes(out.cpu().numpy()) == _expected(ops)
+    rc, _ = _raw_encode(dev(keys, 1), d_koff, dev(vals), d_voff, ts, tomb, out, out_off)
+    assert rc == _lib.GCK_EINVAL
+    rc, _ = _raw_encode(dev(keys), d_koff, dev(vals, 3), d_voff, ts, tomb, out, out_off)
+    assert rc == _lib.GCK_EINVAL

@@ -11,7 +11,7 @@ for _ in range(3):
 out = {"phase_ms": ctx.stats()["ms_phase"]}
 ms, gh = ctypes.c_double(), ctypes.c_double()
 for pat in range(3, 15):
-    g._lib.check(ctx._L.gck_diag_stream_pattern(ctx._h, pat, 3, ctypes.byref(ms), ctypes.byref(gh)))
+    g._lib.check(g._lib.load_diag().gck_diag_stream_pattern(ctx._h, pat, 3, ctypes.byref(ms), ctypes.byref(gh)))
     kind = "dep" if pat < 9 else "indep"
     out[f"{kind}_{8 << ((pat - 3) % 6)}Ki"] = dict(ms=round(ms.value, 3), ghops=round(gh.value, 2))
 print(json.dumps(out))
