@@ -27,6 +27,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 GiB = 1 << 30
+C4_KEYS_PER_FILE = 312_500  # C4's key universe = this x the corpus's files
 CONFIGS = {
     # BASELINE.json configs[]: C1 CPU plumbing, C2 8 GiB fixed 4 KiB, C3 32 GiB Zipf, C5 = C3 + 1% flips
     "c1": dict(seed=1, val_fixed=1024, key_min=16, key_max=16, max_file_size=64 << 20, n_files=1),
@@ -36,10 +37,12 @@ CONFIGS = {
     "c5": dict(seed=3, val_fixed=0, key_min=8, key_max=24, key_universe=5_000_000, tomb_permille=10,
                flip_permille=10, max_file_size=2 << 30, n_files=16),
     # C4: one corpus of 16 x N files (8 GPUs: 128 x 2 GiB = 256 GiB), file n a
-    # one-file C3-spec corpus with seed 4 + n, cut into N
-    # contiguous walk-order shards (gocask_amd.shard.c4_file_ids)
-    "c4": dict(seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=312_500, tomb_permille=10,
-               max_file_size=2 << 30, n_files=1),
+    # one-file C3-spec corpus (ops, values, deletes from seed 4 + n; SURVEY.md
+    # §8d) whose keys come from ONE corpus-wide universe (key_seed 4, 50 % of
+    # the records as C3: 312,500 ids per file), so keys repeat across files and
+    # shards; cut into N contiguous walk-order shards (shard.c4_file_ids)
+    "c4": dict(seed=4, key_seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=C4_KEYS_PER_FILE,
+               tomb_permille=10, max_file_size=2 << 30, n_files=1),
 }
 C4_FILES_PER_GPU = 16
 DESCR = {
@@ -47,7 +50,7 @@ DESCR = {
     "c2": "C2: 1 x 8 GiB file, 16 B keys, 4 KiB values",
     "c3": "C3: 32 GiB = 16 x 2 GiB rotated files, 8-24 B keys, Zipf(1.1) 64 B-64 KiB values, 1% tombstones",
     "c5": "C5: C3 + 1% single-bit flips in values",
-    "c4": "C4: {n} x 2 GiB files (per-file seed 4+n, C3 spec), one corpus cut into {g} contiguous walk-order shards",
+    "c4": "C4: {n} x 2 GiB files (C3 spec, per-file seed 4+n, one corpus-wide key universe), one corpus cut into {g} contiguous walk-order shards",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -236,6 +239,16 @@ def shard_config(cfg_name, rank):
     return cfg
 
 
+def c4_spec(world, rank, files_per_rank=C4_FILES_PER_GPU):
+    """(file ids, last_is_active, kw) of rank's C4 shard: the corpus has
+    files_per_rank x world files, its key universe C4_KEYS_PER_FILE per file."""
+    from gocask_amd import shard
+
+    ids, last_active = shard.c4_file_ids(world, rank, files_per_rank)
+    kw = dict(CONFIGS["c4"], key_universe=C4_KEYS_PER_FILE * files_per_rank * world)
+    return ids, last_active, kw
+
+
 def encode_workload(ctx, cfg_name, world, rank):
     """Encode this rank's files into its context.  C4: the rank's contiguous
     walk-order range of the one global corpus (no data-path collective: the
@@ -243,8 +256,8 @@ def encode_workload(ctx, cfg_name, world, rank):
     if cfg_name == "c4":
         from gocask_amd import shard
 
-        ids, last_active = shard.c4_file_ids(world, rank, C4_FILES_PER_GPU)
-        return ctx.encode_files(ids, last_is_active=last_active, **CONFIGS["c4"])
+        ids, last_active, kw = c4_spec(world, rank)
+        return ctx.encode_files(ids, last_is_active=last_active, **kw)
     return ctx.encode(**shard_config(cfg_name, rank))
 
 

@@ -123,6 +123,7 @@ class GckCorpusCfg(ctypes.Structure):
         ("tomb_permille", ctypes.c_uint32),
         ("flip_permille", ctypes.c_uint32),
         ("ts_base", ctypes.c_uint32),
+        ("key_seed", ctypes.c_uint64),
     ]
 
 

@@ -305,7 +305,7 @@ class ReplayContext:
         """Encode a synthetic corpus on the device (gck_encode_corpus)."""
         c = GckCorpusCfg()
         d = dict(seed=1, max_file_size=64 * MB, n_ops=0, n_files=1, key_min=16, key_max=16, key_universe=0,
-                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000)
+                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000, key_seed=0)
         d.update(kw)
         for k, v in d.items():
             setattr(c, k, v)
@@ -323,7 +323,7 @@ class ReplayContext:
         (walk) order, into the arena (gck_encode_files): BASELINE C4's shards."""
         c = GckCorpusCfg()
         d = dict(seed=1, max_file_size=64 * MB, n_ops=0, n_files=1, key_min=16, key_max=16, key_universe=0,
-                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000)
+                 val_fixed=1024, tomb_permille=0, flip_permille=0, ts_base=1700000000, key_seed=0)
         d.update(kw)
         for k, v in d.items():
             setattr(c, k, v)

@@ -55,7 +55,7 @@ struct OpDesc {
 // One lane per op: key, value (generated, CRC'd on the fly, optionally one bit
 // flipped after the CRC), then the header.
 __global__ __launch_bounds__(256) void k_encode(uint8_t *__restrict__ arena, const OpDesc *__restrict__ ops,
-                                                uint64_t n_ops, uint64_t seed, uint32_t ts_base,
+                                                uint64_t n_ops, uint64_t seed, uint64_t kseed, uint32_t ts_base,
                                                 uint32_t flip_permille) {
     __shared__ uint32_t T[256];
     for (uint32_t n = threadIdx.x; n < 256; n += blockDim.x) {
@@ -71,10 +71,10 @@ __global__ __launch_bounds__(256) void k_encode(uint8_t *__restrict__ arena, con
     const uint32_t klen = o.klen & 0x7FFFFFFFu, vlen = o.vlen;
     uint8_t *p = arena + o.dst;
     uint8_t *key = p + 16;
-    const uint64_t w0 = mix64(o.keyid ^ H(seed, 7, 0));
+    const uint64_t w0 = mix64(o.keyid ^ H(kseed, 7, 0));
     uint32_t kc = 0xFFFFFFFFu;
     for (uint32_t j = 0; j < klen; ++j) {
-        const uint64_t w = j < 8 ? w0 : H(seed, 8, o.keyid * 64 + j / 8);
+        const uint64_t w = j < 8 ? w0 : H(kseed, 8, o.keyid * 64 + j / 8);
         const uint8_t b = (uint8_t)(w >> (8 * (j % 8)));
         key[j] = b;
         kc = T[(kc ^ b) & 0xff] ^ (kc >> 8);
@@ -111,23 +111,28 @@ __global__ __launch_bounds__(256) void k_encode(uint8_t *__restrict__ arena, con
 }
 
 // Host plan: op sizes from the spec, greedy rotation, lexical walk order.
-static int plan(const gck_corpus_cfg *cfg, std::vector<OpDesc> &ops, std::vector<uint32_t> &op_file,
+// Keys: from cfg->seed, or with key_seed from one universe shared by the
+// per-file corpora of gck_encode_files (kfile = the file's id).
+static uint64_t key_seed_of(const gck_corpus_cfg *cfg) { return cfg->key_seed ? cfg->key_seed : cfg->seed; }
+static int plan(const gck_corpus_cfg *cfg, uint64_t kfile, std::vector<OpDesc> &ops, std::vector<uint32_t> &op_file,
                 std::vector<uint64_t> &sizes) {
     if (cfg->key_min < 8 || cfg->key_max > 512 || cfg->key_max < cfg->key_min) return GCK_EINVAL;
     if (!cfg->n_ops && !cfg->n_files) return GCK_EINVAL;
     if (!cfg->val_fixed && cfg->max_file_size == 0) return GCK_EINVAL;
     if (cfg->val_fixed >= (1u << 23)) return GCK_EINVAL;
     const auto &thr = zipf_thr();
+    const uint64_t kseed = key_seed_of(cfg);
     uint32_t cur = 0;
     uint64_t size = 0;
     sizes.clear();
     for (uint64_t i = 0;; ++i) {
         if (cfg->n_ops && i >= cfg->n_ops) break;
         const bool tomb = cfg->tomb_permille && (H(cfg->seed, 3, i) % 1000u) < cfg->tomb_permille;
-        const uint64_t keyid = cfg->key_universe ? H(cfg->seed, 1, i) % cfg->key_universe : i;
+        const uint64_t kidx = cfg->key_seed ? (kfile << 32 | i) : i;
+        const uint64_t keyid = cfg->key_universe ? H(kseed, 1, kidx) % cfg->key_universe : kidx;
         const uint32_t klen =
             cfg->key_min +
-            (cfg->key_max > cfg->key_min ? (uint32_t)(H(cfg->seed, 6, keyid) % (cfg->key_max - cfg->key_min + 1)) : 0);
+            (cfg->key_max > cfg->key_min ? (uint32_t)(H(kseed, 6, keyid) % (cfg->key_max - cfg->key_min + 1)) : 0);
         const uint32_t vlen =
             tomb ? klen : (cfg->val_fixed ? cfg->val_fixed : 63u + zipf_sample(thr, (uint32_t)(H(cfg->seed, 2, i) >> 32)));
         const uint64_t entry = 16ull + (tomb ? 0 : klen) + vlen;
@@ -168,7 +173,7 @@ int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files
     std::vector<OpDesc> ops;
     std::vector<uint32_t> op_file;
     std::vector<uint64_t> sizes;
-    int rc = plan(cfg, ops, op_file, sizes);
+    int rc = plan(cfg, 0, ops, op_file, sizes);
     if (rc) return rc;
     const uint32_t nf = (uint32_t)sizes.size();
     // walk order = names sorted bytewise (filepath.Walk)
@@ -196,7 +201,7 @@ int gck_encode_corpus(gck_ctx *ctx, const gck_corpus_cfg *cfg, uint32_t *n_files
     if (!ops.empty()) {
         const uint32_t grid = (uint32_t)((ops.size() + 255) / 256);
         k_encode<<<grid, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), d_ops.as<OpDesc>(), ops.size(), cfg->seed,
-                                             cfg->ts_base, cfg->flip_permille);
+                                             key_seed_of(cfg), cfg->ts_base, cfg->flip_permille);
         GCK_HIP(hipGetLastError());
     }
     GCK_HIP(hipStreamSynchronize(c->stream));
@@ -222,7 +227,7 @@ int gck_encode_files(gck_ctx *ctx, const gck_corpus_cfg *cfg, const uint32_t *fi
         one.n_ops = 0;
         std::vector<uint32_t> op_file;
         std::vector<uint64_t> sizes;
-        const int rc = plan(&one, ops[k], op_file, sizes);
+        const int rc = plan(&one, file_ids[k], ops[k], op_file, sizes);
         if (rc) return rc;
         lens[k] = sizes[0];
         reset[k] = (last_is_active && k + 1 == n) ? 0 : 1;
@@ -238,7 +243,8 @@ int gck_encode_files(gck_ctx *ctx, const gck_corpus_cfg *cfg, const uint32_t *fi
         GCK_HIP(hipMemcpy(d_ops.p, ops[k].data(), ops[k].size() * sizeof(OpDesc), hipMemcpyHostToDevice));
         const uint32_t grid = (uint32_t)((ops[k].size() + 255) / 256);
         k_encode<<<grid, 256, 0, c->stream>>>(c->arena.as<uint8_t>(), d_ops.as<OpDesc>(), ops[k].size(),
-                                             cfg->seed + file_ids[k], cfg->ts_base, cfg->flip_permille);
+                                             cfg->seed + file_ids[k], cfg->key_seed ? cfg->key_seed : cfg->seed + file_ids[k],
+                                             cfg->ts_base, cfg->flip_permille);
         GCK_HIP(hipGetLastError());
         GCK_HIP(hipStreamSynchronize(c->stream));  // d_ops is reused by the next file
     }

@@ -275,6 +275,12 @@ typedef struct gck_corpus_cfg {
     uint32_t tomb_permille;
     uint32_t flip_permille; /* single-bit flips inside values, after the CRC     */
     uint32_t ts_base;
+    uint64_t key_seed;      /* 0: key ids, lengths and bytes from seed (op i:    */
+                            /* key id H(seed, 1, i)); else from key_seed, op i   */
+                            /* of file id f drawing H(key_seed, 1, f << 32 | i): */
+                            /* one key universe across gck_encode_files' per-   */
+                            /* file corpora (BASELINE C4; f = 0 in               */
+                            /* gck_encode_corpus)                                */
 } gck_corpus_cfg;
 
 /* Plan the corpus (host) and encode it straight into the context's device arena.

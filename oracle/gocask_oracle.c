@@ -407,11 +407,14 @@ typedef struct {
     uint64_t entry;
 } op_t;
 
+static uint64_t kseed(const orc_corpus_cfg *c) { return c->key_seed ? c->key_seed : c->seed; }
+
 static void op_describe(const orc_corpus_cfg *c, uint64_t i, op_t *o) {
+    const uint64_t kidx = c->key_seed ? ((uint64_t)c->key_file << 32 | i) : i;
     o->tomb = c->tomb_permille && (H(c->seed, 3, i) % 1000u) < c->tomb_permille;
-    o->keyid = c->key_universe ? H(c->seed, 1, i) % c->key_universe : i;
+    o->keyid = c->key_universe ? H(kseed(c), 1, kidx) % c->key_universe : kidx;
     o->klen = c->key_min + (c->key_max > c->key_min
-                                ? (uint32_t)(H(c->seed, 6, o->keyid) % (c->key_max - c->key_min + 1))
+                                ? (uint32_t)(H(kseed(c), 6, o->keyid) % (c->key_max - c->key_min + 1))
                                 : 0);
     if (o->tomb) o->vlen = o->klen;
     else o->vlen = c->val_fixed ? c->val_fixed : 63u + zipf_sample((uint32_t)(H(c->seed, 2, i) >> 32));
@@ -419,9 +422,9 @@ static void op_describe(const orc_corpus_cfg *c, uint64_t i, op_t *o) {
 }
 
 static void key_bytes(const orc_corpus_cfg *c, uint64_t keyid, uint32_t klen, uint8_t *k) {
-    uint64_t w0 = mix64(keyid ^ H(c->seed, 7, 0));
+    uint64_t w0 = mix64(keyid ^ H(kseed(c), 7, 0));
     for (uint32_t j = 0; j < klen; j++) {
-        uint64_t w = j < 8 ? w0 : H(c->seed, 8, keyid * 64 + j / 8);
+        uint64_t w = j < 8 ? w0 : H(kseed(c), 8, keyid * 64 + j / 8);
         k[j] = (uint8_t)(w >> (8 * (j % 8)));
     }
 }

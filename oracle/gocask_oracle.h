@@ -98,6 +98,11 @@ typedef struct {
     uint32_t tomb_permille;
     uint32_t flip_permille;
     uint32_t ts_base;
+    uint64_t key_seed;        /* 0: keys from seed; else key ids / lengths /  */
+                              /* bytes from key_seed, op i drawing key id     */
+                              /* H(key_seed, 1, key_file << 32 | i)           */
+    uint32_t key_file;        /* the file id of a per-file corpus (C4)        */
+    uint32_t pad_;
 } orc_corpus_cfg;
 
 /* Dry run: number of ops and per-file sizes (creation order). */

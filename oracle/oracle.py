@@ -67,6 +67,9 @@ class CorpusCfg(ctypes.Structure):
         ("tomb_permille", ctypes.c_uint32),
         ("flip_permille", ctypes.c_uint32),
         ("ts_base", ctypes.c_uint32),
+        ("key_seed", ctypes.c_uint64),
+        ("key_file", ctypes.c_uint32),
+        ("pad_", ctypes.c_uint32),
     ]
 
 
@@ -183,7 +186,7 @@ def corpus_cfg(**kw) -> CorpusCfg:
     c = CorpusCfg()
     defaults = dict(seed=1, max_file_size=64 << 20, n_ops=0, n_files=1, key_min=16, key_max=16,
                     key_universe=0, val_fixed=1024, tomb_permille=0, flip_permille=0,
-                    ts_base=1700000000)
+                    ts_base=1700000000, key_seed=0, key_file=0)
     defaults.update(kw)
     for k, v in defaults.items():
         setattr(c, k, v)

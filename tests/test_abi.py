@@ -61,7 +61,7 @@ def test_abi_struct_layouts():
     assert L.REC_DTYPE.itemsize == 40
     assert ctypes.sizeof(L.GckFile) == 24
     assert ctypes.sizeof(L.GckResult) == 48
-    assert ctypes.sizeof(L.GckCorpusCfg) == 64
+    assert ctypes.sizeof(L.GckCorpusCfg) == 72
 
 
 def test_encoder_zipf_table_matches_oracle(lib, orc):

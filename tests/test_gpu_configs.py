@@ -119,3 +119,93 @@ def test_config3_full_32gib(g, orc):
 
 def test_config5_full_32gib_reject_set(g, orc):
     _check_full(g, orc, "c5")
+
+
+def test_config4_last_rank_shard_16x2gib(g, orc):
+    """BASELINE C4 at full size on one GPU: the shard bench.py's rank 7 replays
+    at N = 8 (16 x 2 GiB of the 128-file corpus, its last file the active one),
+    with the corpus-wide key universe (keys repeat across files: the keydir is
+    built across files, core/keydir.go:22-49).  Checked by the spec's
+    properties (as C3, per file; key lengths from the shared key ids), the
+    active file against the oracle field for field, and the keydir merge over a
+    one-rank RCCL group against the last writer of every key id."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from gocask_amd import shard
+
+    world, rank = 8, 7
+    ids, last_active, kw = bench.c4_spec(world, rank)
+    assert last_active and len(ids) == 16 and kw["key_seed"] == 4
+    U = kw["key_universe"]
+    assert U == 312_500 * 128
+    base = rank * 16  # the files of lower ranks (shard.file_base at N = 8)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        with g.ReplayContext() as ctx:
+            info = ctx.encode_files(ids, last_is_active=True, **kw)
+            ctx.run()
+            got, st = ctx.fetch()
+            stats = ctx.stats()
+            n_live, ph = shard.merge_keydir(ctx, dist, base)
+            ents, _ = ctx.kd_fetch_merged()
+    finally:
+        dist.destroy_process_group()
+    nf = len(ids)
+    sizes = [int(x) for x in info["sizes"]]
+    assert sum(sizes) > 31 << 30
+    assert st["status"] == 0 and len(got) == info["n_ops"] and stats["n_crc_fail"] == 0
+    assert st["final_last_offset"] == sizes[-1] % (1 << 32)  # the active file does not reset
+    fidx = got["file"].astype(np.int64)
+    assert (np.diff(fidx) >= 0).all() and fidx[0] == 0 and fidx[-1] == nf - 1
+    tomb = (got["flags"] & 1) == 1
+    off = got["rec_off"].astype(np.uint64)
+    klen = got["key_len"].astype(np.uint64)
+    vsz = got["value_size"].astype(np.uint64)
+    ent = np.uint64(16) + klen + np.where(tomb, np.uint64(0), vsz)
+    ks = np.where(tomb, np.uint64(0), klen)
+    assert np.array_equal(got["value_pos"], ((off + np.uint64(16) + ks) % np.uint64(1 << 32)).astype(np.uint32))
+    assert ((got["flags"] & 2) == 2).all() and np.array_equal(got["crc_calc"], got["crc"])
+    bounds = np.searchsorted(fidx, np.arange(nf + 1))
+    keyid = np.zeros(len(got), dtype=np.uint64)
+    for w, n in enumerate(ids):
+        a, b = bounds[w], bounds[w + 1]
+        assert b > a and off[a] == 0
+        assert np.array_equal(off[a + 1:b], off[a:b - 1] + ent[a:b - 1]), w
+        assert int(off[b - 1] + ent[b - 1]) == sizes[w], w
+        ops = got["ts"][a:b].astype(np.uint64) - np.uint64(TS0)
+        assert np.array_equal(ops, np.arange(b - a, dtype=np.uint64)), w  # op i of the file, in order
+        assert np.array_equal(tomb[a:b], (spec.H(4 + n, 3, ops) % np.uint64(1000)) < np.uint64(kw["tomb_permille"]))
+        # keys from the corpus-wide universe: op i of file n draws key id
+        # H(4, 1, n << 32 | i) % U, its length key_min + H(4, 6, id) % 17
+        keyid[a:b] = spec.H(4, 1, (np.uint64(n) << np.uint64(32)) | ops) % np.uint64(U)
+    want_len = np.uint64(kw["key_min"]) + spec.H(4, 6, keyid) % np.uint64(kw["key_max"] - kw["key_min"] + 1)
+    assert np.array_equal(klen, want_len)
+    # keys repeat across the shard's files
+    first = np.unique(keyid, return_index=True)[1]
+    last_rev = np.unique(keyid[::-1], return_index=True)[1]
+    last = len(keyid) - 1 - last_rev
+    assert (fidx[last] != fidx[first]).sum() > 100_000
+    # the merged keydir = the last record of every key id, kept if a Put
+    live = last[~tomb[last]]
+    assert n_live == len(ents) == len(live)
+    got_pairs = np.sort(ents["rec"]["file"].astype(np.uint64) << np.uint64(40) | ents["rec"]["rec_off"].astype(np.uint64))
+    want_pairs = np.sort((fidx[live].astype(np.uint64) + np.uint64(base)) << np.uint64(40) | off[live])
+    assert np.array_equal(got_pairs, want_pairs)
+    assert ph["status"]["status"] == 0
+    # the active file (2 GiB) against the oracle, field for field
+    n = ids[-1]
+    files, _ = orc.gen_corpus(**{**kw, "seed": 4 + n, "key_file": n})
+    assert len(files[0]) == sizes[-1]
+    want, wst = orc.replay(files, [False])
+    a = bounds[nf - 1]
+    assert wst["status"] == 0 and len(want) == len(got) - a
+    for f in FIELDS:
+        w = want[f] + (nf - 1 if f == "file" else 0)
+        assert np.array_equal(got[f][a:], w), f

@@ -368,16 +368,18 @@ def test_sharded_keys_in_order_never_cuts_after_the_active_file(g, orc, world):
     assert int(kd[b"foobar"]["value_pos"]) == 66
 
 
-def test_encode_files_matches_oracle_one_file_corpora(g, orc):
-    # BASELINE C4's generator: file n is a one-file corpus with seed + n
+@pytest.mark.parametrize("key_seed", [0, 4])
+def test_encode_files_matches_oracle_one_file_corpora(g, orc, key_seed):
+    # BASELINE C4's generator: file n is a one-file corpus with seed + n; with
+    # key_seed its keys come from one universe shared by all files
     kw = dict(seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=2000, tomb_permille=10, flip_permille=10,
-              max_file_size=1 << 20, n_files=1)
+              max_file_size=1 << 20, n_files=1, key_seed=key_seed)
     ids = [3, 0, 11]
     with g.ReplayContext() as ctx:
         info = ctx.encode_files(ids, last_is_active=True, **kw)
         files = []
         for k, n in enumerate(ids):
-            want_f, want_names = orc.gen_corpus(**{**kw, "seed": 4 + n})
+            want_f, want_names = orc.gen_corpus(**{**kw, "seed": 4 + n, "key_file": n})
             assert len(want_f) == 1 and int(info["sizes"][k]) == len(want_f[0])
             got = ctx.read_file(k, 0, len(want_f[0]))
             assert np.array_equal(got, want_f[0]), n
@@ -389,3 +391,58 @@ def test_encode_files_matches_oracle_one_file_corpora(g, orc):
     for f in FIELDS:
         assert np.array_equal(recs[f], want[f]), f
     assert st["final_last_offset"] == wst["final_last_offset"] == len(files[-1])
+
+
+def _c4_files(orc, world, files_per_rank, universe, max_file_size, tomb_permille=10):
+    """The C4 corpus spec (bench.py CONFIGS["c4"]: per-file seed 4 + n, keys
+    from one universe with key_seed 4) at a small file size: (files in walk
+    order, reset flags, shard ranges) for `world` ranks."""
+    from gocask_amd import shard
+
+    kw = dict(seed=4, key_seed=4, val_fixed=0, key_min=8, key_max=24, key_universe=universe,
+              tomb_permille=tomb_permille, max_file_size=max_file_size, n_files=1)
+    wf, ranges = [], []
+    for r in range(world):
+        ids, _ = shard.c4_file_ids(world, r, files_per_rank)
+        ranges.append((len(wf), len(wf) + len(ids)))
+        for n in ids:
+            f, _ = orc.gen_corpus(**{**kw, "seed": 4 + n, "key_file": n})
+            wf.append(f[0])
+    reset = [i + 1 < len(wf) for i in range(len(wf))]
+    return wf, reset, ranges
+
+
+@pytest.mark.parametrize("tomb_permille", [10, 150])
+def test_merge_c4_keys_shared_across_shards(g, orc, tomb_permille):
+    """C4 key density (a universe of half the records, shared by every file):
+    later shards overwrite and delete keys of earlier ones, and the merged
+    keydir equals keyDir.set / unset over all files in walk order
+    (core/keydir.go:22-49)."""
+    import torch
+
+    wf, reset, ranges = _c4_files(orc, 4, 2, universe=1200, max_file_size=1 << 20, tomb_permille=tomb_permille)
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] == 0
+    assert 1500 < len(want) < 4000  # the universe is about half the records
+    shard_of_file = [s for s, (a, b) in enumerate(ranges) for _ in range(a, b)]
+    # keys cross shards: some key's last word (a Put or a Delete) comes from a
+    # later shard than one of its earlier Puts
+    first_put, crosses, deletes_across = {}, 0, 0
+    for r in want:
+        o = int(r["rec_off"]) + 16
+        key = bytes(wf[int(r["file"])][o:o + int(r["key_len"])])
+        s = shard_of_file[int(r["file"])]
+        if key in first_put and first_put[key] < s:
+            crosses += 1
+            deletes_across += int(r["flags"]) & 1
+        if not int(r["flags"]) & 1:
+            first_put.setdefault(key, s)
+    assert crosses > 100 and deletes_across > 0, (crosses, deletes_across)
+    shards = [(wf[a:b], reset[a:b]) for a, b in ranges]
+    packed = _pack_shards(g, torch, shards, 4)
+    try:
+        owners = [_merge_owner(torch, packed, p, packed[p][0]) for p in range(4)]
+    finally:
+        for c, *_ in packed:
+            c.close()
+    _check_merged(wf, owners, _global_keydir(wf, want), 4, shard_of_file)
