@@ -63,6 +63,8 @@ typedef struct {
 uint32_t orc_crc32(const uint8_t *p, uint64_t n);
 /* Same result, slicing-by-8 (used by the timed CPU baseline). */
 uint32_t orc_crc32_fast(const uint8_t *p, uint64_t n);
+/* Go's amd64 speed class: PCLMULQDQ folding for >= 64 bytes (cpu baseline). */
+uint32_t orc_crc32_clmul(const uint8_t *p, uint64_t n);
 
 /* Replay the files in walk order.  verify_crc computes the per-record verdict
  * (the core/db.go:311 rule applied to every record).  out may be NULL to only

@@ -91,6 +91,8 @@ def lib():
         L.orc_crc32.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.orc_crc32_fast.restype = ctypes.c_uint32
         L.orc_crc32_fast.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.orc_crc32_clmul.restype = ctypes.c_uint32
+        L.orc_crc32_clmul.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.orc_replay.restype = ctypes.c_int
         L.orc_replay.argtypes = [ctypes.POINTER(OrcFile), ctypes.c_uint32, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(OrcStatus)]

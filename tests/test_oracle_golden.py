@@ -18,10 +18,13 @@ def test_crc_check_values(orc):
     assert orc.crc32(b"") == 0
     assert orc.crc32(b"val") == 2548021861  # the CRC core/db_test.go:428-471 stores for "val"
     rng = np.random.default_rng(0)
-    for n in [1, 7, 8, 9, 63, 64, 1000, 4097]:
+    for n in [1, 7, 8, 9, 63, 64, 65, 79, 80, 127, 128, 129, 1000, 4097, 65536 + 13]:
         b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
         assert orc.crc32(b) == zlib.crc32(b)
         assert orc.lib().orc_crc32_fast(np.frombuffer(b, np.uint8).ctypes.data, n) == zlib.crc32(b)
+        # the CPU baseline's CLMUL path (Go's amd64 ieeeCLMUL speed class), also at odd addresses
+        a = np.frombuffer(b"\0" + b, np.uint8)
+        assert orc.lib().orc_crc32_clmul(a.ctypes.data + 1, n) == zlib.crc32(b), n
 
 
 @pytest.mark.parametrize("name", case_names())
