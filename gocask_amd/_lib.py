@@ -72,6 +72,7 @@ class GckOpts(ctypes.Structure):
         ("chunk_cap", ctypes.c_uint32),
         ("flags", ctypes.c_uint32),
         ("spec_window", ctypes.c_uint32),
+        ("max_resident", ctypes.c_uint64),
     ]
 
 
@@ -85,6 +86,8 @@ class GckResult(ctypes.Structure):
         ("err_file", ctypes.c_uint32),
         ("files_walked", ctypes.c_uint32),
         ("err_off", ctypes.c_uint64),
+        ("n_groups", ctypes.c_uint32),
+        ("n_resident", ctypes.c_uint32),
     ]
 
 

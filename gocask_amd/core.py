@@ -79,7 +79,7 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0, max_resident=0):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
@@ -87,6 +87,7 @@ def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
     o.chunk_cap = chunk_cap
     o.flags = 0
     o.spec_window = spec_window
+    o.max_resident = max_resident
     return o
 
 
@@ -221,7 +222,7 @@ def _result(res: GckResult):
         ctypes.memmove(recs.ctypes.data, res.recs, n * REC_DTYPE.itemsize)
     return recs, dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=n,
                       n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset,
-                      files_walked=res.files_walked)
+                      files_walked=res.files_walked, n_groups=res.n_groups, n_resident=res.n_resident)
 
 
 def host_register(arr):
@@ -233,15 +234,16 @@ def host_unregister(arr):
     check(_lib.load().gck_host_unregister(arr.ctypes.data))
 
 
-def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0):
+def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0,
+           max_resident=0):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window)),
-                      ctypes.byref(res))
+    rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window,
+                                                        max_resident)), ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
         return _result(res)
@@ -249,7 +251,7 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0):
+def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0):
     """gck_replay_into: host-in/host-out replay (pipelined over file groups)
     with the tuples written into recs (a REC_DTYPE array; register it with
     host_register for DMA rate).  Returns the status dict; recs[:n] hold the
@@ -259,11 +261,12 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0):
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes)),
+    rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_resident=max_resident)),
                            recs.ctypes.data if recs.size else None, recs.size, ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     return dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=res.n,
-                n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset, files_walked=res.files_walked)
+                n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset, files_walked=res.files_walked,
+                n_groups=res.n_groups, n_resident=res.n_resident)
 
 
 def release_cache():

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kCmpBlock) void k_cmp_fcount(const uint32_t *__rest
 }
 __global__ __launch_bounds__(64) void k_cmp_ftop(uint64_t *__restrict__ bcnt, uint64_t nb, uint32_t lead,
                                                  uint32_t *__restrict__ fstart, uint64_t n, uint32_t *__restrict__ n_files) {
-    uint64_t run = lead;
+    uint64_t run = 0;  // block offsets among the starts (k_cmp_fscatter adds lead)
     for (uint64_t i0 = 0; i0 < nb; i0 += 64) {
         const uint64_t i = i0 + threadIdx.x;
         const uint64_t v = i < nb ? bcnt[i] : 0;
@@ -219,8 +219,8 @@ __global__ __launch_bounds__(64) void k_cmp_ftop(uint64_t *__restrict__ bcnt, ui
     }
     if (threadIdx.x == 0) {
         if (lead) fstart[0] = 0;  // the empty first file
-        fstart[run] = (uint32_t)n;
-        *n_files = (uint32_t)run;
+        fstart[lead + run] = (uint32_t)n;
+        *n_files = (uint32_t)(lead + run);
     }
 }
 __global__ __launch_bounds__(kCmpBlock) void k_cmp_fscatter(const uint32_t *__restrict__ on, uint64_t n,
@@ -473,6 +473,8 @@ extern "C" int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file
     const uint64_t n = c->n_live;
     std::vector<uint32_t> fs(nf + 1);
     if (nf) GCK_HIP(hipMemcpy(fs.data(), c->d_cfstart.p, (nf + 1) * 4, hipMemcpyDeviceToHost));
+    for (uint32_t k = 0; k < nf; ++k)  // file starts are record indices in order (never trust them blindly)
+        if (fs[k] > fs[k + 1] || fs[k + 1] > n) return GCK_EDEVICE;
     std::vector<uint64_t> pos(n + 1), hpos(n + 1);
     if (file_sizes || hint_sizes) {
         GCK_HIP(hipMemcpy(pos.data(), c->d_cpos.p, (n + 1) * 8, hipMemcpyDeviceToHost));

@@ -46,25 +46,39 @@ struct DBuf {
 };
 
 enum Phase {
-    PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
+    PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds (pipelined: group 0's)
     PH_SCAN,          // record slots per chunk, per-file summary
-    PH_HOST,          // D2H summary + host bookkeeping
+    PH_HOST,          // D2H summary + host bookkeeping (device path: k_account_grp)
     PH_RECORDS,       // k_row_fill, k_compact, k_row_tail
-    PH_CRC,           // k_crc_rows: the HBM-bound kernel
+    PH_CRC,           // k_crc_rows: the HBM-bound kernel (pipelined: every group's launch)
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
     PH_PIPE = PH_END, // (time) device span of the whole run
+    PH_HIDDEN,        // (time) pipelined: boundary .. records of groups 1.. on the side stream
+    PH_WAIT,          // (time) pipelined: k_crc_rows launches waiting for their group's records
     PH_NPHASE
 };
+
+// The device path runs file groups as a two-stream software pipeline: the
+// boundary side (boundary, scans, accounting, record table) of group g + 1
+// on a side stream while k_crc_rows streams group g.
+constexpr uint32_t kMaxGroups = 8;
+constexpr uint32_t kGbSlots = kMaxGroups + 1;  // d_gbase: the groups' record bases, then ranges
 
 
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // the pipelined device path's boundary side
     // end-of-run counters and results land here by a kernel's PCIe writes
     // (coherent pinned host memory, mapped): no DMA-engine copy, which would
     // queue behind any large H2D already queued (gck_replay's file groups)
     uint32_t *h_mbox = nullptr, *d_mbox = nullptr;
+    // layout tables go up through pinned, mapped host memory read by a kernel
+    // on `stream` (k_upload), not by DMA copies, which would queue behind any
+    // large H2D in flight (gck_replay's file groups)
+    uint8_t *h_up = nullptr, *d_up = nullptr;
+    size_t up_cap = 0;
     gck_opts opts{};
     int n_cu = 256;
     int fin_blocks_per_cu = 4;  // resident k_finalize workgroups per CU
@@ -77,6 +91,17 @@ struct Ctx {
     std::vector<uint8_t> f_reset;
     std::vector<uint32_t> f_first_chunk, f_nchunks;
     uint64_t data_bytes = 0;
+    // file groups of the pipelined device path (ctx_layout): group g = files
+    // [grp_file[g], grp_file[g+1]), chunks [grp_chunk[g], grp_chunk[g+1]),
+    // CRC rows [grp_row0[g], grp_row1[g]); row grp_row1[g] of every group but
+    // the last is an empty gap row whose row_first the group's own records
+    // phase writes (k_crc_rows of group g reads it while group g + 1 is
+    // being built).  Cuts follow files that reset lastOffset.
+    uint32_t n_groups = 1;
+    bool pipeline = true;  // false: one group (gck_replay's pooled contexts)
+    std::vector<uint32_t> grp_file, grp_chunk;
+    std::vector<uint64_t> grp_row0, grp_row1;
+    hipEvent_t ev_s0[kMaxGroups] = {}, ev_s1[kMaxGroups] = {}, ev_c0[kMaxGroups] = {}, ev_c1[kMaxGroups] = {};
 
     // chunk metadata
     uint32_t n_chunks = 0;

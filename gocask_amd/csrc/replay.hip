@@ -37,6 +37,10 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
+// device-path pipeline shape (ctx_layout, pipe_shape): file groups and the
+// first group's share of the bytes in permille
+constexpr uint32_t kPipeGroups = 4;
+constexpr uint32_t kPipeFirstPermille = 250;
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -595,55 +599,62 @@ __global__ void k_file_summary(const uint32_t *__restrict__ f_first_chunk,
     f_tpos[f] = tpos;
 }
 
-// Zero the run's counters / results (32 u32), record range, row_first[0]
-// and the CRC block queue: one launch instead of four memsets.
-__global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ rng, uint32_t *__restrict__ row_first,
+// Zero the run's counters / results (32 u32: status GCK_OK = 0), the group
+// record bases and ranges, row_first[0] and the groups' CRC block queues: one
+// launch instead of several memsets.
+__global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb, uint32_t *__restrict__ row_first,
                            uint32_t *__restrict__ queue) {
     const uint32_t t = threadIdx.x;
     if (t < 32) cnt[t] = 0;
-    if (t < 2) rng[t] = 0;
-    if (t == 0) {
-        row_first[0] = 0;
-        *queue = 0;
-    }
+    if (t < kGbSlots + 2 * kMaxGroups + 2) gb[t] = 0;
+    if (t < kMaxGroups) queue[t] = 0;
+    if (t == 0) row_first[0] = 0;
 }
 
-// The host bookkeeping of a run (core/db.go:110-140), on the device so a run
-// needs no host round trip: per file the lastOffset carried in (reset after
-// every file but the active one, core/db.go:117-119), the first startup error
-// (it aborts filepath.Walk: later files contribute nothing, disk.go:134-141),
-// the run's record range and the final lastOffset.  One thread; res (u64):
-// 0 status, 1 error file, 2 error offset, 3 files walked, 4 final lastOffset,
-// 5 records (unclamped).  rng[1] = min(records, cap).
-__global__ void k_account(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
-                          const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
-                          const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec,
-                          uint32_t *__restrict__ carry, uint64_t *__restrict__ rng, uint64_t cap,
-                          uint64_t *__restrict__ res) {
-    uint32_t last = 0, status = GCK_OK, err_file = 0, walked = nf;
-    uint64_t err_off = 0, n_total = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
+// The host bookkeeping of a run (core/db.go:110-140) for the files [f0, f1)
+// of one group, on the device so a run needs no host round trip; groups run
+// in walk order.  Per file the lastOffset carried in (reset after every file
+// but the active one, core/db.go:117-119; a group starts after a resetting
+// file, so at 0), the first startup error (it aborts filepath.Walk: later
+// files and groups contribute nothing, disk.go:134-141), the group's record
+// range and the run's results so far.  One thread; res (u64): 0 status,
+// 1 error file, 2 error offset, 3 files walked, 4 final lastOffset, 5 records
+// (unclamped); gb = the group's record base; grng = its record range [lo, hi)
+// clamped to cap; rng = the run's [0, hi).
+__global__ void k_account_grp(uint32_t f0, uint32_t f1, const uint64_t *__restrict__ flen,
+                              const uint32_t *__restrict__ freset, const uint32_t *__restrict__ fterm,
+                              const uint64_t *__restrict__ ftpos, const uint64_t *__restrict__ ffirst,
+                              const uint64_t *__restrict__ fnrec, uint32_t *__restrict__ carry,
+                              const uint64_t *__restrict__ gb, uint64_t cap, uint64_t *__restrict__ res,
+                              uint64_t *__restrict__ grng, uint64_t *__restrict__ rng) {
+    const uint64_t lo = gb[0] < cap ? gb[0] : cap;
+    if (res[0] != GCK_OK) {  // an earlier group hit a startup error
+        grng[0] = grng[1] = lo;
+        return;
+    }
+    uint32_t last = 0, walked = f1;
+    uint64_t n_end = gb[0];
+    for (uint32_t f = f0; f < f1; ++f) {
         carry[f] = last;
         const uint64_t valid = fterm[f] != T_NONE ? ftpos[f] : flen[f];
-        n_total = ffirst[f] + fnrec[f];
+        n_end = ffirst[f] + fnrec[f];
         last += (uint32_t)valid;
         if (fterm[f] == T_ERR) {
-            status = GCK_EUNEXPECTED_EOF;
-            err_file = f;
-            err_off = ftpos[f];
+            res[0] = GCK_EUNEXPECTED_EOF;
+            res[1] = f;
+            res[2] = ftpos[f];
             walked = f + 1;
             break;
         }
         if (freset[f]) last = 0;
     }
-    rng[0] = 0;
-    rng[1] = n_total < cap ? n_total : cap;
-    res[0] = status;
-    res[1] = err_file;
-    res[2] = err_off;
     res[3] = walked;
     res[4] = last;
-    res[5] = n_total;
+    res[5] = n_end;
+    grng[0] = lo;
+    grng[1] = n_end < cap ? n_end : cap;
+    rng[0] = 0;
+    rng[1] = grng[1];
 }
 
 // row_first[row] = the first record whose value ends after the row's first
@@ -738,16 +749,15 @@ __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uin
     return rec_off[r] + 16 + (uint64_t)kv.x + kv.y;  // tombstone: KeySize 0, the key is the "value"
 }
 
-// Record range [rng[0], rng[1]) of the run (device-resident).
-//
-// row_first[row] = first record whose value ends after the row's first byte,
-// for the rows [r0, ...); rows past the last record end keep k_row_fill's
-// value rng[1] (k_row_fill writes rows (r0, r1]; row r0 is set by the caller).
-// Grid-stride over the device range.
+// row_first[row] = first record whose value ends after the row's first byte.
+// k_row_fill sets rows [r0, r1] to rng[1] (the record range's end: the value
+// of rows past the last record end); k_compact then sets the rows of every
+// record, k_row_tail the rows after each file's last record, on the same
+// stream.  Grid-stride over the range.
 __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64_t r1,
                            const uint64_t *__restrict__ rng) {
     const uint32_t v = (uint32_t)rng[1];
-    for (uint64_t row = r0 + 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
+    for (uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
          row += (uint64_t)gridDim.x * blockDim.x)
         row_first[row] = v;
 }
@@ -755,13 +765,15 @@ __global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64
 // Rows after file f's last record, up to the next file's first row, get the
 // next record: ffirst[f] + fnrec[f] (the rows of records are set by
 // k_compact).  The last record ends at the file's length, or where its walk
-// stopped (EOF class or startup error, as k_account).  Files whose records
-// all lie past the run's range keep k_row_fill's value.  One workgroup per file.
+// stopped (EOF class or startup error, as k_account_grp).  Files whose
+// records all lie past the range rng keep k_row_fill's value.  One workgroup
+// per file of [f0, f0 + gridDim.x); nf = files in the arena.
 __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *__restrict__ flen,
                            const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
-                           const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec, uint32_t nf,
-                           uint64_t n_rows, const uint64_t *__restrict__ rng, uint32_t *__restrict__ row_first) {
-    const uint32_t f = blockIdx.x;
+                           const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec, uint32_t f0,
+                           uint32_t nf, uint64_t n_rows, const uint64_t *__restrict__ rng,
+                           uint32_t *__restrict__ row_first) {
+    const uint32_t f = f0 + blockIdx.x;
     const uint64_t re = rng[1];
     if (f >= nf || ffirst[f] >= re) return;
     const uint64_t end = fbase[f] + (fterm[f] != T_NONE ? ftpos[f] : flen[f]);
@@ -1527,7 +1539,14 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), 256, 0));
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    GCK_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
+    for (uint32_t g = 0; g < kMaxGroups; ++g) {
+        GCK_HIP(hipEventCreate(&c->ev_s0[g]));
+        GCK_HIP(hipEventCreate(&c->ev_s1[g]));
+        GCK_HIP(hipEventCreate(&c->ev_c0[g]));
+        GCK_HIP(hipEventCreate(&c->ev_c1[g]));
+    }
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     // the constant tables are the same for every context: built once per process
     struct Tables {
@@ -1575,17 +1594,86 @@ static void ctx_free(Ctx *c) {
     for (DBuf *b : all) b->release();
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
     c->h_mbox = c->d_mbox = nullptr;
+    if (c->h_up) (void)hipHostFree(c->h_up);
+    c->h_up = c->d_up = nullptr;
+    c->up_cap = 0;
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t *st : {&c->stream}) {
+    for (hipEvent_t *evs : {c->ev_s0, c->ev_s1, c->ev_c0, c->ev_c1})
+        for (uint32_t g = 0; g < kMaxGroups; ++g)
+            if (evs[g]) {
+                (void)hipEventDestroy(evs[g]);
+                evs[g] = nullptr;
+            }
+    for (hipStream_t *st : {&c->stream, &c->side}) {
         if (*st) (void)hipStreamDestroy(*st);
         *st = nullptr;
     }
 }
 
-// Place files (walk order) in the arena and build the chunk table.
+// Layout tables from pinned, mapped host memory (Ctx::h_up) into device
+// buffers: up to 8 segments of 4-byte words, one grid dimension each.
+struct UpSeg {
+    uint32_t *dst;
+    uint64_t src_off, words;
+};
+struct UpList {
+    UpSeg seg[8];
+};
+__global__ void k_upload(const uint8_t *__restrict__ src, UpList l) {
+    const UpSeg sg = l.seg[blockIdx.y];
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src + sg.src_off);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sg.words; i += (uint64_t)gridDim.x * blockDim.x)
+        sg.dst[i] = s[i];
+}
+
+// File groups of the pipelined device path: G groups, the first holding
+// first_pm / 1000 of the bytes (its boundary side is the exposed part of the
+// pipeline), the rest about equal, each cut after a file that resets
+// lastOffset (core/db.go:117-119), so every group's lastOffset starts at 0.
+// Returns the cut file indices (cut[0] = 0, cut.back() = nfiles).
+static std::vector<uint32_t> plan_groups(const uint64_t *lens, const uint8_t *reset, uint32_t nf, uint32_t G,
+                                         uint32_t first_pm) {
+    std::vector<uint32_t> cut{0};
+    uint64_t tot = 0;
+    for (uint32_t f = 0; f < nf; ++f) tot += lens[f];
+    if (G > 1 && nf > 1 && tot) {
+        const double t0 = (double)tot * first_pm / 1000.0;
+        uint64_t acc = 0;
+        for (uint32_t f = 0; f + 1 < nf && cut.size() < G; ++f) {
+            acc += lens[f];
+            const uint32_t k = (uint32_t)cut.size();  // the boundary being placed
+            const double target = k == 1 ? t0 : t0 + ((double)tot - t0) * (k - 1) / (G - 1);
+            if (reset[f] && (double)acc >= target) cut.push_back(f + 1);
+        }
+    }
+    cut.push_back(nf);
+    return cut;
+}
+
+// Group count and first-group share of the pipeline (GCK_PIPE="G,first_permille"
+// overrides them for measurements).
+static void pipe_shape(uint32_t &G, uint32_t &first_pm) {
+    G = kPipeGroups;
+    first_pm = kPipeFirstPermille;
+    if (const char *e = getenv("GCK_PIPE")) {
+        unsigned a = 0, b = 0;
+        if (sscanf(e, "%u,%u", &a, &b) == 2 && a >= 1 && a <= kMaxGroups && b >= 1 && b < 1000) {
+            G = a;
+            first_pm = b;
+        }
+    }
+}
+
+// Place files (walk order) in the arena and build the chunk table and, for
+// the pipelined device path, the file groups (one empty gap row after every
+// group but the last).
 int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after) {
     GCK_HIP(hipSetDevice(c->device));
+    uint32_t G = 1, first_pm = 500;
+    if (c->pipeline) pipe_shape(G, first_pm);
+    const std::vector<uint32_t> cut = plan_groups(lens, reset_after, nfiles, G, first_pm);
+    c->n_groups = (uint32_t)cut.size() - 1;
     c->nfiles = nfiles;
     c->f_base.assign(nfiles, 0);
     c->f_len.assign(lens, lens + nfiles);
@@ -1596,7 +1684,11 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     const uint64_t CB = c->opts.chunk_bytes;
     std::vector<uint32_t> ch_file;
     std::vector<uint64_t> ch_start, ch_end;
-    for (uint32_t f = 0; f < nfiles; ++f) {
+    for (uint32_t f = 0, g = 0; f < nfiles; ++f) {
+        if (g + 1 < c->n_groups && f == cut[g + 1]) {
+            pos += kRow;  // the gap row after group g
+            ++g;
+        }
         c->f_base[f] = pos;
         pos += (lens[f] + kRow - 1) / kRow * kRow;
         data += lens[f];
@@ -1613,6 +1705,15 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     c->data_bytes = data;
     c->n_rows = pos / kRow;
     c->n_chunks = (uint32_t)ch_file.size();
+    c->grp_file = cut;
+    c->grp_chunk.assign(c->n_groups + 1, c->n_chunks);
+    c->grp_row0.assign(c->n_groups, 0);
+    c->grp_row1.assign(c->n_groups, c->n_rows);
+    for (uint32_t g = 0; g < c->n_groups && nfiles; ++g) {
+        c->grp_chunk[g] = c->f_first_chunk[cut[g]];
+        c->grp_row0[g] = c->f_base[cut[g]] / kRow;
+        if (g + 1 < c->n_groups) c->grp_row1[g] = c->f_base[cut[g + 1]] / kRow - 1;  // the gap row
+    }
     const uint64_t nc = c->n_chunks, nf = nfiles ? nfiles : 1;
     const uint64_t cap = c->opts.chunk_cap;
     int rc;
@@ -1631,22 +1732,48 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure(16)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure((kGbSlots + 2 * kMaxGroups + 2) * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
-        (rc = c->d_queue.ensure(16)))
+        (rc = c->d_queue.ensure(kMaxGroups * 4 + 16)))
         return rc;
-    if (nfiles) {
-        GCK_HIP(hipMemcpy(c->d_fbase.p, c->f_base.data(), nfiles * 8, hipMemcpyHostToDevice));
-        GCK_HIP(hipMemcpy(c->d_flen.p, c->f_len.data(), nfiles * 8, hipMemcpyHostToDevice));
-        GCK_HIP(hipMemcpy(c->d_ffirst.p, c->f_first_chunk.data(), nfiles * 4, hipMemcpyHostToDevice));
-        GCK_HIP(hipMemcpy(c->d_fnch.p, c->f_nchunks.data(), nfiles * 4, hipMemcpyHostToDevice));
-        std::vector<uint32_t> rs(reset_after, reset_after + nfiles);
-        GCK_HIP(hipMemcpy(c->d_freset.p, rs.data(), nfiles * 4, hipMemcpyHostToDevice));
+    // the tables, staged in pinned mapped host memory and copied by k_upload
+    // on the context's stream (the previous upload has been consumed: the
+    // stream is drained first, and runs are synchronous)
+    std::vector<uint32_t> rs(reset_after, reset_after + nfiles);
+    struct {
+        void *dst;
+        const void *src;
+        uint64_t bytes;
+    } tab[8] = {{c->d_fbase.p, c->f_base.data(), nfiles * 8ull},     {c->d_flen.p, c->f_len.data(), nfiles * 8ull},
+                {c->d_ffirst.p, c->f_first_chunk.data(), nfiles * 4ull}, {c->d_fnch.p, c->f_nchunks.data(), nfiles * 4ull},
+                {c->d_freset.p, rs.data(), nfiles * 4ull},              {c->d_ch_file.p, ch_file.data(), nc * 4},
+                {c->d_ch_start.p, ch_start.data(), nc * 8},             {c->d_ch_end.p, ch_end.data(), nc * 8}};
+    uint64_t up = 0;
+    for (auto &t : tab) up += (t.bytes + 15) & ~15ull;
+    GCK_HIP(hipStreamSynchronize(c->stream));
+    if (up > c->up_cap) {
+        if (c->h_up) (void)hipHostFree(c->h_up);
+        c->h_up = c->d_up = nullptr;
+        c->up_cap = 0;
+        void *hp = nullptr, *dp = nullptr;
+        if (hipHostMalloc(&hp, up, hipHostMallocMapped) != hipSuccess) return GCK_ENOMEM;
+        c->h_up = static_cast<uint8_t *>(hp);
+        GCK_HIP(hipHostGetDevicePointer(&dp, hp, 0));
+        c->d_up = static_cast<uint8_t *>(dp);
+        c->up_cap = up;
     }
-    if (nc) {
-        GCK_HIP(hipMemcpy(c->d_ch_file.p, ch_file.data(), nc * 4, hipMemcpyHostToDevice));
-        GCK_HIP(hipMemcpy(c->d_ch_start.p, ch_start.data(), nc * 8, hipMemcpyHostToDevice));
-        GCK_HIP(hipMemcpy(c->d_ch_end.p, ch_end.data(), nc * 8, hipMemcpyHostToDevice));
+    UpList l{};
+    uint64_t off = 0, most = 0;
+    for (int k = 0; k < 8; ++k) {
+        if (tab[k].bytes) memcpy(c->h_up + off, tab[k].src, tab[k].bytes);
+        l.seg[k] = UpSeg{static_cast<uint32_t *>(tab[k].dst), off, tab[k].bytes / 4};
+        most = std::max<uint64_t>(most, tab[k].bytes / 4);
+        off += (tab[k].bytes + 15) & ~15ull;
+    }
+    if (most) {
+        const uint32_t gx = (uint32_t)std::min<uint64_t>((most + 255) / 256, 1024);
+        k_upload<<<dim3(gx, 8), 256, 0, c->stream>>>(c->d_up, l);
+        GCK_HIP(hipGetLastError());
     }
     return GCK_OK;
 }
@@ -1712,9 +1839,10 @@ static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_
             c->d_fnrec.as<uint64_t>() + f0, f1 - f0);
 }
 
-// Record table of chunks [c0, c1) and row index (row_first) of rows [r0, r1].
-static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1,
-                           const uint64_t *rng, uint64_t cap) {
+// Record table of chunks [c0, c1) and row index (row_first) of rows [r0, r1]
+// of files [f0, f1); rng = the records' range.
+static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1, uint32_t f0,
+                           uint32_t f1, const uint64_t *rng, uint64_t cap) {
     const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
     const uint32_t grid = (uint32_t)c->n_cu * 4;
     k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
@@ -1727,20 +1855,21 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                              c->d_rec_file.as<uint32_t>(), c->d_row_first.as<uint32_t>(),
                                              c->d_counters.as<uint32_t>());
-    if (c->nfiles)
-        k_row_tail<<<c->nfiles, 256, 0, s>>>(c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
-                                             c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
-                                             c->d_fnrec.as<uint64_t>(), c->nfiles, c->n_rows, rng,
-                                             c->d_row_first.as<uint32_t>());
+    if (f1 > f0)
+        k_row_tail<<<f1 - f0, 256, 0, s>>>(c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
+                                           c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
+                                           c->d_fnrec.as<uint64_t>(), f0, c->nfiles, c->n_rows, rng,
+                                           c->d_row_first.as<uint32_t>());
 }
 
-// CRC partials of rows [r0, r1) (k_crc_rows).  Record-slot scratch: cap ..
-// cap + kEpScratch; rend scratch: rows n_rows ...
-static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, bool queue_zeroed = false) {
+// CRC partials of rows [r0, r1) (k_crc_rows), block queue slot q.  Record-slot
+// scratch: cap .. cap + kEpScratch; rend scratch: rows n_rows ...
+static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, uint32_t q,
+                      bool queue_zeroed = false) {
     if (r1 <= r0) return GCK_OK;
     const uint64_t nb = (r1 - r0 + kBlockRows - 1) / kBlockRows;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
-    uint32_t *queue = c->d_queue.as<uint32_t>();
+    uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_crc_rows<<<grid, 1024, 0, s>>>(
         c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
@@ -1882,9 +2011,9 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
 
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, n_total);
+    launch_records(c, s, 0, nc, 0, c->n_rows, 0, nf, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total))) return rc;
+    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, 0))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -1913,40 +2042,62 @@ __global__ void k_publish(const uint32_t *__restrict__ cnt, uint32_t *mbox) {
 
 // The same run with no host round trip, for a context whose record table
 // was sized by an earlier run (repeated replays of a resident arena): the
-// bookkeeping runs on the device (k_account), the record table is clamped to
-// its capacity, and one copy at the end brings back counters and results.
+// bookkeeping runs on the device (k_account_grp), the record table is clamped
+// to its capacity, and the counters come back through the mapped mailbox.
 // Returns GCK_ERERUN when the run cannot be trusted as is (more records than
 // capacity, or speculation not settled by the device rounds): the caller then
 // reruns on the host path, whose result is exact.
+//
+// Software pipeline over the file groups (ctx_layout): the side stream builds
+// group after group -- boundary, scans, accounting, record table -- and
+// k_crc_rows of group g starts on the main stream as soon as group g's record
+// table is done, so the boundary side of groups 1.. runs beside the CRC
+// stream of earlier groups (those kernels use no LDS and few registers: they
+// fit next to k_crc_rows' 16 waves per CU).  Only group 0's boundary side and
+// the finalize after the last group are exposed.  One group: everything on
+// the main stream, as before.
 constexpr int GCK_ERERUN = -1;
 static int ctx_run_device(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
-    hipStream_t s = c->stream;
-    const uint32_t nc = c->n_chunks, nf = c->nfiles;
+    hipStream_t m = c->stream;
+    const uint32_t G = c->n_groups;
+    hipStream_t s = G > 1 ? c->side : m;
     const uint64_t cap = c->rec_cap;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
-    uint64_t *gbase = c->d_gbase.as<uint64_t>();
+    uint64_t *gb = c->d_gbase.as<uint64_t>();              // record base of group g: gb[g]
+    uint64_t *grng = gb + kGbSlots, *rng = grng + 2 * kMaxGroups;  // group ranges, the run's range
     uint64_t *res = c->d_counters.as<uint64_t>() + 8;
-    k_run_init<<<1, 64, 0, s>>>(cnt, gbase, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
-    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
-    launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
-    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
-    launch_scan(c, s, 0, nc, 0, nf, gbase, cap);
-    GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
-    k_account<<<1, 1, 0, s>>>(nf, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(), c->d_fterm.as<uint32_t>(),
-                              c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
-                              c->d_carry.as<uint32_t>(), gbase, cap, res);
-    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, gbase, cap);
-    GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
+    k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
+    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
+    if (s != m) GCK_HIP(hipStreamWaitEvent(s, c->ev[PH_BOUNDARY], 0));
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t f0 = c->grp_file[g], f1 = c->grp_file[g + 1], c0 = c->grp_chunk[g], c1 = c->grp_chunk[g + 1];
+        GCK_HIP(hipEventRecord(c->ev_s0[g], s));
+        launch_boundary(c, s, c0, c1, cnt + CNT_VAL);
+        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
+        launch_scan(c, s, c0, c1, f0, f1, gb + g, cap);
+        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
+        k_account_grp<<<1, 1, 0, s>>>(f0, f1, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
+                                      c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(),
+                                      c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
+                                      c->d_carry.as<uint32_t>(), gb + g, cap, res, grng + 2 * g, rng);
+        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
+        launch_records(c, s, c0, c1, c->grp_row0[g], c->grp_row1[g], f0, f1, grng + 2 * g, cap);
+        GCK_HIP(hipEventRecord(c->ev_s1[g], s));
+    }
     int rc;
-    if ((rc = launch_crc(c, s, 0, c->n_rows, cap, true))) return rc;
-    GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
-    launch_finalize(c, s, gbase, cap);
-    GCK_HIP(hipEventRecord(c->ev[PH_END], s));
-    k_publish<<<1, 32, 0, s>>>(cnt, c->d_mbox);
-    GCK_HIP(hipStreamSynchronize(s));
+    for (uint32_t g = 0; g < G; ++g) {
+        if (s != m) GCK_HIP(hipStreamWaitEvent(m, c->ev_s1[g], 0));
+        GCK_HIP(hipEventRecord(c->ev_c0[g], m));
+        if ((rc = launch_crc(c, m, c->grp_row0[g], c->grp_row1[g], cap, g, true))) return rc;
+        GCK_HIP(hipEventRecord(c->ev_c1[g], m));
+    }
+    GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
+    launch_finalize(c, m, rng, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_END], m));
+    k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
+    GCK_HIP(hipStreamSynchronize(m));
     GCK_HIP(hipGetLastError());
     uint32_t h[32];
     memcpy(h, c->h_mbox, 128);
@@ -1961,15 +2112,23 @@ static int ctx_run_device(Ctx *c) {
     c->n_fixups = h[CNT_FIXUP];
     c->n_overflow = h[CNT_STAGE];
     c->n_crc_fail = h[CNT_REJECT];
-    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
-    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
+    auto el = [](hipEvent_t a, hipEvent_t b) {
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
-        c->ms_phase[p] = ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        return (double)ms;
+    };
+    for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
+    c->ms_phase[PH_BOUNDARY] = el(c->ev[PH_BOUNDARY], c->ev[PH_SCAN]);
+    c->ms_phase[PH_SCAN] = el(c->ev[PH_SCAN], c->ev[PH_HOST]);
+    c->ms_phase[PH_HOST] = el(c->ev[PH_HOST], c->ev[PH_RECORDS]);
+    c->ms_phase[PH_RECORDS] = el(c->ev[PH_RECORDS], c->ev_s1[0]);
+    for (uint32_t g = 0; g < G; ++g) {
+        c->ms_phase[PH_CRC] += el(c->ev_c0[g], c->ev_c1[g]);
+        c->ms_phase[PH_WAIT] += el(g ? c->ev_c1[g - 1] : c->ev_s1[0], c->ev_c0[g]);
+        if (g) c->ms_phase[PH_HIDDEN] += el(c->ev_s0[g], c->ev_s1[g]);
     }
-    float span = 0;
-    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
-    c->ms_phase[PH_PIPE] = span;
+    c->ms_phase[PH_FINAL] = el(c->ev[PH_FINAL], c->ev[PH_END]);
+    c->ms_phase[PH_PIPE] = el(c->ev[PH_BOUNDARY], c->ev[PH_END]);
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
@@ -2098,7 +2257,8 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
 }
 
 const char *gck_phase_name(int phase) {
-    static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows", "finalize", "pipeline"};
+    static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows",
+                                  "finalize", "pipeline", "side_hidden", "crc_wait"};
     return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
@@ -2119,16 +2279,23 @@ int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, u
 }
 
 // Host-in/host-out replay, pipelined over file groups: the files are cut into
-// contiguous walk-order groups of >= kGroupBytes, each cut after a file that
-// resets lastOffset (so every group replays exactly as the whole walk would,
-// as shards do, gocask_amd/shard.py), one context per group.  All H2D copies
-// are queued at once on a copy stream; group g's replay waits only for its own
-// files, so it runs while later groups are still crossing PCIe.  The first
+// contiguous walk-order groups, each cut after a file that resets lastOffset
+// (so every group replays exactly as the whole walk would, as shards do,
+// gocask_amd/shard.py).  A ring of R device contexts holds R groups at a
+// time: group g's files cross PCIe on a copy stream into context g % R, and
+// it replays on the run stream as soon as they are resident, while later
+// groups are still in flight; a context is laid out again for group g + R
+// once group g's tuples have left.  R = G (every group resident) when the
+// data-file bytes fit the budget -- gck_opts.max_resident, else 60 % of the
+// device's free memory -- so a database larger than HBM streams through a
+// bounded ring instead of failing (Open replays any database size,
+// core/db.go:110-143; data files default to 10 GiB, db.go:45-48).  The first
 // group with a startup error ends the walk (core/db.go:134-138): later groups
-// contribute nothing.  The tuples of the contributing groups (their file
-// indices rebased) are gathered into one array: into the caller's dst (cap
-// records) when dst != NULL, else into library-owned pinned memory.
-constexpr uint64_t kGroupBytes = 1ull << 30;
+// contribute nothing.  The tuples of the contributing groups (file indices
+// rebased) go into the caller's dst (cap records) when dst != NULL, else into
+// library-owned pinned memory.
+constexpr uint64_t kGroupBytes = 1ull << 30;  // group size target (smaller under a tight budget)
+constexpr double kAutoBudgetShare = 0.6;      // share of free HBM the ring may take by default
 
 __global__ void k_rebase_file(gck_rec *recs, uint64_t n, uint32_t base) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
@@ -2154,10 +2321,12 @@ __global__ void k_push_recs(const uint4 *__restrict__ src, uint4 *__restrict__ d
     }
 }
 
-// Contexts of the grouped replay are kept for the next call (per device and
-// options): their arenas and tables stay allocated, so a repeated Open pays
-// no hipMalloc and no table upload.  gck_replay_release_cache frees them.
+// Contexts of the grouped replay are kept for the next call: their arenas
+// and tables stay allocated, so a repeated Open pays no hipMalloc and no table
+// upload.  Bounded: at most kPoolMax contexts, all for one options key (a
+// call with other options evicts them).  gck_replay_release_cache frees them.
 namespace {
+constexpr size_t kPoolMax = 4;
 struct PoolEntry {
     gck_opts key;
     gck_ctx *ctx;
@@ -2167,6 +2336,7 @@ std::vector<PoolEntry> g_pool;
 gck_opts pool_key(const gck_opts *o) {
     gck_opts k{};
     if (o) k = *o;
+    k.max_resident = 0;  // a budget, not a context setting
     return k;
 }
 bool same_opts(const gck_opts &a, const gck_opts &b) {
@@ -2188,8 +2358,32 @@ int pool_take(const gck_opts *o, gck_ctx **out) {
 }
 void pool_give(const gck_opts *o, gck_ctx *c) {
     if (!c) return;
+    const gck_opts k = pool_key(o);
+    std::vector<gck_ctx *> drop;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size();)
+            if (!same_opts(g_pool[i].key, k)) {
+                drop.push_back(g_pool[i].ctx);
+                g_pool.erase(g_pool.begin() + (ptrdiff_t)i);
+            } else {
+                ++i;
+            }
+        if (g_pool.size() < kPoolMax)
+            g_pool.push_back(PoolEntry{k, c});
+        else
+            drop.push_back(c);
+    }
+    for (gck_ctx *d : drop) gck_ctx_destroy(d);
+}
+// device bytes held by pooled contexts for these options (reusable by a call)
+uint64_t pool_bytes(const gck_opts *o) {
+    const gck_opts k = pool_key(o);
+    uint64_t b = 0;
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    g_pool.push_back(PoolEntry{pool_key(o), c});
+    for (auto &e : g_pool)
+        if (same_opts(e.key, k)) b += e.ctx->c.arena.cap;
+    return b;
 }
 }  // namespace
 
@@ -2207,28 +2401,58 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     memset(out, 0, sizeof(*out));
     for (uint32_t f = 0; f < nfiles; ++f)
         if (files[f].len && !files[f].data) return GCK_EINVAL;
+    const uint64_t budget_opt = opts ? opts->max_resident : 0;
+    uint64_t tot = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) tot += files[f].len;
+    // group target: kGroupBytes, or a third of a tight budget (so at least
+    // two groups of files smaller than that fit at once)
+    const uint64_t tgt = budget_opt ? std::max<uint64_t>(1, std::min(kGroupBytes, budget_opt / 3)) : kGroupBytes;
     std::vector<uint32_t> cut{0};  // group g = files [cut[g], cut[g+1])
-    uint64_t acc = 0;
-    for (uint32_t f = 0; f < nfiles; ++f) {
-        acc += files[f].len;
-        if (acc >= kGroupBytes && files[f].reset_after && f + 1 < nfiles) {
-            cut.push_back(f + 1);
-            acc = 0;
+    {
+        uint64_t acc = 0;
+        for (uint32_t f = 0; f < nfiles; ++f) {
+            acc += files[f].len;
+            if (acc >= tgt && files[f].reset_after && f + 1 < nfiles) {
+                cut.push_back(f + 1);
+                acc = 0;
+            }
         }
     }
     cut.push_back(nfiles);
     const uint32_t G = (uint32_t)cut.size() - 1;
-    std::vector<gck_ctx *> cs(G, nullptr);
+    std::vector<uint64_t> gbytes(G, 0);
+    for (uint32_t g = 0; g < G; ++g)
+        for (uint32_t f = cut[g]; f < cut[g + 1]; ++f) gbytes[g] += (files[f].len + kRow - 1) / kRow * kRow;
+    const uint64_t maxg = std::max<uint64_t>(*std::max_element(gbytes.begin(), gbytes.end()), kRow);
+    // ring size R: every group when the bytes fit the budget
+    uint64_t budget = budget_opt;
+    if (!budget) {
+        size_t fr = 0, tt = 0;
+        if (hipSetDevice(opts ? opts->device : 0) != hipSuccess || hipMemGetInfo(&fr, &tt) != hipSuccess) {
+            (void)hipGetLastError();
+            return GCK_EDEVICE;
+        }
+        // records, stage and output add about a third to the data bytes
+        budget = (uint64_t)(kAutoBudgetShare * (double)(fr + pool_bytes(opts)) / 1.35);
+    }
+    uint64_t fit = 0;
+    for (uint32_t g = 0; g < G; ++g) fit += gbytes[g];
+    const uint32_t R = fit <= budget ? G : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(G, budget / maxg));
+    out->n_groups = G;
+    out->n_resident = R;
+    std::vector<gck_ctx *> cs(R, nullptr);
     std::vector<hipEvent_t> ev(G, nullptr);
     hipStream_t copy = nullptr, run_s = nullptr;
-    std::vector<hipStream_t> own_s(G, nullptr);  // the contexts' own streams while they run on run_s
+    std::vector<hipStream_t> own_s(R, nullptr);  // the contexts' own streams while they run on run_s
+    std::vector<void *> chunks(G, nullptr);        // ring mode, gck_replay: each group's tuples (pinned)
+    std::vector<uint64_t> chunk_n(G, 0);
     int rc = GCK_OK;
     auto cleanup = [&](bool keep) {
         if (copy) (void)hipStreamSynchronize(copy);
         if (run_s) {
             (void)hipStreamSynchronize(run_s);
-            for (uint32_t g = 0; g < G; ++g)
-                if (own_s[g]) cs[g]->c.stream = own_s[g];
+            for (uint32_t k = 0; k < R; ++k)
+                if (own_s[k]) cs[k]->c.stream = own_s[k];
             (void)hipStreamDestroy(run_s);
         }
         for (auto *c : cs)
@@ -2236,14 +2460,17 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (copy) (void)hipStreamDestroy(copy);
+        for (void *p : chunks)
+            if (p) (void)hipHostFree(p);
         for (auto *c : cs) {
+            if (!c) continue;
             if (keep)
                 pool_give(opts, c);
             else
                 gck_ctx_destroy(c);
         }
     };
-    for (uint32_t g = 0; g < G && !rc; ++g) rc = pool_take(opts, &cs[g]);
+    for (uint32_t k = 0; k < R && !rc; ++k) rc = pool_take(opts, &cs[k]);
     if (rc) {
         cleanup(true);
         return rc;
@@ -2261,9 +2488,9 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         cleanup(false);
         return GCK_EDEVICE;
     }
-    for (uint32_t g = 0; g < G; ++g) {
-        own_s[g] = cs[g]->c.stream;
-        cs[g]->c.stream = run_s;
+    for (uint32_t k = 0; k < R; ++k) {
+        own_s[k] = cs[k]->c.stream;
+        cs[k]->c.stream = run_s;
     }
     const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
@@ -2272,8 +2499,9 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         (void)hipEventCreate(&tev0);
         (void)hipEventRecord(tev0, copy);
     }
-    for (uint32_t g = 0; g < G && !rc; ++g) {  // layouts, then every H2D queued on the copy stream (below)
-        Ctx *c = &cs[g]->c;
+    // lay group g out in its ring context and queue its files' H2D
+    auto prep = [&](uint32_t g) -> int {
+        Ctx *c = &cs[g % R]->c;
         const uint32_t f0 = cut[g], n = cut[g + 1] - f0;
         std::vector<uint64_t> lens(n);
         std::vector<uint8_t> reset(n);
@@ -2281,37 +2509,36 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
             lens[k] = files[f0 + k].len;
             reset[k] = files[f0 + k].reset_after ? 1 : 0;
         }
-        if ((rc = ctx_layout(c, lens.data(), n, reset.data()))) break;
+        // (the contexts already pipeline against the H2D of later groups on
+        // one shared run stream: no second stream per context)
+        c->pipeline = false;
+        int r;
+        if ((r = ctx_layout(c, lens.data(), n, reset.data()))) return r;
         // a fresh context would take the host path on its first run, whose
         // small D2H copies queue behind the file copies: give it a record table
         // for the device path (one record per 256 B; more reruns exactly)
-        if (!c->rec_cap) {
-            uint64_t bytes = 0;
-            for (uint32_t k = 0; k < n; ++k) bytes += lens[k];
-            const uint64_t est = bytes / 256 + 4096;
-            if ((rc = ensure_records(c, est))) break;
+        uint64_t bytes = 0;
+        for (uint32_t k = 0; k < n; ++k) bytes += lens[k];
+        const uint64_t est = bytes / 256 + 4096;
+        if (c->rec_cap < est) {
+            if ((r = ensure_records(c, est))) return r;
             c->rec_cap = est;
         }
-    }
-    // every layout first: their small synchronous copies would otherwise
-    // queue behind the file copies of earlier groups on the DMA engine
-    for (uint32_t g = 0; g < G && !rc; ++g) {
-        Ctx *c = &cs[g]->c;
-        const uint32_t f0 = cut[g], n = cut[g + 1] - f0;
         for (uint32_t k = 0; k < n; ++k)
             if (files[f0 + k].len && hipMemcpyAsync(c->arena.as<uint8_t>() + c->f_base[k], files[f0 + k].data,
                                                     files[f0 + k].len, hipMemcpyHostToDevice, copy) != hipSuccess)
-                rc = GCK_EDEVICE;
+                return GCK_EDEVICE;
         if (hipEventCreateWithFlags(&ev[g], trace ? hipEventDefault : hipEventDisableTiming) != hipSuccess ||
             hipEventRecord(ev[g], copy) != hipSuccess)
-            rc = GCK_EDEVICE;
-    }
-    // Each group replays once its files are resident; into caller memory, its
-    // tuples (file indices rebased) leave right away on its own stream, so the
-    // D2H of group g overlaps the H2D and replay of the groups after it.
+            return GCK_EDEVICE;
+        return GCK_OK;
+    };
+    // every resident group's layout first, then (in prep) its copies: a
+    // layout uploads its tables by a kernel, never behind the file copies
+    for (uint32_t g = 0; g < std::min(R, G) && !rc; ++g) rc = prep(g);
     uint32_t last = G;  // groups [0, last) contribute
     uint64_t off = 0;
-    bool early = into;  // D2H issued group by group while the caller's array has room
+    bool early = into;  // tuples delivered group by group while the caller's array has room
     // the device mapping of a registered (pinned) dst, for k_push_recs; plain
     // pageable memory has none and takes the DMA copy
     gck_rec *ddst = nullptr;
@@ -2320,8 +2547,13 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         if (hipHostGetDevicePointer(&dp, dst, 0) == hipSuccess && dp) ddst = static_cast<gck_rec *>(dp);
         else (void)hipGetLastError();
     }
+    uint64_t n_total = 0;
+    std::vector<uint64_t> g_fail(G, 0);
+    int32_t st_status = GCK_OK;
+    uint32_t st_err_file = 0, st_walked = 0, st_last = 0;
+    uint64_t st_err_off = 0;
     for (uint32_t g = 0; g < G && !rc; ++g) {
-        Ctx *c = &cs[g]->c;
+        Ctx *c = &cs[g % R]->c;
         if (hipStreamWaitEvent(c->stream, ev[g], 0) != hipSuccess) {
             rc = GCK_EDEVICE;
             break;
@@ -2329,15 +2561,22 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         const auto tr0 = std::chrono::steady_clock::now();
         const int r = ctx_run(c);
         if (trace)
-            fprintf(stderr, "[gck_replay] group %u run returned at %.2f ms (run call %.2f ms, device path %d)\n", g,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(),
+            fprintf(stderr, "[gck_replay] group %u (slot %u) run returned at %.2f ms (run call %.2f ms, device path %d)\n",
+                    g, g % R, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count(),
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count(),
                     (int)c->device_path);
         if (r != GCK_OK && r != GCK_EUNEXPECTED_EOF) {
             rc = r;
             break;
         }
-        if (early && c->n_recs) {
+        g_fail[g] = c->n_crc_fail;
+        n_total += c->n_recs;
+        st_status = c->status;
+        st_err_file = cut[g] + c->err_file;
+        st_err_off = c->err_off;
+        st_walked = cut[g] + c->files_walked;
+        st_last = c->final_last_offset;  // cuts follow resetting files: the last contributing group's
+        if (c->n_recs && early) {
             if (off + c->n_recs > cap) {
                 early = false;
             } else if (ddst) {
@@ -2353,10 +2592,31 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
                     rc = GCK_EDEVICE;
                 off += c->n_recs;
             }
+        } else if (c->n_recs && !into && R < G) {
+            // ring mode, library-owned output: the group's tuples into a pinned
+            // chunk now (its context is about to be reused), joined at the end
+            void *hp = nullptr, *dp = nullptr;
+            if (hipHostMalloc(&hp, c->n_recs * sizeof(gck_rec), hipHostMallocMapped) != hipSuccess ||
+                hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
+                if (hp) (void)hipHostFree(hp);
+                rc = GCK_ENOMEM;
+                break;
+            }
+            chunks[g] = hp;
+            chunk_n[g] = c->n_recs;
+            k_push_recs<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<uint4>(), static_cast<uint4 *>(dp),
+                                                                     c->n_recs, cut[g]);
         }
         if (r == GCK_EUNEXPECTED_EOF) {
             last = g + 1;
             break;
+        }
+        if (g + R < G) {  // this context takes group g + R once its tuples have left
+            if (hipStreamSynchronize(c->stream) != hipSuccess) {
+                rc = GCK_EDEVICE;
+                break;
+            }
+            rc = prep(g + R);
         }
     }
     if (rc) {
@@ -2364,25 +2624,22 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         return rc;
     }
     if (trace) {
-        for (uint32_t g = 0; g < G; ++g) (void)hipStreamSynchronize(cs[g]->c.stream);
+        (void)hipStreamSynchronize(run_s);
         (void)hipStreamSynchronize(copy);
         const double host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_begin).count();
         float copy_ms = 0;
-        (void)hipEventElapsedTime(&copy_ms, tev0, ev[G - 1]);
-        fprintf(stderr, "[gck_replay] groups %u host %.2f ms, H2D (copy stream) %.2f ms\n", G, host_ms, copy_ms);
+        (void)hipEventElapsedTime(&copy_ms, tev0, ev[last - 1]);
+        fprintf(stderr, "[gck_replay] groups %u resident %u host %.2f ms, H2D (copy stream) %.2f ms\n", G, R, host_ms,
+                copy_ms);
         (void)hipEventDestroy(tev0);
     }
-    uint64_t n_total = 0;
-    for (uint32_t g = 0; g < last; ++g) n_total += cs[g]->c.n_recs;
-    const Ctx *lc = &cs[last - 1]->c;
     out->n = n_total;
-    out->status = lc->status;
-    out->err_file = cut[last - 1] + lc->err_file;
-    out->err_off = lc->err_off;
-    out->files_walked = cut[last - 1] + lc->files_walked;
-    // cuts follow resetting files: the last contributing group's lastOffset
-    out->final_last_offset = lc->final_last_offset;
-    for (uint32_t g = 0; g < last; ++g) out->n_crc_fail += cs[g]->c.n_crc_fail;
+    out->status = st_status;
+    out->err_file = st_err_file;
+    out->err_off = st_err_off;
+    out->files_walked = st_walked;
+    out->final_last_offset = st_last;
+    for (uint32_t g = 0; g < last; ++g) out->n_crc_fail += g_fail[g];
     if (into) {
         cleanup(true);
         if (cap < n_total) return GCK_EINVAL;  // out->n says how many records to make room for
@@ -2397,17 +2654,24 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         }
         h = static_cast<gck_rec *>(p);
     }
-    for (uint32_t g = 0; g < last && !rc; ++g) {
-        Ctx *c = &cs[g]->c;
-        if (!c->n_recs) continue;
-        if (cut[g]) k_rebase_file<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<gck_rec>(), c->n_recs, cut[g]);
-        if (hipMemcpyAsync(h + off, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost, c->stream) !=
-            hipSuccess)
-            rc = GCK_EDEVICE;
-        off += c->n_recs;
+    if (R < G) {  // the groups' chunks, in order
+        if (hipStreamSynchronize(run_s) != hipSuccess) rc = GCK_EDEVICE;
+        for (uint32_t g = 0; g < last && !rc; ++g) {
+            if (chunk_n[g]) memcpy(h + off, chunks[g], chunk_n[g] * sizeof(gck_rec));
+            off += chunk_n[g];
+        }
+    } else {
+        for (uint32_t g = 0; g < last && !rc; ++g) {
+            Ctx *c = &cs[g]->c;
+            if (!c->n_recs) continue;
+            if (cut[g]) k_rebase_file<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<gck_rec>(), c->n_recs, cut[g]);
+            if (hipMemcpyAsync(h + off, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost, c->stream) !=
+                hipSuccess)
+                rc = GCK_EDEVICE;
+            off += c->n_recs;
+        }
+        if (hipStreamSynchronize(run_s) != hipSuccess) rc = GCK_EDEVICE;
     }
-    for (uint32_t g = 0; g < last; ++g)
-        if (hipStreamSynchronize(cs[g]->c.stream) != hipSuccess) rc = GCK_EDEVICE;
     if (rc) {
         if (h) (void)hipHostFree(h);
         cleanup(false);

@@ -86,6 +86,9 @@ typedef struct gck_opts {
                            /* (rounded up to 4 KiB; default 0 = the whole chunk).  A      */
                            /* chunk whose first record lies further in is covered by the  */
                            /* walk of the chunk before it.                                 */
+    uint64_t max_resident; /* gck_replay / gck_replay_into: data-file bytes resident on   */
+                           /* the device at once (0 = 60 % of free device memory); a     */
+                           /* larger database streams through a ring of file groups      */
 } gck_opts;
 
 typedef struct gck_result {
@@ -97,14 +100,19 @@ typedef struct gck_result {
     uint32_t err_file;          /* file index of the startup error                      */
     uint32_t files_walked;      /* files the reference would have walked                */
     uint64_t err_off;           /* header offset of the record that hit the error       */
+    uint32_t n_groups;          /* gck_replay*: file groups the files were cut into     */
+    uint32_t n_resident;        /* gck_replay*: groups resident at once (the ring)      */
 } gck_result;
 
 /* One-shot host-in/host-out replay: H2D, device pipeline, D2H.  Pipelined over
- * groups of files (>= 1 GiB, cut after files that reset lastOffset): every H2D
- * copy is queued at once and each group replays as soon as its own files are
+ * groups of files (>= 1 GiB, or a third of opts->max_resident; cut after files
+ * that reset lastOffset): each group replays as soon as its own files are
  * resident, while later groups still cross PCIe (register the files with
- * gck_host_register for asynchronous DMA).  Results are those of one replay
- * of all files in walk order. */
+ * gck_host_register for asynchronous DMA).  A ring of groups bounds the device
+ * memory (opts->max_resident): a database larger than it streams through.
+ * Results are those of one replay of all files in walk order.  GCK_ENOMEM:
+ * the device could not hold even one group (a caller may fall back to the CPU
+ * path, as for GCK_EDEVICE). */
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
 /* The same, tuples into caller memory dst (cap records; pin it for DMA rate);
  * out->recs = NULL.  Each group's tuples leave as soon as it has replayed.
