@@ -7,12 +7,14 @@ thin ctypes layer over it (the Python counterpart of a cgo stub).
 from .core import (GB, KB, MB, TB, Config, DB, DefaultConfig, ErrCRCFailed, ErrInvalidKey, ErrInvalidValue,
                    ErrKeyNotFound, ErrPartialWrite, ErrUnexpectedEOF, GoCaskError, InMemoryDB, NewDB, NewDisk,
                    NewInMemory, Open, ReplayContext, StartupError, WithDataDir, WithMaxDataFileSize, device_count,
-                   host_register, host_unregister, keydir, release_cache, replay, replay_into, zipf_table)
+                   host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into,
+                   replay_multi, zipf_table)
 from ._lib import F_CRC_OK, F_TOMBSTONE, REC_DTYPE
 
 __all__ = [
     "GB", "KB", "MB", "TB", "Config", "DB", "DefaultConfig", "ErrCRCFailed", "ErrInvalidKey", "ErrInvalidValue",
     "ErrKeyNotFound", "ErrPartialWrite", "ErrUnexpectedEOF", "GoCaskError", "InMemoryDB", "NewDB", "NewDisk",
     "NewInMemory", "Open", "ReplayContext", "StartupError", "WithDataDir", "WithMaxDataFileSize", "device_count",
-    "host_register", "host_unregister", "keydir", "replay", "zipf_table", "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
+    "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into",
+    "replay_multi", "zipf_table", "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
 ]

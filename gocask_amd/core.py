@@ -269,6 +269,36 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resi
                 n_groups=res.n_groups, n_resident=res.n_resident)
 
 
+def replay_multi(files, reset_after=None, devices=(0,), chunk_bytes=0):
+    """gck_replay_multi: the files sharded over `devices` (one rank each), the
+    keydir merged across them with RCCL inside the library.  Returns (live
+    keydir records, REC_DTYPE with global file indices; status dict)."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    res = GckResult()
+    rc = L.gck_replay_multi(fa, len(arrs), devs.ctypes.data, len(devs), ctypes.byref(_opts(int(devs[0]), chunk_bytes)),
+                            ctypes.byref(res))
+    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+    try:
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
+def plan_shards(sizes, reset_after, world):
+    """gck_plan_shards (host only): [(a, b), ...] file ranges per shard."""
+    L = _lib.load()
+    sz = np.ascontiguousarray(sizes, dtype=np.uint64)
+    rs = np.ascontiguousarray([1 if r else 0 for r in reset_after], dtype=np.uint8)
+    out = np.zeros(2 * world, dtype=np.uint32)
+    check(L.gck_plan_shards(sz.ctypes.data if sz.size else None, rs.ctypes.data if rs.size else None, len(sz), world,
+                            out.ctypes.data))
+    return [(int(out[2 * r]), int(out[2 * r + 1])) for r in range(world)]
+
+
 def release_cache():
     """gck_replay_release_cache: free the device contexts gck_replay keeps."""
     _lib.load().gck_replay_release_cache()

@@ -2402,8 +2402,6 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     for (uint32_t f = 0; f < nfiles; ++f)
         if (files[f].len && !files[f].data) return GCK_EINVAL;
     const uint64_t budget_opt = opts ? opts->max_resident : 0;
-    uint64_t tot = 0;
-    for (uint32_t f = 0; f < nfiles; ++f) tot += files[f].len;
     // group target: kGroupBytes, or a third of a tight budget (so at least
     // two groups of files smaller than that fit at once)
     const uint64_t tgt = budget_opt ? std::max<uint64_t>(1, std::min(kGroupBytes, budget_opt / 3)) : kGroupBytes;

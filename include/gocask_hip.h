@@ -259,6 +259,29 @@ int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_k
  * dst = keys = NULL only reports the sizes. */
 int gck_kd_fetch_merged(gck_ctx *ctx, gck_kd_entry *dst, uint64_t cap, uint8_t *keys, uint64_t keys_cap,
                         uint64_t *n, uint64_t *n_key_bytes);
+
+/* ---- several GPUs in one call ------------------------------
+ * gck_replay over ndev devices (one rank per device): the files (walk order)
+ * are cut into ndev contiguous shards of about equal bytes, only after files
+ * that reset lastOffset (gck_plan_shards), and shard s replays on devices[s]
+ * (a host thread per device).  The first startup error in walk order ends the
+ * walk (core/db.go:134-138): its records before the error count, later shards
+ * nothing.  Then the keydir merge above runs inside the library: per shard the
+ * keydir with tombstones, partitioned by key hash over the devices, exchanged
+ * with RCCL (ncclCommInitAll over the devices, grouped ncclSend / ncclRecv over
+ * xGMI; librccl.so.1 is loaded at the first call), merged per owner.
+ * out->recs = the global live keydir, one gck_rec per live key (rec.file = the
+ * walk index into files[]; any order), out->n = live keys; n_crc_fail = CRC
+ * rejects among the replayed records; status, err_file, err_off, files_walked
+ * and final_last_offset as gck_replay reports them.  Free with
+ * gck_result_free.  GCK_EDEVICE when RCCL cannot be loaded or a device fails. */
+int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
+                     const gck_opts *opts, gck_result *out);
+/* The shard plan (host only, no device): shard s = files [ranges[2 s],
+ * ranges[2 s + 1]); empty shards when there are fewer allowed cuts than
+ * shards.  A cut at i needs reset_after[i - 1] (core/db.go:117-119). */
+int gck_plan_shards(const uint64_t *sizes, const uint8_t *reset_after, uint32_t nfiles, uint32_t world,
+                    uint32_t *ranges);
 int gck_ctx_stats(gck_ctx *ctx, gck_stats *out);
 const char *gck_phase_name(int phase);
 /* Device pointers of the last run's outputs (gck_rec array, n records) and the

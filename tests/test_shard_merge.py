@@ -255,3 +255,19 @@ def test_gather_status_two_ranks_gloo():
         assert p.exitcode == 0
     for _, g, c in res:
         assert g == dict(status=1, err_file=3, err_off=74, files_walked=4, final_last_offset=9) and c == [True, True]
+
+
+def test_library_plan_shards_equals_python():
+    """gck_plan_shards (the C-ABI planner gck_replay_multi uses; host only, no
+    device) cuts exactly as gocask_amd.shard.plan_shards."""
+    import random
+
+    import gocask_amd as g
+    from gocask_amd import shard
+
+    rng = random.Random(5)
+    for _ in range(2000):
+        n, w = rng.randint(0, 24), rng.randint(1, 9)
+        sizes = [rng.choice([0, 1, 4096, rng.randint(0, 1 << 31)]) for _ in range(n)]
+        reset = [rng.random() < 0.85 for _ in range(n)]
+        assert g.plan_shards(sizes, reset, w) == shard.plan_shards(sizes, reset, w), (sizes, reset, w)
