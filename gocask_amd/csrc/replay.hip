@@ -379,8 +379,8 @@ __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_
     ch_wend[c] = ce;
 }
 
-// One lane per chunk: latency-bound header chain from the speculative entry
-// to the walk bound (walk_bound).
+// One lane per chunk of [c_begin, c_end): latency-bound header chain from the
+// speculative entry to the walk bound (walk_bound).
 __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint64_t *__restrict__ fbase,
                                               const uint64_t *__restrict__ flen,
@@ -390,9 +390,9 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint64_t *__restrict__ ch_entry, uint32_t *ch_count,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
                                               uint64_t *ch_wend, uint2 *s_kv, uint32_t cap,
-                                              uint32_t chunk_shift, uint32_t n_chunks) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_chunks) return;
+                                              uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end) {
+    const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= c_end) return;
     const uint32_t f = ch_file[c];
     const uint64_t entry = ch_entry[c];
     const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
@@ -683,8 +683,9 @@ struct DirectEmit {
     __device__ void prime() const {}
 };
 
-// Record table in walk order: one wavefront per chunk copies its staged
-// (KeySize, ValueSize) pairs and rebuilds the record offsets from the chunk's
+// Record table in walk order: one wavefront per chunk c0 + c (the chunk
+// arrays are passed offset by c0; the stage is indexed by global chunk) copies
+// its staged (KeySize, ValueSize) pairs and rebuilds the record offsets from the chunk's
 // entry by a scan of the entry sizes; chunks that overflowed the stage re-walk
 // straight into the table.  A workgroup takes 16 consecutive chunks, so the
 // stage lines it reads (slot i of kStageIl consecutive chunks, stage_slot)
@@ -697,7 +698,7 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   const uint64_t *__restrict__ ch_entry,
                                                   const uint32_t *__restrict__ ch_count,
                                                   const uint64_t *__restrict__ rec_base,
-                                                  const uint2 *__restrict__ s_kv, uint32_t cap,
+                                                  const uint2 *__restrict__ s_kv, uint32_t cap, uint32_t c0,
                                                   uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
                                                   uint2 *rec_kv, uint32_t *rec_file, uint32_t *row_first,
                                                   uint32_t *counters) {
@@ -714,12 +715,12 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
         uint64_t run = base + entry;  // arena offset of the next record
         // the next batch's stage entries are loaded while this batch is
         // written (a batch per round trip otherwise: ~3 per chunk on C3)
-        uint2 nxt = lane < cnt ? s_kv[stage_slot(c, lane, cap)] : make_uint2(0u, 0u);
+        uint2 nxt = lane < cnt ? s_kv[stage_slot(c0 + c, lane, cap)] : make_uint2(0u, 0u);
         for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
             const uint32_t i = i0 + lane;
             const bool in = i < cnt;
             const uint2 kv = nxt;
-            nxt = i + 64 < cnt ? s_kv[stage_slot(c, i + 64, cap)] : make_uint2(0u, 0u);
+            nxt = i + 64 < cnt ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
             // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
             // inclusive scan is exact in 24-bit halves (entries < 2^33)
             const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
@@ -1810,7 +1811,7 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
                                         c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
                                         c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
                                         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                        c->d_ch_wend.as<uint64_t>(), c->d_stage.as<uint2>(), cap, c->chunk_shift, c1);
+                                        c->d_ch_wend.as<uint64_t>(), c->d_stage.as<uint2>(), cap, c->chunk_shift, c0, c1);
     for (int r = 0; r <= kRounds; ++r) {
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
@@ -1851,7 +1852,7 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
                                              c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
                                              c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
                                              c->d_rec_base.as<uint64_t>() + c0,
-                                             c->d_stage.as<uint2>(), ccap, n, cap,
+                                             c->d_stage.as<uint2>(), ccap, c0, n, cap,
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                              c->d_rec_file.as<uint32_t>(), c->d_row_first.as<uint32_t>(),
                                              c->d_counters.as<uint32_t>());

@@ -20,6 +20,10 @@
  * the lexically last directory entry without its extension).
  * Prints "status <rc> last_offset <n> keys <n>" then one line per live key:
  * "<key hex> <crc> <ts> <value_pos> <value_size> <file Name()>", sorted.
+ * SHIM_TIME=1: time the Open as the shim pays it (walk + stat + mmap +
+ * gck_host_register inside the callback, gck_replay, gck_result_free,
+ * unregister + munmap) and print one JSON line instead of the keys.
+ * SHIM_MULTI=1: gck_replay_multi on device 0 (the live keydir comes back).
  */
 #define _GNU_SOURCE
 #include <dirent.h>
@@ -29,6 +33,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "gocask_hip.h"
@@ -121,7 +126,15 @@ static int cmp_kd(const void *a, const void *b) {
     return c ? c : (x->klen > y->klen) - (x->klen < y->klen);
 }
 
+static double now_ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec / 1e6;
+}
+
 int main(int argc, char **argv) {
+    const int timing = getenv("SHIM_TIME") && atoi(getenv("SHIM_TIME"));
+    const int multi = getenv("SHIM_MULTI") && atoi(getenv("SHIM_MULTI"));
     if (argc < 2) {
         fprintf(stderr, "usage: %s <db dir> [active name]\n", argv[0]);
         return 2;
@@ -141,10 +154,12 @@ int main(int argc, char **argv) {
         }
         if (n >= 0) free(ents);
     }
+    const double t0 = now_ms();
     if (walk(argv[1]) != 0) {
         fprintf(stderr, "walk failed\n");
         return 3;
     }
+    const double t1 = now_ms();
     int rc = GCK_OK;
     gck_result res;
     memset(&res, 0, sizeof res);
@@ -155,12 +170,40 @@ int main(int argc, char **argv) {
             gf[i].len = g_files[i].len;
             gf[i].reset_after = strcmp(g_files[i].name, active) != 0;
         }
-        rc = gck_replay(gf, (uint32_t)g_n, NULL, &res);
+        if (multi) {
+            const int32_t dev0 = 0;
+            rc = gck_replay_multi(gf, (uint32_t)g_n, &dev0, 1, NULL, &res);
+        } else {
+            rc = gck_replay(gf, (uint32_t)g_n, NULL, &res);
+        }
         free(gf);
         if (rc != GCK_OK && rc != GCK_EUNEXPECTED_EOF) {
             fprintf(stderr, "gck_replay: %d %s\n", rc, gck_last_error());
             return 4;
         }
+    }
+    const double t2 = now_ms();
+    if (timing) {
+        uint64_t bytes = 0;
+        for (size_t i = 0; i < g_n; ++i) bytes += g_files[i].len;
+        const uint64_t n = res.n, fail = res.n_crc_fail;
+        const uint32_t last = res.final_last_offset, groups = res.n_groups, resident = res.n_resident;
+        if (g_n) gck_result_free(&res);
+        const double t3 = now_ms();
+        for (size_t i = 0; i < g_n; ++i)
+            if (g_files[i].len) {
+                gck_host_unregister(g_files[i].map);
+                munmap((void *)g_files[i].map, g_files[i].len);
+            }
+        const double t4 = now_ms();
+        printf("{\"files\": %zu, \"bytes\": %llu, \"status\": %d, \"records\": %llu, \"crc_rejects\": %llu, "
+               "\"last_offset\": %u, \"groups\": %u, \"resident\": %u, \"walk_mmap_register_ms\": %.2f, "
+               "\"replay_ms\": %.2f, \"free_ms\": %.2f, \"unregister_unmap_ms\": %.2f, \"open_ms\": %.2f, "
+               "\"open_gib_s\": %.3f, \"multi\": %d}\n",
+               g_n, (unsigned long long)bytes, rc, (unsigned long long)n, (unsigned long long)fail, last, groups,
+               resident, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0, bytes / ((t4 - t0) * 1e-3) / (1 << 30), multi);
+        free(g_files);
+        return 0;
     }
     /* keyDir.set / unset in walk order: a sorted array, last writer wins */
     kd_entry *kd = calloc(res.n ? res.n : 1, sizeof(kd_entry));

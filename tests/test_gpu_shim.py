@@ -26,8 +26,10 @@ def shim():
     return SHIM
 
 
-def run(shim, d, active=None):
-    p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120)
+def run(shim, d, active=None, multi=False):
+    env = dict(os.environ, SHIM_MULTI="1" if multi else "0")
+    p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120,
+                       env=env)
     assert p.returncode == 0, p.stderr
     lines = p.stdout.splitlines()
     head = lines[0].split()
@@ -99,3 +101,16 @@ def test_shim_disk_layout(shim, orc, tmp_path):
     assert set(kd) == set(okd)
     for k, r in okd.items():
         assert kd[k]["value_pos"] == int(r["value_pos"]) and kd[k]["file"] == walk[int(r["file"])]
+
+
+@pytest.mark.parametrize("name", ["existing_after_startup", "keys_in_order", "updated_values_across_files",
+                                  "deleted_after_startup", "datatxt_1000_puts", "partial_write_desync"])
+def test_shim_multi_gpu_call_same_keydir(shim, orc, tmp_path, name):
+    """The shim's several-GPU call (gck_replay_multi, RCCL inside the library;
+    one device here) gives the keydir and status of the single-GPU call."""
+    meta, files, reset = load_case(name)
+    for w, f in zip(meta["walk"], files):
+        (tmp_path / (w + ".csk")).write_bytes(f.tobytes())
+    one = run(shim, tmp_path, meta["active"])
+    many = run(shim, tmp_path, meta["active"], multi=True)
+    assert one == many

@@ -1,0 +1,46 @@
+"""Host-inclusive Open of the C3 workload as the cgo shim pays it
+(tests/shim/shim_test.c in SHIM_TIME mode): the 16 x 2 GiB
+files written to /dev/shm (page cache, as a warm database directory), then
+the shim walks, stats, mmaps and gck_host_register's every file inside the
+Walk callback, calls gck_replay (or gck_replay_multi on device 0), frees the
+tuples, unregisters and unmaps.  One JSON line per run; the directory is
+removed at the end.   python tools/shim_c3.py [reps]"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import gocask_amd as g  # noqa: E402
+
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+d = "/dev/shm/gck_c3"
+shutil.rmtree(d, ignore_errors=True)
+os.makedirs(d)
+try:
+    with g.ReplayContext() as ctx:
+        info = ctx.encode(**bench.CONFIGS["c3"])
+        for w in range(info["n_files"]):
+            n = int(info["walk_order"][w])
+            size = int(info["sizes"][n])
+            buf = ctx.read_file(w, 0, size)
+            with open(os.path.join(d, f"data_{n}_{1700000000 + n}.csk"), "wb") as f:
+                f.write(buf.tobytes())
+            del buf
+    shim = os.path.join(ROOT, "tests", "shim", "build", "shim_test")
+    out = []
+    for mode in ("0", "1"):
+        for r in range(reps):
+            p = subprocess.run([shim, d], capture_output=True, text=True, timeout=300,
+                               env=dict(os.environ, SHIM_TIME="1", SHIM_MULTI=mode))
+            if p.returncode:
+                raise SystemExit(p.stderr)
+            row = json.loads(p.stdout.strip().splitlines()[-1])
+            row["rep"] = r
+            out.append(row)
+            print(json.dumps(row), flush=True)
+finally:
+    shutil.rmtree(d, ignore_errors=True)
