@@ -38,9 +38,13 @@ enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 // device-path pipeline shape (ctx_layout, pipe_shape): file groups and the
-// first group's share of the bytes in permille
-constexpr uint32_t kPipeGroups = 4;
-constexpr uint32_t kPipeFirstPermille = 250;
+// first group's share of the bytes in permille.  One group: measured on C3
+// (DESIGN.md §7), the boundary side of later groups beside k_crc_rows slows
+// both (its dependent loads wait behind the stream: 0.36 ms per group alone,
+// 1.3-1.7 ms beside it; k_crc_rows 5.74 -> 6.31 ms), 7.09 -> 7.56 ms per step
+// for four groups, 7.17 for two, 8.11 for eight.
+constexpr uint32_t kPipeGroups = 1;
+constexpr uint32_t kPipeFirstPermille = 500;
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -271,21 +275,30 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 }
             }
             if (wb == kNone) break;
-            uint64_t lanes = __ballot(cm != 0);
-            while (lanes && found == kNone) {
-                const int l = __ffsll((long long)lanes) - 1;
-                uint64_t lm = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(cm >> 32), l) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cm, l);
-                while (lm) {
+            // Candidates in scan order are lane l's bits, then lane l + 1's.
+            // Every lane tests its own candidates in order, all lanes at once
+            // (a chain test is 5 dependent header loads: in turn, one lane's
+            // candidates after another's made the search latency-bound); the
+            // answer is the first passing candidate of the lowest lane with
+            // one, so lanes above the lowest that has passed stop.
+            uint64_t lm = cm, mine = kNone;
+            for (uint64_t pend = __ballot(lm != 0); pend;) {
+                const uint64_t passed = __ballot(mine != kNone);
+                const uint64_t go = passed ? pend & ((passed & (0 - passed)) - 1) : pend;
+                if (!go) break;
+                if ((go >> lane) & 1) {
                     const int t = __ffsll((long long)lm) - 1;
-                    const uint64_t q = wb + 64ull * l + t;
-                    if (q < ce && chain_ok(arena, base, len, q, mk)) {
-                        found = q;
-                        break;
-                    }
+                    const uint64_t q = wb + 64ull * lane + t;
+                    if (q < ce && chain_ok(arena, base, len, q, mk)) mine = q;
                     lm &= lm - 1;
                 }
-                lanes &= lanes - 1;
+                pend = __ballot(lm != 0 && mine == kNone);
+            }
+            const uint64_t passed = __ballot(mine != kNone);
+            if (passed) {
+                const int L = __builtin_ctzll(passed);
+                found = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mine >> 32), L) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mine, L);
             }
             from = wb + 4096;
         }
@@ -299,15 +312,21 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         // the shortest first record wins (ties: the earliest).  (Preferring
         // the latest mis-speculated ~5 chunks of C3's 65 K, the earliest ~15.)
         if (found != kNone) {
-            const Hdr h0 = ld_hdr(arena, base + found);
-            uint64_t best = 16ull + h0.ks + h0.vs, pick = found;
-#pragma unroll 1
-            for (uint32_t k = 1; k <= 3; ++k) {
-                if (found + k >= ce) break;
-                const Hdr hk = ld_hdr(arena, base + found + k);
-                const uint64_t hop = 16ull + hk.ks + hk.vs;
-                if (hop < best && chain_ok(arena, base, len, found + k, mk)) {
-                    best = hop;
+            // lanes 0..3 take found + lane at once: its first hop, kept if it
+            // chains (found itself does); the shortest wins, ties the earliest
+            uint64_t hop = ~0ull;
+            if (lane <= 3 && found + lane < ce) {
+                const Hdr hk = ld_hdr(arena, base + found + lane);
+                const uint64_t h = 16ull + hk.ks + hk.vs;
+                if (lane == 0 || chain_ok(arena, base, len, found + lane, mk)) hop = h;
+            }
+            uint64_t best = ~0ull, pick = found;
+#pragma unroll
+            for (int k = 0; k <= 3; ++k) {
+                const uint64_t hk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(hop >> 32), k) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)hop, k);
+                if (hk < best) {
+                    best = hk;
                     pick = found + k;
                 }
             }
@@ -1309,7 +1328,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     };
     auto issue = [&](const Geo &g, Dep &o) {
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + g.w0);
-        o.vp = *reinterpret_cast<const uint4 *>(arena + g.bsp);  // block holding byte rs - 1
+        // block holding byte rs - 1: only a record with a predecessor in its
+        // file needs it (ft_prev; without one, bsp = rs and it is unused)
+        o.vp = make_uint4(0, 0, 0, 0);
+        if (g.prev_same) o.vp = *reinterpret_cast<const uint4 *>(arena + g.bsp);
         // header + keys up to 24 B as three 16 B loads (dword aligned; the
         // arena is padded): every load instruction of a wave touches 64
         // records' lines, so the count of instructions, not bytes, is the cost
@@ -1324,10 +1346,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         o.vend = make_uint4(0, 0, 0, 0);
         if (!g.have)
             o.vend = *reinterpret_cast<const uint4 *>(arena + g.bse);
-        // row sums rend[fr .. fr + 11] the record crosses (three 16 B loads; rend is padded)
+        // row sums rend[fr .. fr + 11] the record crosses (up to three 16 B
+        // loads, rend is padded; only the ones a record spanning rows uses:
+        // most records lie inside one row)
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = reinterpret_cast<const u32x4_a4 *>(rend + g.fr)[i];
+            u32x4_a4 v = {0u, 0u, 0u, 0u};
+            if (g.lr > g.fr + 4 * i) v = reinterpret_cast<const u32x4_a4 *>(rend + g.fr)[i];
             o.rr[4 * i] = v.x;
             o.rr[4 * i + 1] = v.y;
             o.rr[4 * i + 2] = v.z;
@@ -1335,7 +1360,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
         o.xi = xinv[g.d];
         o.xv0 = xb[g.V & 0xFFFF];
-        o.xhi = xa[g.V >> 16];
+        o.xhi = g.V >= 65536 ? xa[g.V >> 16] : 0u;
         o.cf = carry[g.f];
         o.fb = fbase[g.f];
     };

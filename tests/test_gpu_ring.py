@@ -46,12 +46,15 @@ def _corpus(orc, seed=91, n_files=12, fsize=2 << 20, active=None):
     return wf, reset
 
 
-@pytest.mark.parametrize("budget,ring", [(8 << 20, 2), (12 << 20, 3), (1 << 20, 1)])
-def test_ring_equals_oracle(g, orc, budget, ring):
+@pytest.mark.parametrize("budget", [8 << 20, 12 << 20, 1 << 20])
+def test_ring_equals_oracle(g, orc, budget):
     wf, reset = _corpus(orc, active=4)  # the active file mid-way: its lastOffset carries into file 5
     want, wst = orc.replay(wf, reset)
     got, gst = g.replay(wf, reset, max_resident=budget)
-    assert gst["n_groups"] >= 4 and gst["n_resident"] == ring < gst["n_groups"], gst
+    # groups of >= budget / 3 bytes (cut after resetting files); as many
+    # resident at once as the budget holds of the largest
+    assert gst["n_groups"] >= 4 and 1 <= gst["n_resident"] < gst["n_groups"], gst
+    assert gst["n_resident"] == (1 if budget < (2 << 20) else 2)
     _same(got, gst, want, wst)
     # into caller memory: pageable (DMA copies) and pinned (k_push_recs)
     recs = np.zeros(len(want) + 5, dtype=g.REC_DTYPE)

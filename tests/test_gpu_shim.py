@@ -31,7 +31,12 @@ def run(shim, d, active=None, multi=False):
     p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120,
                        env=env)
     assert p.returncode == 0, p.stderr
+    # (RCCL may print banner lines on stdout when the multi-GPU call loads it):
+    # the result starts at the "status" line
     lines = p.stdout.splitlines()
+    at = [i for i, ln in enumerate(lines) if ln.startswith("status ")]
+    assert at, p.stdout[:2000]
+    lines = lines[at[0]:]
     head = lines[0].split()
     st = dict(status=int(head[1]), last_offset=int(head[3]), keys=int(head[5]))
     kd = {}
