@@ -136,7 +136,7 @@ class GckConfig(ctypes.Structure):
 
 _lib = None
 _diag = None
-DIAG_PATH = os.path.join(os.path.dirname(LIB_PATH), "libgocask_diag.so")
+DIAG_PATH = os.environ.get("GCK_DIAG_PATH") or os.path.join(HERE, "libgocask_diag.so")
 
 
 def _torch_runtime_first():
@@ -254,6 +254,8 @@ def load_diag():
     D.gck_diag_stream_read.argtypes = [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
     D.gck_diag_stream_pattern.restype = ctypes.c_int
     D.gck_diag_stream_pattern.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
+    D.gck_diag_chunks.restype = ctypes.c_int
+    D.gck_diag_chunks.argtypes = [vp, vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]
     _diag = D
     return D
 

@@ -215,3 +215,21 @@ extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter
     if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
     return GCK_OK;
 }
+
+// Per-chunk state of the last run: the chain length k_walk followed (records
+// staged) and the final entry of every chunk (UINT64_MAX: none), for the
+// boundary-phase measurements (tools/chunks.py).
+extern "C" int gck_diag_chunks(gck_ctx *ctx, uint32_t *count, uint64_t *entry, uint64_t cap, uint64_t *n) {
+    if (!ctx || !n) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    *n = c->n_chunks;
+    if (!count || !entry) return GCK_OK;
+    if (cap < c->n_chunks) return GCK_EINVAL;
+    GCK_HIP(hipSetDevice(c->device));
+    GCK_HIP(hipStreamSynchronize(c->stream));
+    if (c->n_chunks) {
+        GCK_HIP(hipMemcpy(count, c->d_ch_count.p, (uint64_t)c->n_chunks * 4, hipMemcpyDeviceToHost));
+        GCK_HIP(hipMemcpy(entry, c->d_ch_entry.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost));
+    }
+    return GCK_OK;
+}

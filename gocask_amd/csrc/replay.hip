@@ -36,6 +36,10 @@ const char *last_error() { return g_err.c_str(); }
 
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
+#ifndef GCK_SPEC_AHEAD
+#define GCK_SPEC_AHEAD 2
+#endif
+constexpr int kSpecAhead = GCK_SPEC_AHEAD;  // k_spec_entry: 4 KiB windows loaded ahead of the one scanned
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 // device-path pipeline shape (ctx_layout, pipe_shape): file groups and the
 // first group's share of the bytes in permille.  One group: measured on C3
@@ -255,7 +259,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         uint64_t from = cs;
         while (found == kNone && from < lim) {
             uint64_t wb = kNone, cm = 0;
-            {
+            if constexpr (kSpecAhead == 2) {
                 u32x4 A[5], B[5], C[5];
                 load(from, A);
                 load(from + 4096, B);
@@ -272,6 +276,26 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                     cm = cands(C);
                     if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
                     if (b0 + 3 * 4096 >= lim) break;
+                }
+            } else if constexpr (kSpecAhead == 1) {
+                u32x4 A[5], B[5];
+                load(from, A);
+                for (uint64_t b0 = from;; b0 += 2 * 4096) {
+                    load(b0 + 4096, B);
+                    cm = cands(A);
+                    if (__ballot(cm != 0)) { wb = b0; break; }
+                    if (b0 + 4096 >= lim) break;
+                    load(b0 + 2 * 4096, A);
+                    cm = cands(B);
+                    if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
+                    if (b0 + 2 * 4096 >= lim) break;
+                }
+            } else {
+                u32x4 A[5];
+                for (uint64_t b0 = from; b0 < lim; b0 += 4096) {
+                    load(b0, A);
+                    cm = cands(A);
+                    if (__ballot(cm != 0)) { wb = b0; break; }
                 }
             }
             if (wb == kNone) break;
@@ -1248,9 +1272,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // reuses bytes 256.. of its region (the M entries 1..15, rewritten by every
     // gf_mul_lds; LDS operations of one wave execute in order)
     __shared__ uint32_t Gm[4 * 1024 + 512];
+    // the shift constants every record needs, from small LDS tables instead
+    // of random global loads (each a distinct line per lane for the TA):
+    // x^{-8d}, d < 4096, as two 64-entry tables (d & 63, 64 (d >> 6)), and
+    // x^{8v}, v < 65536, as two byte tables (v & 0xFF, 256 (v >> 8)); one
+    // more multiply each
+    __shared__ uint32_t Xi[128];
+    __shared__ uint32_t Xb[512];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
         Tz[i] = zrow[i];
         T[i] = g_slice[i];
+    }
+    for (uint32_t i = threadIdx.x; i < 64; i += blockDim.x) {
+        Xi[i] = xinv[i];
+        Xi[64 + i] = xinv[64 * i];
+    }
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        Xb[i] = xb[i];
+        Xb[256 + i] = xb[256 * i];
     }
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) Gm[4096 + i] = mulx(mulx(mulx(mulx(i >> 5))));
     Gm[(threadIdx.x >> 6) * 1024 + (threadIdx.x & 63)] = 0;  // entry 0 of every lane
@@ -1323,7 +1362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     struct Dep {
         uint4 vp, vend;
         uint32_t pw[12], rr[12];
-        uint32_t xi, xv0, xhi, cf;
+        uint32_t xhi, cf;
         uint64_t fb;
     };
     auto issue = [&](const Geo &g, Dep &o) {
@@ -1337,7 +1376,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         // records' lines, so the count of instructions, not bytes, is the cost
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
-            const u32x4_a4 v = reinterpret_cast<const u32x4_a4 *>(wp)[i];
+            // (the third only when the prefix [w0, vs) reaches its words:
+            // keys under 12 + (4 - lead) bytes end in the first 32)
+            u32x4_a4 v = {0u, 0u, 0u, 0u};
+            if (i < 2 || g.vs - g.w0 >= 32) v = reinterpret_cast<const u32x4_a4 *>(wp)[i];
             o.pw[4 * i] = v.x;
             o.pw[4 * i + 1] = v.y;
             o.pw[4 * i + 2] = v.z;
@@ -1358,8 +1400,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             o.rr[4 * i + 2] = v.z;
             o.rr[4 * i + 3] = v.w;
         }
-        o.xi = xinv[g.d];
-        o.xv0 = xb[g.V & 0xFFFF];
         o.xhi = g.V >= 65536 ? xa[g.V >> 16] : 0u;
         o.cf = carry[g.f];
         o.fb = fbase[g.f];
@@ -1372,7 +1412,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + w0);
         const uint4 vp = o.vp, vend = o.vend;
         const uint32_t *pw = o.pw, *rr = o.rr;
-        const uint32_t xi = o.xi, xv0 = o.xv0, xhi = o.xhi, cf = o.cf;
+        const uint32_t xhi = o.xhi, cf = o.cf;
         const uint64_t fb = o.fb;
         // ---- compute
         const uint32_t ft_prev = crc_block(T, e_prev, vp, (uint32_t)(rs - bsp));
@@ -1398,6 +1438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             acc ^= z4096(Tz, h_acc);
         }
         // F(s, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
+        const uint32_t xi = gf_mul_lds(ldsb, mw, rxb, Xi[64 + (g.d >> 6)], Xi[g.d & 63]);  // x^{-8d}
         const uint32_t chain = ft ^ gf_mul_lds(ldsb, mw, rxb, xi, acc);
         // F(s, prefix): header + key bytes [rs, vs) as aligned words from
         // rs & ~3; the first word's bytes before rs are shifted out
@@ -1418,8 +1459,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         for (uint32_t i = 12; i < nw; ++i) p = slice4t(T, p ^ wp[i]);
         if (nw >= 12) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
-        // x^(8V) = xa[V >> 16] * xb[V & 0xFFFF]
-        const uint32_t xv = V < 65536 ? xv0 : gf_mul_lds(ldsb, mw, rxb, xhi, xv0);
+        // x^(8V) = xa[V >> 16] * x^(8 (V & 0xFF00)) * x^(8 (V & 0xFF))
+        uint32_t xv = gf_mul_lds(ldsb, mw, rxb, Xb[256 + ((V >> 8) & 0xFF)], Xb[V & 0xFF]);
+        if (V >= 65536) xv = gf_mul_lds(ldsb, mw, rxb, xhi, xv);
         // crc = F(0, value) ^ crc32(0^V), crc32(0^V) = Z_V(~0) ^ ~0, and Z_V is
         // linear: one multiply covers the prefix and the init term (no
         // crc32(0^V) table load)
