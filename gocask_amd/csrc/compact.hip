@@ -6,7 +6,7 @@
 // database with MaxDataFileSize M (core/db.go:185-231: an entry that does not
 // fit rotates first, rotateDataFile:214-231), each record's bytes verbatim
 // (header, key, value: CRCs and timestamps unchanged).  One hint file per data
-// file lists its records as Bitcask hint entries, little-endian
+// file lists its records as hint entries (invented here, no CRC), little-endian
 //   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
 // (ValuePos = the value's offset in the merged file mod 2^32, as
 // core/keydir.go:25 would set it), so a later start can fill the keydir

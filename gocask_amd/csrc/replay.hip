@@ -828,6 +828,10 @@ __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *_
 
 constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
 constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
+#ifndef GCK_ROWS_AHEAD
+#define GCK_ROWS_AHEAD 1
+#endif
+constexpr int kRowsAhead = GCK_ROWS_AHEAD;  // k_crc_rows: rows loaded ahead of the one processed (1..3)
 constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue claim
 constexpr uint32_t kStaticEighths = 4;     // eighths of k_crc_rows' full rounds assigned statically
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
@@ -1114,10 +1118,14 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     load_plan(q, pc);
     load_plan(qn, pn);
     load_batch(pc, bc);
-    // one row in flight ahead of the one processed (two buffers alternate, so
+    // kRowsAhead rows in flight ahead of the one processed (the buffers rotate
+    // with a period NB dividing the 4 rows of a quad, so each has fixed
+    // registers)
+    constexpr int NB = kRowsAhead == 1 ? 2 : 4;
     // each has fixed registers)
-    u32x4 buf[2][4];
-    issue(q * kBlockRows, buf[0]);
+    u32x4 buf[NB][4];
+#pragma unroll
+    for (int d = 0; d < kRowsAhead; ++d) issue(q * kBlockRows + d, buf[d]);
     for (;;) {
         // block q: plan pc and batch bc are resident; pn (block qn) landed
         // during the previous block: its record ends now, the plan of the
@@ -1144,14 +1152,15 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
                 // the next row: this block's, or the next block's first
-                const uint64_t nrow = st + 1 < kSteps ? row_b + (uint64_t)(st + 1) : qn * kBlockRows;
-                issue(nrow, buf[(u + 1) % 2]);
+                const int ahead = st + kRowsAhead;
+                const uint64_t nrow = ahead < kSteps ? row_b + (uint64_t)ahead : qn * kBlockRows + (uint64_t)(ahead - kSteps);
+                issue(nrow, buf[(u + kRowsAhead) % NB]);
                 // keep the next row's loads here, ahead of this row's compute:
                 // left alone, the scheduler sinks them past most of the chain
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u % 2], rend_buf);
+                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u % NB], rend_buf);
             }
         }
         // the block's 64 rrow values, one coalesced store (rows past the end

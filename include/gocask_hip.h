@@ -183,7 +183,8 @@ int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * not fit rotates first, core/db.go:214-231; a first record larger than the
  * limit leaves the first file empty), each record's bytes verbatim (header,
  * key, value: CRCs and timestamps unchanged).  One hint file per data file
- * lists its records as little-endian Bitcask hint entries
+ * lists its records as little-endian hint entries (format invented here, parity
+ * unpinned: the reference has no hint files; the header CRC is not included)
  *   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
  * (ValuePos = the value's offset in its merged file mod 2^32, as
  * core/keydir.go:25 sets it on a replay of the merged files).  The outputs stay
