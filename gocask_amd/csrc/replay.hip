@@ -36,10 +36,6 @@ const char *last_error() { return g_err.c_str(); }
 
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
-#ifndef GCK_SPEC_AHEAD
-#define GCK_SPEC_AHEAD 2
-#endif
-constexpr int kSpecAhead = GCK_SPEC_AHEAD;  // k_spec_entry: 4 KiB windows loaded ahead of the one scanned
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 // device-path pipeline shape (ctx_layout, pipe_shape): file groups and the
 // first group's share of the bytes in permille.  One group: measured on C3
@@ -67,6 +63,9 @@ __device__ __forceinline__ uint32_t ab(uint32_t hi, uint32_t lo, uint32_t sh) {
 
 struct Hdr {
     uint32_t crc, ts, ks, vs;
+#ifdef GCK_XP_WALKX
+    uint32_t x;
+#endif
 };
 
 // 16-byte little-endian header at any byte offset (core/header.go:58-62).  The
@@ -109,7 +108,26 @@ template <class Emit>
 __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uint64_t len, uint64_t ce,
                            uint64_t p, Emit emit, uint32_t &count, uint64_t &exit, uint32_t &term,
                            uint64_t &tpos) {
+#ifdef GCK_XP_WALKX
+    // experiment: the loads a walk computing the header + key CRC and the
+    // previous record's tail would issue (3 x 16 B at o & ~3, the 16 B block
+    // holding o - 1), consumed without compute
+    auto ld = [&](uint64_t o) {
+        const u32x4_a4 *w = reinterpret_cast<const u32x4_a4 *>(arena + (o & ~3ull));
+        const u32x4_a4 a = w[0], b = w[1], c = w[2];
+        const uint4 v = *reinterpret_cast<const uint4 *>(arena + ((o - (o ? 1 : 0)) & ~15ull));
+        const uint32_t sh = (uint32_t)o & 3u;
+        Hdr h;
+        h.crc = ab(a.y, a.x, sh);
+        h.ts = ab(a.z, a.y, sh);
+        h.ks = ab(a.w, a.z, sh);
+        h.vs = ab(b.x, a.w, sh);
+        h.x = b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ v.x ^ v.y ^ v.z ^ v.w;
+        return h;
+    };
+#else
     auto ld = [&](uint64_t o) { return ld_hdr(arena, o); };
+#endif
     uint32_t n = 0;
     term = T_NONE;
     tpos = 0;
@@ -138,6 +156,9 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
         // the next header (the arena is padded: a read at the file end or
         // just past the chunk stays in bounds and is never used)
         const Hdr hn = ld(base + (next < len ? next : 0));
+#ifdef GCK_XP_WALKX
+        asm volatile("" ::"v"(h.x));
+#endif
         emit(n, p, h);
         ++n;
         p = next;
@@ -259,45 +280,24 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         uint64_t from = cs;
         while (found == kNone && from < lim) {
             uint64_t wb = kNone, cm = 0;
-            if constexpr (kSpecAhead == 2) {
-                u32x4 A[5], B[5], C[5];
-                load(from, A);
-                load(from + 4096, B);
-                for (uint64_t b0 = from;; b0 += 3 * 4096) {
-                    load(b0 + 2 * 4096, C);
-                    cm = cands(A);
-                    if (__ballot(cm != 0)) { wb = b0; break; }
-                    if (b0 + 4096 >= lim) break;
-                    load(b0 + 3 * 4096, A);
-                    cm = cands(B);
-                    if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
-                    if (b0 + 2 * 4096 >= lim) break;
-                    load(b0 + 4 * 4096, B);
-                    cm = cands(C);
-                    if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
-                    if (b0 + 3 * 4096 >= lim) break;
-                }
-            } else if constexpr (kSpecAhead == 1) {
-                u32x4 A[5], B[5];
-                load(from, A);
-                for (uint64_t b0 = from;; b0 += 2 * 4096) {
-                    load(b0 + 4096, B);
-                    cm = cands(A);
-                    if (__ballot(cm != 0)) { wb = b0; break; }
-                    if (b0 + 4096 >= lim) break;
-                    load(b0 + 2 * 4096, A);
-                    cm = cands(B);
-                    if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
-                    if (b0 + 2 * 4096 >= lim) break;
-                }
-            } else {
-                u32x4 A[5];
-                for (uint64_t b0 = from; b0 < lim; b0 += 4096) {
-                    load(b0, A);
-                    cm = cands(A);
-                    if (__ballot(cm != 0)) { wb = b0; break; }
-                }
+            u32x4 A[5], B[5], C[5];
+            load(from, A);
+            load(from + 4096, B);
+            for (uint64_t b0 = from;; b0 += 3 * 4096) {
+                load(b0 + 2 * 4096, C);
+                cm = cands(A);
+                if (__ballot(cm != 0)) { wb = b0; break; }
+                if (b0 + 4096 >= lim) break;
+                load(b0 + 3 * 4096, A);
+                cm = cands(B);
+                if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
+                if (b0 + 2 * 4096 >= lim) break;
+                load(b0 + 4 * 4096, B);
+                cm = cands(C);
+                if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
+                if (b0 + 3 * 4096 >= lim) break;
             }
+
             if (wb == kNone) break;
             // Candidates in scan order are lane l's bits, then lane l + 1's.
             // Every lane tests its own candidates in order, all lanes at once
@@ -828,10 +828,6 @@ __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *_
 
 constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
 constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
-#ifndef GCK_ROWS_AHEAD
-#define GCK_ROWS_AHEAD 1
-#endif
-constexpr int kRowsAhead = GCK_ROWS_AHEAD;  // k_crc_rows: rows loaded ahead of the one processed (1..3)
 constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue claim
 constexpr uint32_t kStaticEighths = 4;     // eighths of k_crc_rows' full rounds assigned statically
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
@@ -1118,14 +1114,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     load_plan(q, pc);
     load_plan(qn, pn);
     load_batch(pc, bc);
-    // kRowsAhead rows in flight ahead of the one processed (the buffers rotate
-    // with a period NB dividing the 4 rows of a quad, so each has fixed
-    // registers)
-    constexpr int NB = kRowsAhead == 1 ? 2 : 4;
-    // each has fixed registers)
-    u32x4 buf[NB][4];
-#pragma unroll
-    for (int d = 0; d < kRowsAhead; ++d) issue(q * kBlockRows + d, buf[d]);
+    // one row in flight ahead of the one processed, in two buffers that
+    // alternate within a quad, so each has fixed registers (two or three rows
+    // ahead measured no faster: 6.71-7.08 / 6.87-6.96 against 6.80-6.81 ms
+    // per C3 step on one box, profiles/r3f/ab_rows_ahead.log)
+    u32x4 buf[2][4];
+    issue(q * kBlockRows, buf[0]);
     for (;;) {
         // block q: plan pc and batch bc are resident; pn (block qn) landed
         // during the previous block: its record ends now, the plan of the
@@ -1152,15 +1146,15 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
                 // the next row: this block's, or the next block's first
-                const int ahead = st + kRowsAhead;
+                const int ahead = st + 1;
                 const uint64_t nrow = ahead < kSteps ? row_b + (uint64_t)ahead : qn * kBlockRows + (uint64_t)(ahead - kSteps);
-                issue(nrow, buf[(u + kRowsAhead) % NB]);
+                issue(nrow, buf[(u + 1) & 1]);
                 // keep the next row's loads here, ahead of this row's compute:
                 // left alone, the scheduler sinks them past most of the chain
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u % NB], rend_buf);
+                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u & 1], rend_buf);
             }
         }
         // the block's 64 rrow values, one coalesced store (rows past the end
@@ -1375,11 +1369,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         uint64_t fb;
     };
     auto issue = [&](const Geo &g, Dep &o) {
+#ifdef GCK_XP_HOTARENA
+        // experiment: every arena read from one hot 8 KiB region (wrong CRCs)
+        const uint8_t *hot = arena + ((g.w0 & 8191) & ~3ull);
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(hot);
+        const uint64_t hb = (uint64_t)(hot - arena), bsp_x = hb & ~15ull, bse_x = (hb + 64) & ~15ull;
+#define GCK_BSP bsp_x
+#define GCK_BSE bse_x
+#else
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + g.w0);
+#define GCK_BSP g.bsp
+#define GCK_BSE g.bse
+#endif
         // block holding byte rs - 1: only a record with a predecessor in its
         // file needs it (ft_prev; without one, bsp = rs and it is unused)
         o.vp = make_uint4(0, 0, 0, 0);
-        if (g.prev_same) o.vp = *reinterpret_cast<const uint4 *>(arena + g.bsp);
+        if (g.prev_same) o.vp = *reinterpret_cast<const uint4 *>(arena + GCK_BSP);
         // header + keys up to 24 B as three 16 B loads (dword aligned; the
         // arena is padded): every load instruction of a wave touches 64
         // records' lines, so the count of instructions, not bytes, is the cost
@@ -1396,7 +1401,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         }
         o.vend = make_uint4(0, 0, 0, 0);
         if (!g.have)
-            o.vend = *reinterpret_cast<const uint4 *>(arena + g.bse);
+            o.vend = *reinterpret_cast<const uint4 *>(arena + GCK_BSE);
+#undef GCK_BSP
+#undef GCK_BSE
         // row sums rend[fr .. fr + 11] the record crosses (up to three 16 B
         // loads, rend is padded; only the ones a record spanning rows uses:
         // most records lie inside one row)
