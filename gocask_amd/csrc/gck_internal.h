@@ -56,7 +56,6 @@ enum Phase {
     PH_PIPE = PH_END, // (time) device span of the whole run
     PH_HIDDEN,        // (time) pipelined: boundary .. records of groups 1.. on the side stream
     PH_WAIT,          // (time) pipelined: k_crc_rows launches waiting for their group's records
-    PH_FINSIDE,       // (time) k_finalize of the CRC pieces but the last, beside k_crc_rows
     PH_NPHASE
 };
 
@@ -71,11 +70,6 @@ struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipStream_t side = nullptr;  // the pipelined device path's boundary side
-    // k_finalize beside k_crc_rows: two CU-masked streams, the
-    // CRC pass on crc_cus CUs, the finalize of earlier row pieces on the
-    // other fin_cus (fins null: no masked streams, finalize after the pass)
-    hipStream_t crcs = nullptr, fins = nullptr;
-    int crc_cus = 0, fin_cus = 0;
     // end-of-run counters and results land here by a kernel's PCIe writes
     // (coherent pinned host memory, mapped): no DMA-engine copy, which would
     // queue behind any large H2D already queued (gck_replay's file groups)
@@ -108,7 +102,6 @@ struct Ctx {
     std::vector<uint32_t> grp_file, grp_chunk;
     std::vector<uint64_t> grp_row0, grp_row1;
     hipEvent_t ev_s0[kMaxGroups] = {}, ev_s1[kMaxGroups] = {}, ev_c0[kMaxGroups] = {}, ev_c1[kMaxGroups] = {};
-    hipEvent_t ev_f0[kMaxGroups] = {}, ev_f1[kMaxGroups] = {};  // finalize of CRC piece k beside the pass
 
     // chunk metadata
     uint32_t n_chunks = 0;

@@ -45,15 +45,6 @@ constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 // for four groups, 7.17 for two, 8.11 for eight.
 constexpr uint32_t kPipeGroups = 1;
 constexpr uint32_t kPipeFirstPermille = 500;
-// k_finalize beside k_crc_rows (ctx_run_device): the CRC pass in
-// row pieces on 7/8 of the CUs, the finalize of piece k on the other eighth
-// while piece k + 1 streams, the last piece's finalize on the whole chip.
-// Piece shares in permille of the rows, shrinking so each side finalize
-// (about 4x slower on an eighth of the CUs) ends before the next piece; only
-// runs of at least kFinMinRows rows are cut.  GCK_FSPLIT="p0,p1,..." (or
-// "0": no cut) selects another shape for measurements.
-constexpr uint32_t kFinSplit[] = {450, 300, 170, 80};
-constexpr uint64_t kFinMinRows = 1ull << 18;  // 1 GiB
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -281,7 +272,6 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                 if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
                 if (b0 + 3 * 4096 >= lim) break;
             }
-
             if (wb == kNone) break;
             // Candidates in scan order are lane l's bits, then lane l + 1's.
             // Every lane tests its own candidates in order, all lanes at once
@@ -636,27 +626,6 @@ __global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb
     if (t < kGbSlots + 2 * kMaxGroups + 2) gb[t] = 0;
     if (t < kMaxGroups) queue[t] = 0;
     if (t == 0) row_first[0] = 0;
-}
-
-// Record ranges of the CRC pieces (finalize beside the pass): piece k's records
-// are those whose last byte lies in its rows [cut[k], cut[k+1]), i.e.
-// [row_first[cut[k]], row_first[cut[k+1]]) (row_first is monotone), clamped to
-// the run's range rng; the last piece ends at rng[1].
-struct RowCuts {
-    uint64_t r[kMaxGroups + 1];
-};
-__global__ void k_fin_ranges(const uint32_t *__restrict__ row_first, RowCuts cut, uint32_t P,
-                             const uint64_t *__restrict__ rng, uint64_t *__restrict__ frng) {
-    const uint32_t k = threadIdx.x;
-    if (k >= P) return;
-    const uint64_t lo = rng[0], hi = rng[1];
-    auto at = [&](uint32_t j) {
-        const uint64_t v = row_first[cut.r[j]];
-        return v < lo ? lo : v > hi ? hi : v;
-    };
-    const uint64_t a = k == 0 ? lo : at(k), b = k + 1 == P ? hi : at(k + 1);
-    frng[2 * k] = a;
-    frng[2 * k + 1] = b > a ? b : a;
 }
 
 // The host bookkeeping of a run (core/db.go:110-140) for the files [f0, f1)
@@ -1616,41 +1585,12 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     GCK_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
-    // CU-masked streams for finalize beside the CRC pass: the side gets the
-    // top eighth of the mask's CU indices (GCK_FMASK=2: every eighth index);
-    // k_crc_rows on the other 7/8 ran as fast as on all CUs.
-    // Without them (the mask refused), finalize runs after the pass.
-    if (c->n_cu >= 64 && c->n_cu <= 1024) {
-        const char *fm = getenv("GCK_FMASK");
-        const bool every8 = fm && atoi(fm) == 2;
-        uint32_t mc[32] = {}, mf[32] = {};
-        int nc = 0, nfc = 0;
-        for (int i = 0; i < c->n_cu; ++i) {
-            const bool side = every8 ? (i & 7) == 7 : i >= c->n_cu - c->n_cu / 8;
-            (side ? mf : mc)[i >> 5] |= 1u << (i & 31);
-            ++(side ? nfc : nc);
-        }
-        const uint32_t words = (uint32_t)(c->n_cu + 31) / 32;
-        if (hipExtStreamCreateWithCUMask(&c->crcs, words, mc) == hipSuccess &&
-            hipExtStreamCreateWithCUMask(&c->fins, words, mf) == hipSuccess) {
-            c->crc_cus = nc;
-            c->fin_cus = nfc;
-        } else {
-            (void)hipGetLastError();
-            for (hipStream_t *st : {&c->crcs, &c->fins}) {
-                if (*st) (void)hipStreamDestroy(*st);
-                *st = nullptr;
-            }
-        }
-    }
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
     for (uint32_t g = 0; g < kMaxGroups; ++g) {
         GCK_HIP(hipEventCreate(&c->ev_s0[g]));
         GCK_HIP(hipEventCreate(&c->ev_s1[g]));
         GCK_HIP(hipEventCreate(&c->ev_c0[g]));
         GCK_HIP(hipEventCreate(&c->ev_c1[g]));
-        GCK_HIP(hipEventCreate(&c->ev_f0[g]));
-        GCK_HIP(hipEventCreate(&c->ev_f1[g]));
     }
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     // the constant tables are the same for every context: built once per process
@@ -1704,13 +1644,13 @@ static void ctx_free(Ctx *c) {
     c->up_cap = 0;
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t *evs : {c->ev_s0, c->ev_s1, c->ev_c0, c->ev_c1, c->ev_f0, c->ev_f1})
+    for (hipEvent_t *evs : {c->ev_s0, c->ev_s1, c->ev_c0, c->ev_c1})
         for (uint32_t g = 0; g < kMaxGroups; ++g)
             if (evs[g]) {
                 (void)hipEventDestroy(evs[g]);
                 evs[g] = nullptr;
             }
-    for (hipStream_t *st : {&c->stream, &c->side, &c->crcs, &c->fins}) {
+    for (hipStream_t *st : {&c->stream, &c->side}) {
         if (*st) (void)hipStreamDestroy(*st);
         *st = nullptr;
     }
@@ -1837,7 +1777,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure((kGbSlots + 4 * kMaxGroups + 2) * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure((kGbSlots + 2 * kMaxGroups + 2) * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_queue.ensure(kMaxGroups * 4 + 16)))
         return rc;
@@ -1973,9 +1913,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
                       bool queue_zeroed = false) {
     if (r1 <= r0) return GCK_OK;
     const uint64_t nb = (r1 - r0 + kBlockRows - 1) / kBlockRows;
-    // one workgroup per CU of the stream (k_crc_rows takes a CU's whole LDS)
-    const uint32_t cus = s == c->crcs && c->crc_cus ? (uint32_t)c->crc_cus : (uint32_t)c->n_cu;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)cus);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_crc_rows<<<grid, 1024, 0, s>>>(
@@ -1989,8 +1927,7 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
     if (!max_recs) return;
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
-    const uint64_t cus = s == c->fins && c->fin_cus ? (uint64_t)c->fin_cus : (uint64_t)c->n_cu;
-    const uint64_t want = nblk(max_recs, 256), res = cus * c->fin_blocks_per_cu;
+    const uint64_t want = nblk(max_recs, 256), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
     const uint32_t grid = (uint32_t)(want < res ? want : res);
     k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
@@ -2165,44 +2102,6 @@ __global__ void k_publish(const uint32_t *__restrict__ cnt, uint32_t *mbox) {
 // the finalize after the last group are exposed.  One group: everything on
 // the main stream, as before.
 constexpr int GCK_ERERUN = -1;
-
-// Row cuts of the CRC pass for finalize beside it (kFinSplit, GCK_FSPLIT):
-// the number of pieces P (1: no cut) and cut.r[0..P], whole row blocks.
-static uint32_t fin_cuts(const Ctx *c, uint64_t r0, uint64_t r1, RowCuts &cut) {
-    cut.r[0] = r0;
-    cut.r[1] = r1;
-    if (!c->fins || r1 <= r0) return 1;
-    uint32_t pm[kMaxGroups], P = 0;
-    bool forced = false;
-    if (const char *e = getenv("GCK_FSPLIT")) {
-        forced = true;
-        for (const char *q = e; *q && P < kMaxGroups;) {
-            const long v = strtol(q, const_cast<char **>(&q), 10);
-            if (v <= 0) break;
-            pm[P++] = (uint32_t)v;
-            if (*q == ',') ++q;
-            else break;
-        }
-    } else {
-        for (uint32_t v : kFinSplit) pm[P++] = v;
-    }
-    if (P < 2 || (!forced && r1 - r0 < kFinMinRows)) return 1;
-    uint64_t tot = 0;
-    for (uint32_t k = 0; k < P; ++k) tot += pm[k];
-    const uint64_t blocks = (r1 - r0 + kBlockRows - 1) / kBlockRows;
-    uint64_t acc = 0, prev = r0;
-    uint32_t n = 0;
-    for (uint32_t k = 0; k + 1 < P; ++k) {
-        acc += pm[k];
-        const uint64_t r = r0 + (blocks * acc / tot) * kBlockRows;
-        if (r <= prev || r >= r1) continue;  // empty piece: merged into the next
-        cut.r[++n] = r;
-        prev = r;
-    }
-    cut.r[++n] = r1;
-    return n;
-}
-
 static int ctx_run_device(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
@@ -2233,43 +2132,15 @@ static int ctx_run_device(Ctx *c) {
         GCK_HIP(hipEventRecord(c->ev_s1[g], s));
     }
     int rc;
-    RowCuts cut;
-    const uint32_t P = G == 1 ? fin_cuts(c, c->grp_row0[0], c->grp_row1[0], cut) : 1;
-    if (P > 1) {
-        // finalize beside the CRC pass: pieces on the masked CRC stream, the
-        // finalize of piece k on the side CUs once piece k has streamed
-        uint64_t *frng = rng + 2;
-        k_fin_ranges<<<1, 64, 0, m>>>(c->d_row_first.as<uint32_t>(), cut, P, rng, frng);
-        GCK_HIP(hipEventRecord(c->ev_c0[0], m));
-        GCK_HIP(hipStreamWaitEvent(c->crcs, c->ev_c0[0], 0));
-        GCK_HIP(hipStreamWaitEvent(c->fins, c->ev_c0[0], 0));
-        for (uint32_t k = 0; k < P; ++k) {
-            if (k) GCK_HIP(hipEventRecord(c->ev_c0[k], c->crcs));
-            if ((rc = launch_crc(c, c->crcs, cut.r[k], cut.r[k + 1], cap, k, true))) return rc;
-            GCK_HIP(hipEventRecord(c->ev_c1[k], c->crcs));
-            if (k + 1 < P) {
-                GCK_HIP(hipStreamWaitEvent(c->fins, c->ev_c1[k], 0));
-                GCK_HIP(hipEventRecord(c->ev_f0[k], c->fins));
-                launch_finalize(c, c->fins, frng + 2 * k, cap);
-                GCK_HIP(hipEventRecord(c->ev_f1[k], c->fins));
-            }
-        }
-        GCK_HIP(hipStreamWaitEvent(m, c->ev_c1[P - 1], 0));
-        GCK_HIP(hipStreamWaitEvent(m, c->ev_f1[P - 2], 0));
-        GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
-        launch_finalize(c, m, frng + 2 * (P - 1), cap);
-        GCK_HIP(hipEventRecord(c->ev[PH_END], m));
-    } else {
-        for (uint32_t g = 0; g < G; ++g) {
-            if (s != m) GCK_HIP(hipStreamWaitEvent(m, c->ev_s1[g], 0));
-            GCK_HIP(hipEventRecord(c->ev_c0[g], m));
-            if ((rc = launch_crc(c, m, c->grp_row0[g], c->grp_row1[g], cap, g, true))) return rc;
-            GCK_HIP(hipEventRecord(c->ev_c1[g], m));
-        }
-        GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
-        launch_finalize(c, m, rng, cap);
-        GCK_HIP(hipEventRecord(c->ev[PH_END], m));
+    for (uint32_t g = 0; g < G; ++g) {
+        if (s != m) GCK_HIP(hipStreamWaitEvent(m, c->ev_s1[g], 0));
+        GCK_HIP(hipEventRecord(c->ev_c0[g], m));
+        if ((rc = launch_crc(c, m, c->grp_row0[g], c->grp_row1[g], cap, g, true))) return rc;
+        GCK_HIP(hipEventRecord(c->ev_c1[g], m));
     }
+    GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
+    launch_finalize(c, m, rng, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_END], m));
     k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
     GCK_HIP(hipStreamSynchronize(m));
     GCK_HIP(hipGetLastError());
@@ -2296,19 +2167,10 @@ static int ctx_run_device(Ctx *c) {
     c->ms_phase[PH_SCAN] = el(c->ev[PH_SCAN], c->ev[PH_HOST]);
     c->ms_phase[PH_HOST] = el(c->ev[PH_HOST], c->ev[PH_RECORDS]);
     c->ms_phase[PH_RECORDS] = el(c->ev[PH_RECORDS], c->ev_s1[0]);
-    if (P > 1) {
-        // crc_rows: the pass (first piece start to last piece end); crc_wait:
-        // the side finalize still running after it; finalize_side: the side
-        // finalize launches
-        c->ms_phase[PH_CRC] = el(c->ev_c0[0], c->ev_c1[P - 1]);
-        c->ms_phase[PH_WAIT] = el(c->ev_c1[P - 1], c->ev[PH_FINAL]);
-        for (uint32_t k = 0; k + 1 < P; ++k) c->ms_phase[PH_FINSIDE] += el(c->ev_f0[k], c->ev_f1[k]);
-    } else {
-        for (uint32_t g = 0; g < G; ++g) {
-            c->ms_phase[PH_CRC] += el(c->ev_c0[g], c->ev_c1[g]);
-            c->ms_phase[PH_WAIT] += el(g ? c->ev_c1[g - 1] : c->ev_s1[0], c->ev_c0[g]);
-            if (g) c->ms_phase[PH_HIDDEN] += el(c->ev_s0[g], c->ev_s1[g]);
-        }
+    for (uint32_t g = 0; g < G; ++g) {
+        c->ms_phase[PH_CRC] += el(c->ev_c0[g], c->ev_c1[g]);
+        c->ms_phase[PH_WAIT] += el(g ? c->ev_c1[g - 1] : c->ev_s1[0], c->ev_c0[g]);
+        if (g) c->ms_phase[PH_HIDDEN] += el(c->ev_s0[g], c->ev_s1[g]);
     }
     c->ms_phase[PH_FINAL] = el(c->ev[PH_FINAL], c->ev[PH_END]);
     c->ms_phase[PH_PIPE] = el(c->ev[PH_BOUNDARY], c->ev[PH_END]);
@@ -2441,7 +2303,7 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
 
 const char *gck_phase_name(int phase) {
     static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows",
-                                  "finalize", "pipeline", "side_hidden", "crc_wait", "finalize_side"};
+                                  "finalize", "pipeline", "side_hidden", "crc_wait"};
     return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
