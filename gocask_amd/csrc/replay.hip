@@ -1163,24 +1163,14 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 // end, range end) reads its own end block.
 // ValuePos = lastOffset + 16 + KeySize mod 2^32 (core/keydir.go:25), with
 // lastOffset = carry + offset within the file.
-// a * b mod P (multmodp's product), branch-free: 32 unrolled steps of
-// p ^= b & -(bit of a); b *= x.  About 160 VALU and no SALU, where the early-exit
-// loop of multmodp diverges across lanes and branches on every bit.
-__device__ __forceinline__ uint32_t gf_mul(uint32_t a, uint32_t b) {
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 31; i >= 0; --i) {
-        p ^= b & (uint32_t)((int32_t)(a << (31 - i)) >> 31);  // bit i of a is x^(31-i)
-        if (i) b = (b >> 1) ^ (kPoly & (uint32_t)(-(int32_t)(b & 1u)));
-    }
-    return p;
-}
 // a * b mod P for a per-lane b and any a, by a 4-bit window over a:
 // M[v] = b * (v3 + v2 x + v1 x^2 + v0 x^3) (v = a nibble, its bit 3 the lower
 // power) in a wave-private LDS table, entry-major (entry v of lane l at
 // byte mw + 256 v + 4 l: each lane of a 32-lane group on its own bank), then
 // Horner from the highest-degree nibble with y * x^4 = (y >> 4) ^ R[y & 15].
-// About 60 VALU + 15 LDS writes + 15 LDS reads, against 160 VALU for gf_mul.
+// About 60 VALU + 15 LDS writes + 15 LDS reads, against ≈160 VALU for a
+// branch-free bit-serial product (measured slower in any of finalize's four
+// multiplies).
 // M[0] must be zero (written once per kernel); mw = the wave's region + 4 lane;
 // rb = the lane's copy of R (32 copies, entry e of copy l at + 128 e + 4 l:
 // conflict-free, where one 16-entry copy put 32 lanes on 16 banks).
@@ -1415,8 +1405,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             acc ^= z4096(Tz, h_acc);
         }
         // F(s, [rs, ve)) = ft ^ Z_{-(E-ve)}(acc)
-        const uint32_t xi = gf_mul_lds(ldsb, mw, rxb, Xi[64 + (g.d >> 6)], Xi[g.d & 63]);  // x^{-8d}
-        const uint32_t chain = ft ^ gf_mul_lds(ldsb, mw, rxb, xi, acc);
+        // (a bit-serial VALU product in place of any of these four measured
+        // slower: 0.47-0.64 ms against 0.46-0.47, profiles/r3j/ab_finvalu.log)
+        auto mul = [&](uint32_t a, uint32_t b) { return gf_mul_lds(ldsb, mw, rxb, a, b); };
+        const uint32_t xi = mul(Xi[64 + (g.d >> 6)], Xi[g.d & 63]);  // x^{-8d}
+        const uint32_t chain = ft ^ mul(xi, acc);
         // F(s, prefix): header + key bytes [rs, vs) as aligned words from
         // rs & ~3; the first word's bytes before rs are shifted out
         // (partial_word over its last 4 - lead bytes)
@@ -1437,12 +1430,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (nw >= 12) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
         // x^(8V) = xa[V >> 16] * x^(8 (V & 0xFF00)) * x^(8 (V & 0xFF))
-        uint32_t xv = gf_mul_lds(ldsb, mw, rxb, Xb[256 + ((V >> 8) & 0xFF)], Xb[V & 0xFF]);
-        if (V >= 65536) xv = gf_mul_lds(ldsb, mw, rxb, xhi, xv);
+        uint32_t xv = mul(Xb[256 + ((V >> 8) & 0xFF)], Xb[V & 0xFF]);
+        if (V >= 65536) xv = mul(xhi, xv);
         // crc = F(0, value) ^ crc32(0^V), crc32(0^V) = Z_V(~0) ^ ~0, and Z_V is
         // linear: one multiply covers the prefix and the init term (no
         // crc32(0^V) table load)
-        const uint32_t calc = chain ^ gf_mul_lds(ldsb, mw, rxb, xv, p ^ 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+        const uint32_t calc = chain ^ mul(xv, p ^ 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
         {
             // The wave's records are consecutive gck_recs (40 B each): staged in
             // LDS, then stored as 16 B per lane, 1 KiB contiguous per instruction
