@@ -88,21 +88,28 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
 // k_verify: a wavefront takes 64 items (one per lane: status, location, size,
 // expected CRC in one coalesced load each), then the CRC of every item still
 // GCK_OK in turn, all lanes on one value; a mismatch is GCK_ECRC_FAILED, a
-// match copies the value to dst + dst_off (if dst).
+// match copies the value to dst + dst_off (if dst).  Groups of 64 items: the
+// first one per wavefront static, the rest from an atomic queue (zeroed by
+// the caller), claimed one group ahead: value sizes are heavy-tailed, so a
+// fixed stride left the kernel waiting for the wavefronts that drew the
+// largest values.
 __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ arena, const uint32_t *__restrict__ g_slice,
                                                  uint64_t n,
                                                 const uint64_t *__restrict__ item,
                                                 const uint32_t *__restrict__ vsize,
                                                 const uint32_t *__restrict__ expect, int32_t *__restrict__ status,
                                                 uint32_t *__restrict__ crc_out, const uint64_t *__restrict__ dst_off,
-                                                uint8_t *__restrict__ dst) {
+                                                uint8_t *__restrict__ dst, uint32_t *__restrict__ queue) {
     __shared__ CrcTabs T;
     crc_tables(T, g_slice);
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0, lb1;
     slice_bases(lane, lb0, lb1);
     const uint64_t groups = (n + 63) >> 6, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); gi < groups; gi += waves) {
+    uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    uint32_t claim = 0;
+    if (gi < groups && lane == 0) claim = atomicAdd(queue, 1u);
+    while (gi < groups) {
         const uint64_t mine = (gi << 6) + lane;
         const bool have = mine < n;
         const bool ok = have && status[mine] == GCK_OK;
@@ -134,6 +141,8 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
             crc_out[mine] = crc;
             if (ok && crc != want) status[mine] = GCK_ECRC_FAILED;  // core/db.go:311-313
         }
+        gi = waves + (uint32_t)__builtin_amdgcn_readfirstlane((int)claim);
+        if (gi < groups && lane == 0) claim = atomicAdd(queue, 1u);
     }
 }
 
@@ -196,9 +205,11 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     }
     // one 1024-thread workgroup per CU (the tables take 132 KiB of LDS)
     const uint32_t grid = std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->n_cu);
+    uint32_t *queue = c->d_queue.as<uint32_t>() + kMaxGroups;  // (the replay's CRC queues are slots 0..)
+    GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_verify<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
-                                  c->d_gvoff.as<uint64_t>(), dvals);
+                                  c->d_gvoff.as<uint64_t>(), dvals, queue);
     GCK_HIP(hipEventRecord(b, s));
     GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
@@ -244,10 +255,12 @@ int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint
                                                        c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
                                                        c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                                        c->d_gexp.as<uint32_t>());
+    uint32_t *queue = c->d_queue.as<uint32_t>() + kMaxGroups;
+    GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_verify<<<(uint32_t)c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(),
                                                     c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>(),
                                                     c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(), nullptr,
-                                                    nullptr);
+                                                    nullptr, queue);
     GCK_HIP(hipEventRecord(b, s));
     std::vector<int32_t> st(status ? 0 : n);
     int32_t *sp = status ? status : st.data();
