@@ -181,7 +181,7 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
 // ahead is far below what HBM latency needs).  All control is wave-uniform;
 // every load is issued unconditionally (a dummy reload past the last stripe),
 // so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
-constexpr int kRing = 4;  // ring depths 2, 4 and 8 measured the same
+constexpr int kRing = 4;  // ring depths 2, 4 and 8 measured the same (again in round 3)
 template <class PtrOf, class Combine>
 __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const CrcTabs &t, uint32_t lb0,
                               uint32_t lb1, Combine combine) {
