@@ -52,7 +52,7 @@ def main():
     stats = {}
     for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv"))):
         stats[short(r["Name"])] = float(r["AverageNs"])
-    crc_key = next((k for k in summary if k.startswith("k_crc_rows<")), None)
+    crc_key = next((k for k in summary if (k == "k_crc_rows" or k.startswith("k_crc_rows<"))), None)
     crc = summary.get(crc_key, {})
     sr = next((v for k, v in summary.items() if k.startswith("k_stream_read")), {})
     out = {
@@ -62,7 +62,7 @@ def main():
         "crc_rows_hbm_bytes_per_launch": crc.get("FETCH_SIZE", 0) * 2048 or None,
         "crc_rows_write_bytes_per_launch": crc.get("WRITE_SIZE", 0) * 1024 or None,
         "stream_read_hbm_bytes_per_launch": sr.get("FETCH_SIZE", 0) * 2048 or None,
-        "crc_rows_avg_ns_rocprof": next((v for k, v in stats.items() if k.startswith("k_crc_rows<")), None),
+        "crc_rows_avg_ns_rocprof": next((v for k, v in stats.items() if (k == "k_crc_rows" or k.startswith("k_crc_rows<"))), None),
         "algorithmic_bytes_per_launch": (bench["config"]["bytes_per_gpu"] / bench["roofline"].get("launches_per_step", 1))
         if bench else None,
     }
