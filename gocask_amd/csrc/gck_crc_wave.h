@@ -119,6 +119,9 @@ struct CrcJob {
         b = p - pad - sh;
     }
 };
+// NT: non-temporal stripe loads (bytes read once); without, the lines stay in
+// L2 for a second read of the same bytes (the fused encoder's copy).
+template <bool NT = true>
 __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32_t d[5]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t v = (j << 10) + 16ull * lane;
@@ -128,7 +131,11 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32
         a = v + 16 <= jb.pad ? p0 : a;
     }
     // non-temporal stripe loads (scrub 4.92 -> 4.76-4.90 ms)
-    const u32x4_a4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(a));
+    u32x4_a4 x;
+    if constexpr (NT)
+        x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(a));
+    else
+        x = *reinterpret_cast<const u32x4_a4 *>(a);
     d[0] = x.x;
     d[1] = x.y;
     d[2] = x.z;
@@ -182,7 +189,7 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
 // every load is issued unconditionally (a dummy reload past the last stripe),
 // so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
 constexpr int kRing = 4;  // ring depths 2, 4 and 8 measured the same (again in round 3)
-template <class PtrOf, class Combine>
+template <bool NT = true, class PtrOf, class Combine>
 __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const CrcTabs &t, uint32_t lb0,
                               uint32_t lb1, Combine combine) {
     const uint32_t lane = threadIdx.x & 63;
@@ -194,7 +201,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
     CrcJob lj = job(lt);
     uint64_t ls = 0;
     auto load_next = [&](uint32_t d[5]) {
-        stripe_load(lj, ls, d);
+        stripe_load<NT>(lj, ls, d);
         if (lrem && ++ls == lj.J) {  // the next value (or stay on the last stripe: dummy reloads)
             lrem &= lrem - 1;
             if (lrem) {
