@@ -46,30 +46,28 @@ struct DBuf {
 };
 
 enum Phase {
-    PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds (pipelined: group 0's)
+    PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
     PH_SCAN,          // record slots per chunk, per-file summary
     PH_HOST,          // D2H summary + host bookkeeping (device path: k_account_grp)
     PH_RECORDS,       // k_row_fill, k_compact, k_row_tail
-    PH_CRC,           // k_crc_rows: the HBM-bound kernel (pipelined: every group's launch)
+    PH_CRC,           // k_crc_rows: the HBM-bound kernel
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
     PH_PIPE = PH_END, // (time) device span of the whole run
-    PH_HIDDEN,        // (time) pipelined: boundary .. records of groups 1.. on the side stream
-    PH_WAIT,          // (time) pipelined: k_crc_rows launches waiting for their group's records
     PH_NPHASE
 };
 
-// The device path runs file groups as a two-stream software pipeline: the
-// boundary side (boundary, scans, accounting, record table) of group g + 1
-// on a side stream while k_crc_rows streams group g.
-constexpr uint32_t kMaxGroups = 8;
-constexpr uint32_t kGbSlots = kMaxGroups + 1;  // d_gbase: the groups' record bases, then ranges
+// d_gbase: the record bases gb[0] (0) and gb[1], then the records' range
+// (clamped to capacity) and the run's range.
+constexpr uint32_t kGbSlots = 2, kGbWords = kGbSlots + 4;
+// d_queue: atomic work queues, zeroed before each use: k_crc_rows' row
+// blocks, k_verify's item groups.
+constexpr uint32_t kQueueCrc = 0, kQueueVerify = 1, kQueueSlots = 2;
 
 
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;  // the pipelined device path's boundary side
     // end-of-run counters and results land here by a kernel's PCIe writes
     // (coherent pinned host memory, mapped): no DMA-engine copy, which would
     // queue behind any large H2D already queued (gck_replay's file groups)
@@ -91,17 +89,6 @@ struct Ctx {
     std::vector<uint8_t> f_reset;
     std::vector<uint32_t> f_first_chunk, f_nchunks;
     uint64_t data_bytes = 0;
-    // file groups of the pipelined device path (ctx_layout): group g = files
-    // [grp_file[g], grp_file[g+1]), chunks [grp_chunk[g], grp_chunk[g+1]),
-    // CRC rows [grp_row0[g], grp_row1[g]); row grp_row1[g] of every group but
-    // the last is an empty gap row whose row_first the group's own records
-    // phase writes (k_crc_rows of group g reads it while group g + 1 is
-    // being built).  Cuts follow files that reset lastOffset.
-    uint32_t n_groups = 1;
-    bool pipeline = true;  // false: one group (gck_replay's pooled contexts)
-    std::vector<uint32_t> grp_file, grp_chunk;
-    std::vector<uint64_t> grp_row0, grp_row1;
-    hipEvent_t ev_s0[kMaxGroups] = {}, ev_s1[kMaxGroups] = {}, ev_c0[kMaxGroups] = {}, ev_c1[kMaxGroups] = {};
 
     // chunk metadata
     uint32_t n_chunks = 0;

@@ -205,7 +205,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     }
     // one 1024-thread workgroup per CU (the tables take 132 KiB of LDS)
     const uint32_t grid = std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->n_cu);
-    uint32_t *queue = c->d_queue.as<uint32_t>() + kMaxGroups;  // (the replay's CRC queues are slots 0..)
+    uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueVerify;
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_verify<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
@@ -255,7 +255,7 @@ int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint
                                                        c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
                                                        c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                                        c->d_gexp.as<uint32_t>());
-    uint32_t *queue = c->d_queue.as<uint32_t>() + kMaxGroups;
+    uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueVerify;
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_verify<<<(uint32_t)c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(),
                                                     c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>(),

@@ -27,6 +27,9 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -173,7 +176,25 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
     int rc = gck_plan_shards(sizes.data(), reset.data(), nfiles, ndev, ranges.data());
     if (rc) return rc;
     std::vector<Shard> sh(ndev);
+    // GCK_REPLAY_TRACE=1: the phases' wall times on stderr
+    const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto mark = [&](const char *what) {
+        if (trace)
+            fprintf(stderr, "gck_replay_multi %-14s %9.2f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    // the communicators come up on their own thread while the shards replay
+    // (ncclCommInitAll takes about a second; a later call with the same
+    // device list reuses them)
+    std::vector<ncclComm_t> comm;
+    int comm_rc = GCK_OK;
+    std::thread comm_th([&]() { comm_rc = comms_for(devs, comm); });
+    auto join_comm = [&]() {
+        if (comm_th.joinable()) comm_th.join();
+    };
     auto cleanup = [&]() {
+        join_comm();
         for (uint32_t s = 0; s < ndev; ++s) {
             if (sh[s].ctx) (void)hipSetDevice(sh[s].ctx->c.device);
             for (void *p : {sh[s].d_ents, sh[s].d_keys, sh[s].r_ents, sh[s].r_keys})
@@ -204,6 +225,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         replay_shard(0);
         for (auto &t : th) t.join();
     }
+    mark("replayed");
     for (uint32_t s = 0; s < ndev; ++s)
         if (sh[s].rc) {
             rc = sh[s].rc;
@@ -256,6 +278,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         }
         rc = gck_kd_pack(x.ctx, s, x.a, static_cast<gck_kd_entry *>(x.d_ents), ne, static_cast<uint8_t *>(x.d_keys), nk);
     }
+    mark("packed");
     // receive buffers: owner p gets partition p of every shard, in shard order
     std::vector<std::vector<uint64_t>> e_off(ndev, std::vector<uint64_t>(ndev + 1, 0)),
         k_off(ndev, std::vector<uint64_t>(ndev + 1, 0));
@@ -270,9 +293,10 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
             rc = GCK_ENOMEM;
     }
     // 4. the exchange: RCCL send / recv of every (shard, owner) pair in one group
+    join_comm();
+    mark("comms");
     if (!rc) {
-        std::vector<ncclComm_t> comm;
-        rc = comms_for(devs, comm);
+        rc = comm_rc;
         for (uint32_t s = 0; s < ndev && !rc; ++s) {  // packs done before the sends
             (void)hipSetDevice(devs[s]);
             if (hipStreamSynchronize((hipStream_t)gck_ctx_stream(sh[s].ctx)) != hipSuccess) rc = GCK_EDEVICE;
@@ -309,6 +333,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
             }
         }
     }
+    mark("exchanged");
     // 5. per owner, the merge; the live entries gathered in owner order
     std::vector<uint64_t> n_live(ndev, 0);
     for (uint32_t p = 0; p < ndev && !rc; ++p) {
@@ -339,7 +364,9 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         for (uint64_t i = 0; i < n; ++i) h[at + i] = ents[i].rec;
         at += n;
     }
+    mark("merged+fetched");
     cleanup();
+    mark("freed");
     if (rc) {
         if (h) (void)hipHostFree(h);
         memset(out, 0, sizeof(*out));

@@ -37,14 +37,6 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
-// device-path pipeline shape (ctx_layout, pipe_shape): file groups and the
-// first group's share of the bytes in permille.  One group: measured on C3
-// (DESIGN.md §7), the boundary side of later groups beside k_crc_rows slows
-// both (its dependent loads wait behind the stream: 0.36 ms per group alone,
-// 1.3-1.7 ms beside it; k_crc_rows 5.74 -> 6.31 ms), 7.09 -> 7.56 ms per step
-// for four groups, 7.17 for two, 8.11 for eight.
-constexpr uint32_t kPipeGroups = 1;
-constexpr uint32_t kPipeFirstPermille = 500;
 constexpr uint32_t kNibBase = 32768;
 
 // ---------------------------------------------------------------- helpers ---
@@ -623,8 +615,8 @@ __global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb
                            uint32_t *__restrict__ queue) {
     const uint32_t t = threadIdx.x;
     if (t < 32) cnt[t] = 0;
-    if (t < kGbSlots + 2 * kMaxGroups + 2) gb[t] = 0;
-    if (t < kMaxGroups) queue[t] = 0;
+    if (t < kGbWords) gb[t] = 0;
+    if (t == kQueueCrc) queue[t] = 0;
     if (t == 0) row_first[0] = 0;
 }
 
@@ -1577,14 +1569,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), 256, 0));
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    GCK_HIP(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
-    for (uint32_t g = 0; g < kMaxGroups; ++g) {
-        GCK_HIP(hipEventCreate(&c->ev_s0[g]));
-        GCK_HIP(hipEventCreate(&c->ev_s1[g]));
-        GCK_HIP(hipEventCreate(&c->ev_c0[g]));
-        GCK_HIP(hipEventCreate(&c->ev_c1[g]));
-    }
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
     // the constant tables are the same for every context: built once per process
     struct Tables {
@@ -1637,16 +1622,8 @@ static void ctx_free(Ctx *c) {
     c->up_cap = 0;
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t *evs : {c->ev_s0, c->ev_s1, c->ev_c0, c->ev_c1})
-        for (uint32_t g = 0; g < kMaxGroups; ++g)
-            if (evs[g]) {
-                (void)hipEventDestroy(evs[g]);
-                evs[g] = nullptr;
-            }
-    for (hipStream_t *st : {&c->stream, &c->side}) {
-        if (*st) (void)hipStreamDestroy(*st);
-        *st = nullptr;
-    }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    c->stream = nullptr;
 }
 
 // Layout tables from pinned, mapped host memory (Ctx::h_up) into device
@@ -1665,53 +1642,9 @@ __global__ void k_upload(const uint8_t *__restrict__ src, UpList l) {
         sg.dst[i] = s[i];
 }
 
-// File groups of the pipelined device path: G groups, the first holding
-// first_pm / 1000 of the bytes (its boundary side is the exposed part of the
-// pipeline), the rest about equal, each cut after a file that resets
-// lastOffset (core/db.go:117-119), so every group's lastOffset starts at 0.
-// Returns the cut file indices (cut[0] = 0, cut.back() = nfiles).
-static std::vector<uint32_t> plan_groups(const uint64_t *lens, const uint8_t *reset, uint32_t nf, uint32_t G,
-                                         uint32_t first_pm) {
-    std::vector<uint32_t> cut{0};
-    uint64_t tot = 0;
-    for (uint32_t f = 0; f < nf; ++f) tot += lens[f];
-    if (G > 1 && nf > 1 && tot) {
-        const double t0 = (double)tot * first_pm / 1000.0;
-        uint64_t acc = 0;
-        for (uint32_t f = 0; f + 1 < nf && cut.size() < G; ++f) {
-            acc += lens[f];
-            const uint32_t k = (uint32_t)cut.size();  // the boundary being placed
-            const double target = k == 1 ? t0 : t0 + ((double)tot - t0) * (k - 1) / (G - 1);
-            if (reset[f] && (double)acc >= target) cut.push_back(f + 1);
-        }
-    }
-    cut.push_back(nf);
-    return cut;
-}
-
-// Group count and first-group share of the pipeline (GCK_PIPE="G,first_permille"
-// overrides them for measurements).
-static void pipe_shape(uint32_t &G, uint32_t &first_pm) {
-    G = kPipeGroups;
-    first_pm = kPipeFirstPermille;
-    if (const char *e = getenv("GCK_PIPE")) {
-        unsigned a = 0, b = 0;
-        if (sscanf(e, "%u,%u", &a, &b) == 2 && a >= 1 && a <= kMaxGroups && b >= 1 && b < 1000) {
-            G = a;
-            first_pm = b;
-        }
-    }
-}
-
-// Place files (walk order) in the arena and build the chunk table and, for
-// the pipelined device path, the file groups (one empty gap row after every
-// group but the last).
+// Place files (walk order) in the arena and build the chunk table.
 int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after) {
     GCK_HIP(hipSetDevice(c->device));
-    uint32_t G = 1, first_pm = 500;
-    if (c->pipeline) pipe_shape(G, first_pm);
-    const std::vector<uint32_t> cut = plan_groups(lens, reset_after, nfiles, G, first_pm);
-    c->n_groups = (uint32_t)cut.size() - 1;
     c->nfiles = nfiles;
     c->f_base.assign(nfiles, 0);
     c->f_len.assign(lens, lens + nfiles);
@@ -1722,11 +1655,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     const uint64_t CB = c->opts.chunk_bytes;
     std::vector<uint32_t> ch_file;
     std::vector<uint64_t> ch_start, ch_end;
-    for (uint32_t f = 0, g = 0; f < nfiles; ++f) {
-        if (g + 1 < c->n_groups && f == cut[g + 1]) {
-            pos += kRow;  // the gap row after group g
-            ++g;
-        }
+    for (uint32_t f = 0; f < nfiles; ++f) {
         c->f_base[f] = pos;
         pos += (lens[f] + kRow - 1) / kRow * kRow;
         data += lens[f];
@@ -1743,15 +1672,6 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
     c->data_bytes = data;
     c->n_rows = pos / kRow;
     c->n_chunks = (uint32_t)ch_file.size();
-    c->grp_file = cut;
-    c->grp_chunk.assign(c->n_groups + 1, c->n_chunks);
-    c->grp_row0.assign(c->n_groups, 0);
-    c->grp_row1.assign(c->n_groups, c->n_rows);
-    for (uint32_t g = 0; g < c->n_groups && nfiles; ++g) {
-        c->grp_chunk[g] = c->f_first_chunk[cut[g]];
-        c->grp_row0[g] = c->f_base[cut[g]] / kRow;
-        if (g + 1 < c->n_groups) c->grp_row1[g] = c->f_base[cut[g + 1]] / kRow - 1;  // the gap row
-    }
     const uint64_t nc = c->n_chunks, nf = nfiles ? nfiles : 1;
     const uint64_t cap = c->opts.chunk_cap;
     int rc;
@@ -1770,9 +1690,9 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure((kGbSlots + 2 * kMaxGroups + 2) * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure(kGbWords * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
-        (rc = c->d_queue.ensure(kMaxGroups * 4 + 16)))
+        (rc = c->d_queue.ensure(kQueueSlots * 4)))
         return rc;
     // the tables, staged in pinned mapped host memory and copied by k_upload
     // on the context's stream (the previous upload has been consumed: the
@@ -2051,7 +1971,7 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
     launch_records(c, s, 0, nc, 0, c->n_rows, 0, nf, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
-    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, 0))) return rc;
+    if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, kQueueCrc))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
     launch_finalize(c, s, gbase, n_total);
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
@@ -2084,53 +2004,35 @@ __global__ void k_publish(const uint32_t *__restrict__ cnt, uint32_t *mbox) {
 // to its capacity, and the counters come back through the mapped mailbox.
 // Returns GCK_ERERUN when the run cannot be trusted as is (more records than
 // capacity, or speculation not settled by the device rounds): the caller then
-// reruns on the host path, whose result is exact.
-//
-// Software pipeline over the file groups (ctx_layout): the side stream builds
-// group after group -- boundary, scans, accounting, record table -- and
-// k_crc_rows of group g starts on the main stream as soon as group g's record
-// table is done, so the boundary side of groups 1.. runs beside the CRC
-// stream of earlier groups (those kernels use no LDS and few registers: they
-// fit next to k_crc_rows' 16 waves per CU).  Only group 0's boundary side and
-// the finalize after the last group are exposed.  One group: everything on
-// the main stream, as before.
+// reruns on the host path, whose result is exact.  Every phase on the one
+// stream, in order: running the boundary side of later files beside the CRC
+// pass of earlier ones, and the finalize of earlier rows beside the pass,
+// both measured slower.
 constexpr int GCK_ERERUN = -1;
 static int ctx_run_device(Ctx *c) {
     const auto t0 = std::chrono::steady_clock::now();
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t m = c->stream;
-    const uint32_t G = c->n_groups;
-    hipStream_t s = G > 1 ? c->side : m;
     const uint64_t cap = c->rec_cap;
+    const uint32_t nf = c->nfiles, nc = c->n_chunks;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
-    uint64_t *gb = c->d_gbase.as<uint64_t>();              // record base of group g: gb[g]
-    uint64_t *grng = gb + kGbSlots, *rng = grng + 2 * kMaxGroups;  // group ranges, the run's range
+    uint64_t *gb = c->d_gbase.as<uint64_t>();        // record base gb[0] (0) -> gb[1]
+    uint64_t *grng = gb + kGbSlots, *rng = grng + 2;  // the records' range (clamped), the run's range
     uint64_t *res = c->d_counters.as<uint64_t>() + 8;
     k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
-    if (s != m) GCK_HIP(hipStreamWaitEvent(s, c->ev[PH_BOUNDARY], 0));
-    for (uint32_t g = 0; g < G; ++g) {
-        const uint32_t f0 = c->grp_file[g], f1 = c->grp_file[g + 1], c0 = c->grp_chunk[g], c1 = c->grp_chunk[g + 1];
-        GCK_HIP(hipEventRecord(c->ev_s0[g], s));
-        launch_boundary(c, s, c0, c1, cnt + CNT_VAL);
-        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
-        launch_scan(c, s, c0, c1, f0, f1, gb + g, cap);
-        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
-        k_account_grp<<<1, 1, 0, s>>>(f0, f1, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
-                                      c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(),
-                                      c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
-                                      c->d_carry.as<uint32_t>(), gb + g, cap, res, grng + 2 * g, rng);
-        if (g == 0) GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-        launch_records(c, s, c0, c1, c->grp_row0[g], c->grp_row1[g], f0, f1, grng + 2 * g, cap);
-        GCK_HIP(hipEventRecord(c->ev_s1[g], s));
-    }
+    launch_boundary(c, m, 0, nc, cnt + CNT_VAL);
+    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
+    launch_scan(c, m, 0, nc, 0, nf, gb, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_HOST], m));
+    k_account_grp<<<1, 1, 0, m>>>(0, nf, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
+                                  c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
+                                  c->d_fnrec.as<uint64_t>(), c->d_carry.as<uint32_t>(), gb, cap, res, grng, rng);
+    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], m));
+    launch_records(c, m, 0, nc, 0, c->n_rows, 0, nf, grng, cap);
+    GCK_HIP(hipEventRecord(c->ev[PH_CRC], m));
     int rc;
-    for (uint32_t g = 0; g < G; ++g) {
-        if (s != m) GCK_HIP(hipStreamWaitEvent(m, c->ev_s1[g], 0));
-        GCK_HIP(hipEventRecord(c->ev_c0[g], m));
-        if ((rc = launch_crc(c, m, c->grp_row0[g], c->grp_row1[g], cap, g, true))) return rc;
-        GCK_HIP(hipEventRecord(c->ev_c1[g], m));
-    }
+    if ((rc = launch_crc(c, m, 0, c->n_rows, cap, kQueueCrc, true))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
     launch_finalize(c, m, rng, cap);
     GCK_HIP(hipEventRecord(c->ev[PH_END], m));
@@ -2150,23 +2052,15 @@ static int ctx_run_device(Ctx *c) {
     c->n_fixups = h[CNT_FIXUP];
     c->n_overflow = h[CNT_STAGE];
     c->n_crc_fail = h[CNT_REJECT];
-    auto el = [](hipEvent_t a, hipEvent_t b) {
-        float ms = 0;
-        (void)hipEventElapsedTime(&ms, a, b);
-        return (double)ms;
-    };
     for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
-    c->ms_phase[PH_BOUNDARY] = el(c->ev[PH_BOUNDARY], c->ev[PH_SCAN]);
-    c->ms_phase[PH_SCAN] = el(c->ev[PH_SCAN], c->ev[PH_HOST]);
-    c->ms_phase[PH_HOST] = el(c->ev[PH_HOST], c->ev[PH_RECORDS]);
-    c->ms_phase[PH_RECORDS] = el(c->ev[PH_RECORDS], c->ev_s1[0]);
-    for (uint32_t g = 0; g < G; ++g) {
-        c->ms_phase[PH_CRC] += el(c->ev_c0[g], c->ev_c1[g]);
-        c->ms_phase[PH_WAIT] += el(g ? c->ev_c1[g - 1] : c->ev_s1[0], c->ev_c0[g]);
-        if (g) c->ms_phase[PH_HIDDEN] += el(c->ev_s0[g], c->ev_s1[g]);
+    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
+        c->ms_phase[p] = ms;
     }
-    c->ms_phase[PH_FINAL] = el(c->ev[PH_FINAL], c->ev[PH_END]);
-    c->ms_phase[PH_PIPE] = el(c->ev[PH_BOUNDARY], c->ev[PH_END]);
+    float span = 0;
+    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
+    c->ms_phase[PH_PIPE] = span;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
@@ -2296,7 +2190,7 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
 
 const char *gck_phase_name(int phase) {
     static const char *names[] = {"boundary", "scan", "host_sync", "records", "crc_rows",
-                                  "finalize", "pipeline", "side_hidden", "crc_wait"};
+                                  "finalize", "pipeline"};
     return phase >= 0 && phase < PH_NPHASE ? names[phase] : "";
 }
 
@@ -2545,9 +2439,6 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
             lens[k] = files[f0 + k].len;
             reset[k] = files[f0 + k].reset_after ? 1 : 0;
         }
-        // (the contexts already pipeline against the H2D of later groups on
-        // one shared run stream: no second stream per context)
-        c->pipeline = false;
         int r;
         if ((r = ctx_layout(c, lens.data(), n, reset.data()))) return r;
         // a fresh context would take the host path on its first run, whose

@@ -40,6 +40,9 @@ try:
                 raise SystemExit(p.stderr)
             row = json.loads(p.stdout.strip().splitlines()[-1])
             row["rep"] = r
+            tr = [l for l in p.stderr.splitlines() if l.startswith("gck_replay")]
+            if tr:  # GCK_REPLAY_TRACE=1: the library's phase marks
+                row["trace"] = tr
             out.append(row)
             print(json.dumps(row), flush=True)
 finally:
