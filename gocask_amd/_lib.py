@@ -51,7 +51,7 @@ assert KD_ENTRY_DTYPE.itemsize == 64
 
 # Every symbol include/gocask_hip.h declares (tests check the .so exports them).
 EXPORTED = [
-    "gck_replay", "gck_replay_into", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run",
+    "gck_replay", "gck_replay_into", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run", "gck_ctx_phase_timing",
     "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_ctx_compact", "gck_ctx_fetch_compact", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_replay_multi", "gck_plan_shards", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
     "gck_ctx_read_file", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
@@ -110,6 +110,8 @@ class GckStats(ctypes.Structure):
         ("final_last_offset", ctypes.c_uint32),
         ("n_files", ctypes.c_uint32),
         ("reserved", ctypes.c_uint32),
+        ("n_runs", ctypes.c_uint64),
+        ("ms_crc_rows_sum", ctypes.c_double),
     ]
 
 
@@ -177,6 +179,7 @@ def load():
         "gck_ctx_destroy": (None, [vp]),
         "gck_ctx_load": (ctypes.c_int, [vp, P(GckFile), ctypes.c_uint32]),
         "gck_ctx_run": (ctypes.c_int, [vp]),
+        "gck_ctx_phase_timing": (ctypes.c_int, [vp, ctypes.c_int]),
         "gck_ctx_fetch": (ctypes.c_int, [vp, P(GckResult)]),
         "gck_ctx_fetch_into": (ctypes.c_int, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
         "gck_ctx_keydir": (ctypes.c_int, [vp, ctypes.c_uint32, P(ctypes.c_uint64), P(ctypes.c_double)]),

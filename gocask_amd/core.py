@@ -515,7 +515,12 @@ class ReplayContext:
                     n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
                     device_path=bool(s.device_path), n_reruns=s.n_reruns, status=s.status, err_file=s.err_file,
                     err_off=s.err_off, files_walked=s.files_walked, final_last_offset=s.final_last_offset,
-                    n_files=s.n_files)
+                    n_files=s.n_files, n_runs=s.n_runs, ms_crc_rows_sum=s.ms_crc_rows_sum)
+
+    def phase_timing(self, on=True):
+        """Events between every phase of the next runs (stats()['ms_phase'] per
+        phase); off (the default) times only the CRC pass and the whole run."""
+        check(self._L.gck_ctx_phase_timing(self._h, 1 if on else 0))
 
     def stream_read_ceiling(self, iters=10):
         """Plain streaming read of the resident arena (measurement helper,

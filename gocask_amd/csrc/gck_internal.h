@@ -142,6 +142,9 @@ struct Ctx {
     bool device_path = false;  // the last run had no host round trip (ctx_run_device)
     uint32_t n_reruns = 0;     // device-only runs redone on the host path
     double ms_total = 0, ms_phase[PH_NPHASE] = {};
+    bool phase_timing = false;  // an event between every phase (gck_ctx_phase_timing)
+    double ms_crc_sum = 0;      // k_crc_rows event time summed over runs
+    uint64_t n_runs = 0;
     hipEvent_t ev[PH_END + 1] = {};
 
 

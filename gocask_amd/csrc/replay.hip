@@ -475,11 +475,8 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                     ch_wend);
 }
 
-// Exclusive scan of per-chunk record counts -> rec_base[0..n], offset by a
-// device-resident base (the records of earlier file groups), without LDS (so
-// the kernels can share CUs with k_crc_rows, which holds all of it):
-// one wavefront per block of 4096 counts, one wavefront over the block totals,
-// then an add-back.  rec_base[n] and *base_out = base + total.
+// Exclusive scan of per-chunk record counts -> rec_base[0..n] (one wavefront
+// per block of kScanBlock counts).
 constexpr uint32_t kScanBlock = 4096;
 
 // Inclusive prefix sum over the 64 lanes (DPP row shifts + row broadcasts).
@@ -493,21 +490,82 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     return v;
 }
 
-// Lane l owns the 64 consecutive counts at b0 + 64 l: all of them are loaded
-// at once (one memory round trip per block; a loop of 64-wide steps waited
-// for each step's load: 25 us for C3's 64 Ki chunks), summed per lane, the
-// lane totals scanned over the wave (64-bit: split in 24-bit halves, as
-// k_scan_top), and the lane writes its 64 bases.  Vector loads and stores
-// where the group's chunk offset leaves them 16 B aligned.
-__global__ __launch_bounds__(64) void k_scan_local(const uint32_t *__restrict__ ch_count,
-                                                   uint64_t *__restrict__ rec_base, uint64_t *__restrict__ bsum,
-                                                   uint32_t n) {
+// 64-bit inclusive prefix sum over the lanes (values < 2^48: two 24-bit halves)
+__device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
+    const uint32_t lo = wave_incl_sum((uint32_t)(v & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(v >> 24));
+    return ((uint64_t)hi << 24) + lo;
+}
+
+// The host bookkeeping of a run (core/db.go:110-140) on the device, so a run
+// needs no host round trip.  Per file the lastOffset carried in (reset after
+// every file but the active one, core/db.go:117-119), the first startup error
+// (it aborts filepath.Walk: later files contribute nothing, disk.go:134-141),
+// the record range and the run's results.  One lane; res (u64): 0 status,
+// 1 error file, 2 error offset, 3 files walked, 4 final lastOffset, 5 records
+// (unclamped); grng = the record range [0, hi) clamped to cap, rng the same.
+__device__ void account_run(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
+                            const uint32_t *fterm, const uint64_t *ftpos, const uint64_t *ffirst,
+                            const uint64_t *fnrec, uint32_t *__restrict__ carry, uint64_t cap,
+                            uint64_t *__restrict__ res, uint64_t *__restrict__ grng, uint64_t *__restrict__ rng) {
+    uint32_t last = 0, walked = nf;
+    uint64_t n_end = 0;
+    for (uint32_t f = 0; f < nf; ++f) {
+        carry[f] = last;
+        const uint64_t valid = fterm[f] != T_NONE ? ftpos[f] : flen[f];
+        n_end = ffirst[f] + fnrec[f];
+        last += (uint32_t)valid;
+        if (fterm[f] == T_ERR) {
+            res[0] = GCK_EUNEXPECTED_EOF;
+            res[1] = f;
+            res[2] = ftpos[f];
+            walked = f + 1;
+            break;
+        }
+        if (freset[f]) last = 0;
+    }
+    res[3] = walked;
+    res[4] = last;
+    res[5] = n_end;
+    grng[0] = 0;
+    grng[1] = n_end < cap ? n_end : cap;
+    rng[0] = 0;
+    rng[1] = grng[1];
+}
+
+// Record slots, file summaries and (device path) the run's bookkeeping in one
+// launch (four to five launches before, each ~5 us of dispatch for ~1 us of
+// work).  Block b of the scan is the b-th wavefront to arrive (a ticket), so
+// the single-pass look-back only ever waits on wavefronts that are already
+// running: each publishes its block total at once and its inclusive prefix as
+// soon as it knows it (lb[b]: value | kLbAgg or kLbInc).  The wavefront that
+// finishes last (a second ticket) writes the per-file summaries -- records
+// of the file and the terminal condition of its last non-empty chunk -- then,
+// with acct set, runs account_run, and leaves lb and the tickets zeroed for
+// the next launch.  Per lane 64 consecutive counts, loaded at once (vector
+// loads where aligned).  rec_base[n] and *base_out = min(total, cap); a total
+// past cap is flagged in *overflow (the exact host path reruns).
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+__global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__ ch_count, uint64_t *rec_base,
+                                                    uint32_t n, uint64_t *lb, uint64_t *base_out, uint64_t cap,
+                                                    uint32_t *__restrict__ overflow,
+                                                    const uint32_t *__restrict__ f_first_chunk,
+                                                    const uint32_t *__restrict__ f_nchunks,
+                                                    const uint64_t *__restrict__ ch_entry,
+                                                    const uint32_t *__restrict__ ch_term,
+                                                    const uint64_t *__restrict__ ch_tpos, uint32_t *f_term,
+                                                    uint64_t *f_tpos, uint64_t *f_first_rec, uint64_t *f_nrec,
+                                                    uint32_t nfiles, int acct, const uint64_t *__restrict__ flen,
+                                                    const uint32_t *__restrict__ freset, uint32_t *carry,
+                                                    uint64_t *res, uint64_t *grng, uint64_t *rng) {
     static_assert(kScanBlock == 64 * 64, "a lane owns 64 counts");
-    const uint32_t lane = threadIdx.x;
-    const uint32_t i0 = blockIdx.x * kScanBlock + lane * 64;
+    const uint32_t lane = threadIdx.x, nb = gridDim.x;
+    uint32_t *tickets = reinterpret_cast<uint32_t *>(lb + nb);
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(&tickets[0], 1u);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    const uint32_t i0 = b * kScanBlock + lane * 64;
     uint32_t v[64];
     const bool vec_in = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(ch_count + i0) & 15) == 0;
-    const bool vec_out = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(rec_base + i0) & 15) == 0;
     if (vec_in) {
         const uint4 *src = reinterpret_cast<const uint4 *>(ch_count + i0);
 #pragma unroll
@@ -525,20 +583,44 @@ __global__ __launch_bounds__(64) void k_scan_local(const uint32_t *__restrict__ 
     uint64_t tot = 0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) tot += v[k];
-    const uint32_t lo = wave_incl_sum((uint32_t)(tot & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(tot >> 24));
-    const uint64_t inc = ((uint64_t)hi << 24) + lo;
-    uint64_t run = inc - tot;  // this lane's first base within the block
+    const uint64_t inc = wave_incl_sum64(tot);
+    const uint64_t btot = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(inc >> 32), 63) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)inc, 63);
+    // the block's exclusive base: look back over the published blocks
+    uint64_t excl = 0;
+    if (lane == 0) {
+        if (b == 0) {
+            __hip_atomic_store(&lb[0], btot | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&lb[b], btot | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t j = (int64_t)b - 1; j >= 0;) {
+                const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(w & (kLbAgg | kLbInc))) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += w & kLbVal;
+                if (w & kLbInc) break;
+                --j;
+            }
+            __hip_atomic_store(&lb[b], (excl + btot) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    excl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(excl >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)excl, 0);
+    uint64_t run = excl + inc - tot;  // this lane's first base
+    const bool vec_out = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(rec_base + i0) & 15) == 0;
     if (vec_out) {
         u32x4 *dst = reinterpret_cast<u32x4 *>(rec_base + i0);
 #pragma unroll
         for (int k = 0; k < 32; ++k) {
-            const uint64_t a = run, b = run + v[2 * k];
-            run = b + v[2 * k + 1];
+            const uint64_t a = run, c2 = run + v[2 * k];
+            run = c2 + v[2 * k + 1];
             u32x4 o;
             o.x = (uint32_t)a;
             o.y = (uint32_t)(a >> 32);
-            o.z = (uint32_t)b;
-            o.w = (uint32_t)(b >> 32);
+            o.z = (uint32_t)c2;
+            o.w = (uint32_t)(c2 >> 32);
             dst[k] = o;
         }
     } else {
@@ -548,64 +630,43 @@ __global__ __launch_bounds__(64) void k_scan_local(const uint32_t *__restrict__ 
             run += v[k];
         }
     }
-    if (lane == 63) bsum[blockIdx.x] = inc;
-}
-
-__global__ __launch_bounds__(64) void k_scan_top(uint64_t *__restrict__ bsum, uint32_t nb,
-                                                 const uint64_t *__restrict__ base_in, uint64_t *__restrict__ base_out,
-                                                 uint64_t *__restrict__ rec_base, uint32_t n, uint64_t cap,
-                                                 uint32_t *__restrict__ overflow) {
-    const uint32_t lane = threadIdx.x;
-    uint64_t run = *base_in;
-    for (uint32_t i0 = 0; i0 < nb; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint64_t v = i < nb ? bsum[i] : 0u;
-        // block totals can exceed 32 bits in sum: scan the two halves
-        const uint32_t lo = wave_incl_sum((uint32_t)(v & 0xFFFFFFu));
-        const uint32_t hi = wave_incl_sum((uint32_t)(v >> 24));
-        const uint64_t inc = ((uint64_t)hi << 24) + lo;
-        if (i < nb) bsum[i] = run + inc - v;
-        run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
-               (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
-    }
-    if (lane == 0) {
+    if (b == nb - 1 && lane == 0) {
         // past the record-table capacity the range is clamped (later kernels
         // stay in bounds) and the run is flagged for the exact synchronous path
-        if (run > cap) atomicAdd(overflow, 1u);
-        rec_base[n] = min(run, cap);
-        *base_out = min(run, cap);
+        const uint64_t total = excl + btot;
+        if (total > cap) atomicAdd(overflow, 1u);
+        rec_base[n] = min(total, cap);
+        *base_out = min(total, cap);
     }
-}
-
-__global__ void k_scan_add(uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ bsum, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) rec_base[i] += bsum[i / kScanBlock];
-}
-
-// Per-file summary: records of the file and its terminal condition.
-__global__ void k_file_summary(const uint32_t *__restrict__ f_first_chunk,
-                               const uint32_t *__restrict__ f_nchunks,
-                               const uint64_t *__restrict__ rec_base, const uint64_t *__restrict__ ch_entry,
-                               const uint32_t *__restrict__ ch_term, const uint64_t *__restrict__ ch_tpos,
-                               uint32_t *f_term, uint64_t *f_tpos, uint64_t *f_first_rec, uint64_t *f_nrec,
-                               uint32_t nfiles) {
-    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= nfiles) return;
-    const uint32_t fc = f_first_chunk[f], nc = f_nchunks[f];
-    f_first_rec[f] = rec_base[fc];
-    f_nrec[f] = rec_base[fc + nc] - rec_base[fc];
-    uint32_t term = T_NONE;
-    uint64_t tpos = 0;
-    // the terminal chunk is the last non-empty chunk of the file
-    for (int64_t k = (int64_t)fc + nc - 1; k >= (int64_t)fc; --k) {
-        if (ch_entry[k] != kNone) {
-            term = ch_term[k];
-            tpos = ch_tpos[k];
-            break;
+    // the last wavefront to finish sees every block's bases
+    __threadfence();
+    uint32_t dn = 0;
+    if (lane == 0) dn = atomicAdd(&tickets[1], 1u);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)dn) != nb - 1) return;
+    __threadfence();
+    for (uint32_t f = lane; f < nfiles; f += 64) {
+        const uint32_t fc = f_first_chunk[f], nc = f_nchunks[f];
+        const uint64_t r0 = rec_base[fc], r1 = rec_base[fc + nc];
+        f_first_rec[f] = r0;
+        f_nrec[f] = r1 - r0;
+        uint32_t term = T_NONE;
+        uint64_t tpos = 0;
+        // the terminal chunk is the last non-empty chunk of the file
+        for (int64_t k = (int64_t)fc + nc - 1; k >= (int64_t)fc; --k) {
+            if (ch_entry[k] != kNone) {
+                term = ch_term[k];
+                tpos = ch_tpos[k];
+                break;
+            }
         }
+        f_term[f] = term;
+        f_tpos[f] = tpos;
     }
-    f_term[f] = term;
-    f_tpos[f] = tpos;
+    for (uint32_t k = lane; k < nb + 1; k += 64) lb[k] = 0;  // lb and both tickets
+    __threadfence();
+    __builtin_amdgcn_wave_barrier();
+    if (acct && lane == 0)
+        account_run(nfiles, flen, freset, f_term, f_tpos, f_first_rec, f_nrec, carry, cap, res, grng, rng);
 }
 
 // Zero the run's counters / results (32 u32: status GCK_OK = 0), the group
@@ -618,52 +679,6 @@ __global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb
     if (t < kGbWords) gb[t] = 0;
     if (t == kQueueCrc) queue[t] = 0;
     if (t == 0) row_first[0] = 0;
-}
-
-// The host bookkeeping of a run (core/db.go:110-140) for the files [f0, f1)
-// of one group, on the device so a run needs no host round trip; groups run
-// in walk order.  Per file the lastOffset carried in (reset after every file
-// but the active one, core/db.go:117-119; a group starts after a resetting
-// file, so at 0), the first startup error (it aborts filepath.Walk: later
-// files and groups contribute nothing, disk.go:134-141), the group's record
-// range and the run's results so far.  One thread; res (u64): 0 status,
-// 1 error file, 2 error offset, 3 files walked, 4 final lastOffset, 5 records
-// (unclamped); gb = the group's record base; grng = its record range [lo, hi)
-// clamped to cap; rng = the run's [0, hi).
-__global__ void k_account_grp(uint32_t f0, uint32_t f1, const uint64_t *__restrict__ flen,
-                              const uint32_t *__restrict__ freset, const uint32_t *__restrict__ fterm,
-                              const uint64_t *__restrict__ ftpos, const uint64_t *__restrict__ ffirst,
-                              const uint64_t *__restrict__ fnrec, uint32_t *__restrict__ carry,
-                              const uint64_t *__restrict__ gb, uint64_t cap, uint64_t *__restrict__ res,
-                              uint64_t *__restrict__ grng, uint64_t *__restrict__ rng) {
-    const uint64_t lo = gb[0] < cap ? gb[0] : cap;
-    if (res[0] != GCK_OK) {  // an earlier group hit a startup error
-        grng[0] = grng[1] = lo;
-        return;
-    }
-    uint32_t last = 0, walked = f1;
-    uint64_t n_end = gb[0];
-    for (uint32_t f = f0; f < f1; ++f) {
-        carry[f] = last;
-        const uint64_t valid = fterm[f] != T_NONE ? ftpos[f] : flen[f];
-        n_end = ffirst[f] + fnrec[f];
-        last += (uint32_t)valid;
-        if (fterm[f] == T_ERR) {
-            res[0] = GCK_EUNEXPECTED_EOF;
-            res[1] = f;
-            res[2] = ftpos[f];
-            walked = f + 1;
-            break;
-        }
-        if (freset[f]) last = 0;
-    }
-    res[3] = walked;
-    res[4] = last;
-    res[5] = n_end;
-    grng[0] = lo;
-    grng[1] = n_end < cap ? n_end : cap;
-    rng[0] = 0;
-    rng[1] = grng[1];
 }
 
 // row_first[row] = the first record whose value ends after the row's first
@@ -1689,11 +1704,14 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_wend.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
-        (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + nf + 2) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
+        (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + 4) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
         (rc = c->d_gbase.ensure(kGbWords * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_queue.ensure(kQueueSlots * 4)))
         return rc;
+    // k_scan_chunks' look-back words and tickets start zeroed (each launch
+    // leaves them so)
+    GCK_HIP(hipMemsetAsync(c->d_bsum.p, 0, c->d_bsum.cap, c->stream));
     // the tables, staged in pinned mapped host memory and copied by k_upload
     // on the context's stream (the previous upload has been consumed: the
     // stream is drained first, and runs are synchronous)
@@ -1779,22 +1797,19 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
     }
 }
 
-// Record slots of chunks [c0, c1) after the records of earlier groups
-// (gbase[0] -> gbase[1]), and the summary of files [f0, f1).
-static void launch_scan(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t f0, uint32_t f1, uint64_t *gbase,
-                        uint64_t cap) {
-    const uint32_t n = c1 - c0, nb = nblk(n, kScanBlock);
-    uint64_t *bsum = c->d_bsum.as<uint64_t>() + c0 / kScanBlock + f0;  // disjoint per group
-    if (nb) k_scan_local<<<nb, 64, 0, s>>>(c->d_ch_count.as<uint32_t>() + c0, c->d_rec_base.as<uint64_t>() + c0, bsum, n);
-    k_scan_top<<<1, 64, 0, s>>>(bsum, nb, gbase, gbase + 1, c->d_rec_base.as<uint64_t>() + c0, n, cap,
-                                c->d_counters.as<uint32_t>() + CNT_CAP);
-    if (n) k_scan_add<<<nblk(n, 256), 256, 0, s>>>(c->d_rec_base.as<uint64_t>() + c0, bsum, n);
-    if (f1 > f0)
-        k_file_summary<<<nblk(f1 - f0, 64), 64, 0, s>>>(
-            c->d_ffirst.as<uint32_t>() + f0, c->d_fnch.as<uint32_t>() + f0, c->d_rec_base.as<uint64_t>(),
-            c->d_ch_entry.as<uint64_t>(), c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-            c->d_fterm.as<uint32_t>() + f0, c->d_ftpos.as<uint64_t>() + f0, c->d_ffirstrec.as<uint64_t>() + f0,
-            c->d_fnrec.as<uint64_t>() + f0, f1 - f0);
+// Record slots of every chunk, the file summaries and, with acct (the device
+// path), the run's bookkeeping: one launch of k_scan_chunks.  gbase[1] = the
+// record total (clamped to cap); grng / rng as account_run.
+static void launch_scan(Ctx *c, hipStream_t s, uint64_t *gbase, uint64_t cap, bool acct, uint64_t *res = nullptr,
+                        uint64_t *grng = nullptr, uint64_t *rng = nullptr) {
+    const uint32_t n = c->n_chunks, nb = std::max<uint32_t>(1, nblk(n, kScanBlock));
+    k_scan_chunks<<<nb, 64, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), n,
+                                    c->d_bsum.as<uint64_t>(), gbase + 1, cap, c->d_counters.as<uint32_t>() + CNT_CAP,
+                                    c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
+                                    c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
+                                    c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
+                                    c->nfiles, acct ? 1 : 0, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
+                                    c->d_carry.as<uint32_t>(), res, grng, rng);
 }
 
 // Record table of chunks [c0, c1) and row index (row_first) of rows [r0, r1]
@@ -1926,7 +1941,7 @@ static int ctx_run_host(Ctx *c) {
     launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
     const uint64_t big_cap = ~0ull >> 1;
-    launch_scan(c, s, 0, nc, 0, nf, gbase, big_cap);
+    launch_scan(c, s, gbase, big_cap, false);
     GCK_HIP(hipEventRecord(c->ev[PH_HOST], s));
 
     std::vector<uint32_t> fterm, carry(nf);
@@ -1948,7 +1963,7 @@ static int ctx_run_host(Ctx *c) {
         GCK_HIP(hipStreamSynchronize(s));
         left = v;
         if (!left) {
-            launch_scan(c, s, 0, nc, 0, nf, gbase, big_cap);
+            launch_scan(c, s, gbase, big_cap, false);
             if (read_file_summaries(c, s, fterm, ftpos, ffirst, fnrec)) return GCK_EDEVICE;
             GCK_HIP(hipMemcpyAsync(hcnt, cnt, 64, hipMemcpyDeviceToHost, s));
             GCK_HIP(hipStreamSynchronize(s));
@@ -1989,6 +2004,8 @@ static int ctx_run_host(Ctx *c) {
     float span = 0;
     (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
     c->ms_phase[PH_PIPE] = span;
+    c->ms_crc_sum += c->ms_phase[PH_CRC];
+    ++c->n_runs;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
 }
@@ -2019,16 +2036,16 @@ static int ctx_run_device(Ctx *c) {
     uint64_t *gb = c->d_gbase.as<uint64_t>();        // record base gb[0] (0) -> gb[1]
     uint64_t *grng = gb + kGbSlots, *rng = grng + 2;  // the records' range (clamped), the run's range
     uint64_t *res = c->d_counters.as<uint64_t>() + 8;
-    k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
+    // events: the run's span and the CRC pass always (bench.py's roofline);
+    // between the other phases only with phase timing on (each event between
+    // two kernels costs ~6 us of the run)
+    const bool ph = c->phase_timing;
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
+    k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
     launch_boundary(c, m, 0, nc, cnt + CNT_VAL);
-    GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
-    launch_scan(c, m, 0, nc, 0, nf, gb, cap);
-    GCK_HIP(hipEventRecord(c->ev[PH_HOST], m));
-    k_account_grp<<<1, 1, 0, m>>>(0, nf, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
-                                  c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
-                                  c->d_fnrec.as<uint64_t>(), c->d_carry.as<uint32_t>(), gb, cap, res, grng, rng);
-    GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], m));
+    if (ph) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
+    launch_scan(c, m, gb, cap, true, res, grng, rng);
+    if (ph) GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], m));
     launch_records(c, m, 0, nc, 0, c->n_rows, 0, nf, grng, cap);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], m));
     int rc;
@@ -2053,14 +2070,23 @@ static int ctx_run_device(Ctx *c) {
     c->n_overflow = h[CNT_STAGE];
     c->n_crc_fail = h[CNT_REJECT];
     for (int p = 0; p < PH_NPHASE; ++p) c->ms_phase[p] = 0;
-    for (int p = PH_BOUNDARY; p < PH_END; ++p) {
+    auto el = [&](int a, int b) {
         float ms = 0;
-        (void)hipEventElapsedTime(&ms, c->ev[p], c->ev[p + 1]);
-        c->ms_phase[p] = ms;
+        (void)hipEventElapsedTime(&ms, c->ev[a], c->ev[b]);
+        return (double)ms;
+    };
+    if (ph) {
+        c->ms_phase[PH_BOUNDARY] = el(PH_BOUNDARY, PH_SCAN);
+        c->ms_phase[PH_SCAN] = el(PH_SCAN, PH_RECORDS);  // scans, file summaries, bookkeeping: one kernel
+        c->ms_phase[PH_RECORDS] = el(PH_RECORDS, PH_CRC);
+    } else {
+        c->ms_phase[PH_BOUNDARY] = el(PH_BOUNDARY, PH_CRC);  // every phase before the CRC pass
     }
-    float span = 0;
-    (void)hipEventElapsedTime(&span, c->ev[PH_BOUNDARY], c->ev[PH_END]);
-    c->ms_phase[PH_PIPE] = span;
+    c->ms_phase[PH_CRC] = el(PH_CRC, PH_FINAL);
+    c->ms_phase[PH_FINAL] = el(PH_FINAL, PH_END);
+    c->ms_phase[PH_PIPE] = el(PH_BOUNDARY, PH_END);
+    c->ms_crc_sum += c->ms_phase[PH_CRC];
+    ++c->n_runs;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
@@ -2185,6 +2211,14 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->files_walked = c->files_walked;
     out->final_last_offset = c->final_last_offset;
     out->n_files = c->nfiles;
+    out->n_runs = c->n_runs;
+    out->ms_crc_rows_sum = c->ms_crc_sum;
+    return GCK_OK;
+}
+
+int gck_ctx_phase_timing(gck_ctx *ctx, int on) {
+    if (!ctx) return GCK_EINVAL;
+    ctx->c.phase_timing = on != 0;
     return GCK_OK;
 }
 

@@ -137,7 +137,9 @@ typedef struct gck_stats {
     uint64_t n_fixups;      /* chunks whose speculative entry was wrong (re-walked)   */
     uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
     double ms_total;        /* last gck_ctx_run wall time (host clock)                */
-    double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name */
+    double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name; */
+                            /* the device path times boundary..records as one phase  */
+                            /* (under "boundary") unless gck_ctx_phase_timing is on  */
     uint32_t device_path;   /* 1: the last run had no host round trip (record table sized by an earlier run) */
     uint32_t n_reruns;      /* device-only runs redone on the host path (capacity / unsettled speculation)  */
     /* the last run's outcome, as gck_result reports it (no records copied):   */
@@ -148,6 +150,8 @@ typedef struct gck_stats {
     uint32_t final_last_offset;  /* keyDir.lastOffset after replay                */
     uint32_t n_files;            /* files in the arena                            */
     uint32_t reserved;
+    uint64_t n_runs;             /* runs of this context so far                   */
+    double ms_crc_rows_sum;      /* k_crc_rows time (HIP events) summed over them */
 } gck_stats;
 
 int gck_ctx_create(const gck_opts *opts, gck_ctx **out);
@@ -156,6 +160,9 @@ void gck_ctx_destroy(gck_ctx *ctx);
 int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles);
 /* Run the device pipeline on the resident arena.  Blocks until done. */
 int gck_ctx_run(gck_ctx *ctx);
+/* Events between every phase of the next runs (on) or only around the CRC pass
+ * and the whole run (off, the default: each event costs ~6 us of a run). */
+int gck_ctx_phase_timing(gck_ctx *ctx, int on);
 /* Copy the tuples of the last run to host memory. */
 int gck_ctx_fetch(gck_ctx *ctx, gck_result *out);
 /* Copy the tuples of the last run into caller memory (dst holds cap records;
