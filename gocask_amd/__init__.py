@@ -7,7 +7,7 @@ thin ctypes layer over it (the Python counterpart of a cgo stub).
 from .core import (GB, KB, MB, TB, Config, DB, DefaultConfig, ErrCRCFailed, ErrInvalidKey, ErrInvalidValue,
                    ErrKeyNotFound, ErrPartialWrite, ErrUnexpectedEOF, GoCaskError, InMemoryDB, NewDB, NewDisk,
                    NewInMemory, Open, ReplayContext, StartupError, WithDataDir, WithMaxDataFileSize, device_count,
-                   host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into,
+                   host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into, replay_paths,
                    replay_multi, zipf_table)
 from ._lib import F_CRC_OK, F_TOMBSTONE, REC_DTYPE
 
@@ -15,6 +15,6 @@ __all__ = [
     "GB", "KB", "MB", "TB", "Config", "DB", "DefaultConfig", "ErrCRCFailed", "ErrInvalidKey", "ErrInvalidValue",
     "ErrKeyNotFound", "ErrPartialWrite", "ErrUnexpectedEOF", "GoCaskError", "InMemoryDB", "NewDB", "NewDisk",
     "NewInMemory", "Open", "ReplayContext", "StartupError", "WithDataDir", "WithMaxDataFileSize", "device_count",
-    "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into",
+    "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into", "replay_paths",
     "replay_multi", "zipf_table", "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
 ]

@@ -51,7 +51,7 @@ assert KD_ENTRY_DTYPE.itemsize == 64
 
 # Every symbol include/gocask_hip.h declares (tests check the .so exports them).
 EXPORTED = [
-    "gck_replay", "gck_replay_into", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run", "gck_ctx_phase_timing",
+    "gck_replay", "gck_replay_into", "gck_replay_paths", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run", "gck_ctx_phase_timing",
     "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_ctx_compact", "gck_ctx_fetch_compact", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_replay_multi", "gck_plan_shards", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
     "gck_ctx_read_file", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
@@ -62,6 +62,10 @@ EXPORTED = [
 
 class GckFile(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("reset_after", ctypes.c_uint8)]
+
+
+class GckPath(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("reset_after", ctypes.c_uint8)]
 
 
 class GckOpts(ctypes.Structure):
@@ -173,6 +177,7 @@ def load():
     sig = {
         "gck_replay": (ctypes.c_int, [P(GckFile), ctypes.c_uint32, P(GckOpts), P(GckResult)]),
         "gck_replay_into": (ctypes.c_int, [P(GckFile), ctypes.c_uint32, P(GckOpts), vp, ctypes.c_uint64, P(GckResult)]),
+        "gck_replay_paths": (ctypes.c_int, [P(GckPath), ctypes.c_uint32, P(GckOpts), P(GckResult)]),
         "gck_result_free": (None, [P(GckResult)]),
         "gck_replay_release_cache": (None, []),
         "gck_ctx_create": (ctypes.c_int, [P(GckOpts), P(vp)]),

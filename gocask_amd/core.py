@@ -251,6 +251,28 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
+def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0):
+    """gck_replay_paths: the same replay of files named by path (read by the
+    library with pread into page-locked staging buffers).  Returns (records,
+    status)."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(paths)
+    enc = [os.fsencode(p) for p in paths]
+    pa = (_lib.GckPath * max(1, len(enc)))()
+    for i, p in enumerate(enc):
+        pa[i].path = p
+        pa[i].reset_after = 1 if reset_after[i] else 0
+    res = GckResult()
+    rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident)),
+                            ctypes.byref(res))
+    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+    try:
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
 def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0):
     """gck_replay_into: host-in/host-out replay (pipelined over file groups)
     with the tuples written into recs (a REC_DTYPE array; register it with

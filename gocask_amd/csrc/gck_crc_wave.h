@@ -225,9 +225,13 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
     while (crem) {
 #pragma unroll
         for (int k = 0; k < kRing; ++k) {
+            // the fold (and a value's end) only while values remain; the
+            // reload of ring[k] on every pass, so every path issues the same
+            // loads in the same order and the compiler's vmcnt waits stay
+            // exact (a load inside the branch made the merge at the loop head
+            // wait for every load in flight: the ring drained once per round)
             if (crem) {
                 A = fold_stripe(cj, cs, ring[k], A, t, lb0, lb1);
-                load_next(ring[k]);
                 if (++cs == cj.J) {  // value done
                     const uint32_t f = combine(A);
                     if (lane == (uint32_t)ct) out = f;
@@ -240,6 +244,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
                     }
                 }
             }
+            load_next(ring[k]);
         }
     }
     return out;

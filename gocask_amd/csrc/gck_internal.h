@@ -154,6 +154,34 @@ struct Ctx {
 
 int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after);
 
+// Host-to-device copies of gck_replay's file groups on one copy stream
+// (staging.hip): registered memory by the DMA engine directly (direct), the
+// rest through page-locked staging buffers filled by host threads (add:
+// memcpy from src, or pread from fd when src is null).  Group g's event is
+// recorded on the stream once every chunk of the group is queued (seal, then
+// wait_recorded before a stream waits on it).
+class Copier {
+   public:
+    Copier();
+    ~Copier();
+    int start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev);
+    void add(uint32_t group, const uint8_t *src, int fd, uint64_t off, uint64_t len, uint8_t *dst);
+    int direct(const uint8_t *src, uint64_t len, uint8_t *dst);
+    void seal(uint32_t group);
+    int wait_recorded(uint32_t group);
+    int finish();  // joins the threads; the first error of any copy
+
+   private:
+    struct Impl;
+    Impl *p;
+    int dev_ = 0;
+};
+void stage_release();  // frees the idle staging buffers (gck_replay_release_cache)
+bool host_pinned(const void *p);  // page-locked (registered or hipHostMalloc) host memory
+// n files into device memory through a Copier on stream, then waits for them
+int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, const uint64_t *len, uint8_t *const *dst,
+                    uint32_t n);
+
 }  // namespace gck
 
 struct gck_ctx {

@@ -13,6 +13,10 @@
 //   k_row_tail     first record touching each 4 KiB row (with k_compact)
 //   k_crc_rows     HBM-bound: every byte once, CRC partials of every value
 //   k_finalize     CRC verdict, ValuePos (u32 wrap), gck_rec tuples
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <climits>
 #include <cstdio>
@@ -2144,11 +2148,15 @@ int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles) {
     }
     int rc = ctx_layout(&ctx->c, lens.data(), nfiles, reset.data());
     if (rc) return rc;
-    for (uint32_t f = 0; f < nfiles; ++f)
-        if (files[f].len)
-            GCK_HIP(hipMemcpy(ctx->c.arena.as<uint8_t>() + ctx->c.f_base[f], files[f].data, files[f].len,
-                              hipMemcpyHostToDevice));
-    return GCK_OK;
+    // pageable memory through the staging copier (host threads, page-locked
+    // buffers), registered memory by DMA as is
+    std::vector<const uint8_t *> src(nfiles);
+    std::vector<uint8_t *> dst(nfiles);
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        src[f] = files[f].data;
+        dst[f] = ctx->c.arena.as<uint8_t>() + ctx->c.f_base[f];
+    }
+    return copy_files_sync(ctx->c.device, ctx->c.stream, src.data(), lens.data(), dst.data(), nfiles);
 }
 
 int gck_ctx_run(gck_ctx *ctx) {
@@ -2360,13 +2368,23 @@ void gck_replay_release_cache(void) {
         all.swap(g_pool);
     }
     for (auto &e : all) gck_ctx_destroy(e.ctx);
+    stage_release();
 }
 
-static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
+// A data file to replay: caller memory (data), or an open file (fd, data null)
+struct Src {
+    const uint8_t *data;
+    int fd;
+    uint64_t len;
+    bool reset_after;
+};
+
+static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
                           uint64_t cap, gck_result *out) {
+    const auto t_call = std::chrono::steady_clock::now();
     memset(out, 0, sizeof(*out));
     for (uint32_t f = 0; f < nfiles; ++f)
-        if (files[f].len && !files[f].data) return GCK_EINVAL;
+        if (files[f].len && !files[f].data && files[f].fd < 0) return GCK_EINVAL;
     const uint64_t budget_opt = opts ? opts->max_resident : 0;
     // group target: kGroupBytes, or a third of a tight budget (so at least
     // two groups of files smaller than that fit at once)
@@ -2411,7 +2429,9 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     std::vector<void *> chunks(G, nullptr);        // ring mode, gck_replay: each group's tuples (pinned)
     std::vector<uint64_t> chunk_n(G, 0);
     int rc = GCK_OK;
+    Copier cp;  // the file copies (staging.hip)
     auto cleanup = [&](bool keep) {
+        (void)cp.finish();
         if (copy) (void)hipStreamSynchronize(copy);
         if (run_s) {
             (void)hipStreamSynchronize(run_s);
@@ -2456,8 +2476,18 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
         own_s[k] = cs[k]->c.stream;
         cs[k]->c.stream = run_s;
     }
+    if ((rc = cp.start(dev, copy, &ev))) {
+        cleanup(false);
+        return rc;
+    }
+    // caller memory that is page-locked (gck_host_register) goes by DMA as is
+    std::vector<uint8_t> pinned(nfiles, 0);
+    for (uint32_t f = 0; f < nfiles; ++f) pinned[f] = files[f].data && files[f].len && host_pinned(files[f].data);
     const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
+    if (trace)
+        fprintf(stderr, "[gck_replay] %u contexts ready, copier started at %.2f ms after the call\n", R,
+                std::chrono::duration<double, std::milli>(t_begin - t_call).count());
     hipEvent_t tev0 = nullptr;
     if (trace) {
         (void)hipEventCreate(&tev0);
@@ -2485,13 +2515,19 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
             if ((r = ensure_records(c, est))) return r;
             c->rec_cap = est;
         }
-        for (uint32_t k = 0; k < n; ++k)
-            if (files[f0 + k].len && hipMemcpyAsync(c->arena.as<uint8_t>() + c->f_base[k], files[f0 + k].data,
-                                                    files[f0 + k].len, hipMemcpyHostToDevice, copy) != hipSuccess)
-                return GCK_EDEVICE;
-        if (hipEventCreateWithFlags(&ev[g], trace ? hipEventDefault : hipEventDisableTiming) != hipSuccess ||
-            hipEventRecord(ev[g], copy) != hipSuccess)
+        if (hipEventCreateWithFlags(&ev[g], trace ? hipEventDefault : hipEventDisableTiming) != hipSuccess)
             return GCK_EDEVICE;
+        for (uint32_t k = 0; k < n; ++k) {
+            const Src &f = files[f0 + k];
+            uint8_t *d = c->arena.as<uint8_t>() + c->f_base[k];
+            if (!f.len) continue;
+            if (pinned[f0 + k]) {
+                if ((r = cp.direct(f.data, f.len, d))) return r;
+            } else {
+                cp.add(g, f.data, f.fd, 0, f.len, d);
+            }
+        }
+        cp.seal(g);  // its event follows its last chunk on the copy stream
         return GCK_OK;
     };
     // every resident group's layout first, then (in prep) its copies: a
@@ -2515,6 +2551,7 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     uint64_t st_err_off = 0;
     for (uint32_t g = 0; g < G && !rc; ++g) {
         Ctx *c = &cs[g % R]->c;
+        if ((rc = cp.wait_recorded(g))) break;
         if (hipStreamWaitEvent(c->stream, ev[g], 0) != hipSuccess) {
             rc = GCK_EDEVICE;
             break;
@@ -2643,17 +2680,48 @@ static int replay_grouped(const gck_file *files, uint32_t nfiles, const gck_opts
     return out->status;
 }
 
+static std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles) {
+    std::vector<Src> v(nfiles);
+    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, -1, files[f].len, files[f].reset_after != 0};
+    return v;
+}
+
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
     if (nfiles && !files) return GCK_EINVAL;
-    return replay_grouped(files, nfiles, opts, false, nullptr, 0, out);
+    const std::vector<Src> v = mem_srcs(files, nfiles);
+    return replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
 }
 
 int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_rec *dst, uint64_t cap,
                     gck_result *out) {
     if (!out || (cap && !dst) || (nfiles && !files)) return GCK_EINVAL;
-    return replay_grouped(files, nfiles, opts, true, dst, cap, out);
+    const std::vector<Src> v = mem_srcs(files, nfiles);
+    return replay_grouped(v.data(), nfiles, opts, true, dst, cap, out);
+}
+
+int gck_replay_paths(const gck_path *files, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
+    if (!out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    if (nfiles && !files) return GCK_EINVAL;
+    std::vector<Src> v(nfiles, Src{nullptr, -1, 0, false});
+    auto close_all = [&] {
+        for (auto &s : v)
+            if (s.fd >= 0) close(s.fd);
+    };
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        struct stat st;
+        if (!files[f].path || (v[f].fd = open(files[f].path, O_RDONLY | O_CLOEXEC)) < 0 || fstat(v[f].fd, &st) != 0) {
+            close_all();
+            return GCK_EIO;
+        }
+        v[f].len = (uint64_t)st.st_size;
+        v[f].reset_after = files[f].reset_after != 0;
+    }
+    const int rc = replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
+    close_all();
+    return rc;
 }
 
 void gck_result_free(gck_result *res) {

@@ -1,0 +1,276 @@
+// staging.hip — host-to-device copies of data files that are not page-locked
+// (row f2 of SURVEY.md §8: the pinned H2D pipeline behind Open).
+//
+// gck_replay's files reach the device arena on one copy stream.  Memory the
+// caller registered (gck_host_register) is copied by the DMA engine directly.
+// Anything else -- pageable memory, or files named by path (gck_replay_paths)
+// -- goes through this copier: host threads fill page-locked staging buffers
+// (memcpy from the caller's memory, or pread from the file, which needs no
+// mapping and takes no page faults) and queue each buffer on the copy stream
+// as soon as it is full, so the CPU copies, the PCIe transfer and the
+// replays of earlier file groups all overlap.  Pinning a whole database
+// first (hipHostRegister of every mmap, then unregistering it) costs more
+// than the transfer itself: 1.3 s + 0.5-1.3 s against 0.6 s of PCIe for C3
+// (DESIGN.md §9b).
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "gck_internal.h"
+
+namespace gck {
+
+namespace {
+constexpr uint64_t kStageChunk = 32ull << 20;  // bytes per staging buffer
+
+// Page-locked staging buffers kept for the process, per device: a copier
+// takes the buffers it needs from the free list and gives them back when it
+// finishes (concurrent copiers -- gck_replay_multi's device threads, several
+// Opens -- never share one); gck_replay_release_cache frees the idle ones.
+// Allocating 0.5 GiB of pinned memory per Open would cost more than filling it.
+struct StagePool {
+    std::mutex mu;
+    std::vector<std::pair<int, void *>> idle;  // (device, buffer)
+} g_stage;
+
+int stage_take(int dev, size_t n, std::vector<void *> &out) {
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    for (size_t i = 0; i < g_stage.idle.size() && out.size() < n;)
+        if (g_stage.idle[i].first == dev) {
+            out.push_back(g_stage.idle[i].second);
+            g_stage.idle.erase(g_stage.idle.begin() + (ptrdiff_t)i);
+        } else {
+            ++i;
+        }
+    while (out.size() < n) {
+        void *q = nullptr;
+        if (hipHostMalloc(&q, kStageChunk, hipHostMallocDefault) != hipSuccess) return GCK_ENOMEM;
+        out.push_back(q);
+    }
+    return GCK_OK;
+}
+
+void stage_give(int dev, std::vector<void *> &bufs) {
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    for (void *q : bufs) g_stage.idle.emplace_back(dev, q);
+    bufs.clear();
+}
+
+uint32_t copy_threads() {
+    if (const char *e = getenv("GCK_COPY_THREADS")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 64) return (uint32_t)v;
+    }
+    const uint32_t hw = std::thread::hardware_concurrency();
+    return std::max<uint32_t>(2, std::min<uint32_t>(8, hw ? hw / 2 : 2));
+}
+}  // namespace
+
+bool host_pinned(const void *p) {
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, const_cast<void *>(p), 0) == hipSuccess && dp) return true;
+    (void)hipGetLastError();
+    return false;
+}
+
+int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, const uint64_t *len, uint8_t *const *dst,
+                    uint32_t n) {
+    std::vector<hipEvent_t> ev(1, nullptr);
+    if (hipSetDevice(dev) != hipSuccess || hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess)
+        return GCK_EDEVICE;
+    int rc;
+    {
+        Copier cp;
+        rc = cp.start(dev, stream, &ev);
+        for (uint32_t f = 0; f < n && !rc; ++f) {
+            if (!len[f]) continue;
+            if (host_pinned(src[f]))
+                rc = cp.direct(src[f], len[f], dst[f]);
+            else
+                cp.add(0, src[f], -1, 0, len[f], dst[f]);
+        }
+        cp.seal(0);
+        if (!rc) rc = cp.wait_recorded(0);
+        const int r2 = cp.finish();
+        if (!rc) rc = r2;
+    }
+    if (hipStreamSynchronize(stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
+    (void)hipEventDestroy(ev[0]);
+    return rc;
+}
+
+void stage_release() {
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    for (auto &e : g_stage.idle) (void)hipHostFree(e.second);
+    g_stage.idle.clear();
+}
+
+struct Copier::Impl {
+    struct Job {
+        const uint8_t *src;  // caller memory, or nullptr: pread(fd, off)
+        int fd;
+        uint64_t off, len;
+        uint8_t *dst;
+        uint32_t group;
+    };
+    hipStream_t stream;
+    std::vector<hipEvent_t> *group_ev;
+    std::mutex mu;
+    std::condition_variable cv_job, cv_group;
+    std::deque<Job> jobs;
+    std::vector<uint64_t> pending;   // per group: chunks not yet queued on the stream
+    std::vector<uint8_t> recorded;   // per group: its event recorded after its last chunk
+    std::vector<uint8_t> sealed;     // per group: every chunk submitted
+    std::vector<void *> bufs;
+    std::vector<hipEvent_t> buf_ev;  // per buffer: the last DMA out of it
+    std::vector<uint8_t> buf_busy;
+    std::vector<std::thread> workers;
+    bool stop = false;
+    int err = GCK_OK;
+
+    // group g's event on the stream once its last chunk is queued (mu held)
+    void maybe_record(uint32_t g) {
+        if (!sealed[g] || pending[g] || recorded[g]) return;
+        if (hipEventRecord((*group_ev)[g], stream) != hipSuccess && !err) err = GCK_EDEVICE;
+        recorded[g] = 1;
+        cv_group.notify_all();
+    }
+
+    void work() {
+        for (;;) {
+            Job j;
+            size_t b = 0;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_job.wait(lk, [&] { return stop || !jobs.empty(); });
+                if (jobs.empty()) return;
+                j = jobs.front();
+                jobs.pop_front();
+                // a free staging buffer (one whose last DMA has finished)
+                for (;;) {
+                    bool found = false;
+                    for (b = 0; b < bufs.size(); ++b)
+                        if (!buf_busy[b]) {
+                            found = true;
+                            break;
+                        }
+                    if (found) break;
+                    cv_job.wait(lk);
+                }
+                buf_busy[b] = 1;
+            }
+            (void)hipEventSynchronize(buf_ev[b]);  // the buffer's previous transfer
+            uint8_t *stage = static_cast<uint8_t *>(bufs[b]);
+            bool ok = true;
+            if (j.src) {
+                memcpy(stage, j.src + j.off, j.len);
+            } else {
+                uint64_t got = 0;
+                while (got < j.len) {
+                    const ssize_t r = pread(j.fd, stage + got, j.len - got, (off_t)(j.off + got));
+                    if (r <= 0) {
+                        ok = false;
+                        break;
+                    }
+                    got += (uint64_t)r;
+                }
+            }
+            std::lock_guard<std::mutex> lk(mu);
+            if (!ok && !err) err = GCK_EINVAL;  // the file shrank or could not be read
+            if (ok && (hipMemcpyAsync(j.dst, stage, j.len, hipMemcpyHostToDevice, stream) != hipSuccess ||
+                       hipEventRecord(buf_ev[b], stream) != hipSuccess) &&
+                !err)
+                err = GCK_EDEVICE;
+            buf_busy[b] = 0;
+            --pending[j.group];
+            maybe_record(j.group);
+            cv_job.notify_all();
+        }
+    }
+};
+
+Copier::Copier() : p(new Impl) {}
+Copier::~Copier() {
+    finish();
+    for (auto e : p->buf_ev)
+        if (e) (void)hipEventDestroy(e);
+    delete p;
+}
+
+int Copier::start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev) {
+    p->stream = stream;
+    p->group_ev = group_ev;
+    const size_t G = group_ev->size();
+    p->pending.assign(G, 0);
+    p->recorded.assign(G, 0);
+    p->sealed.assign(G, 0);
+    const uint32_t T = copy_threads();
+    const size_t nb = 2 * (size_t)T;
+    dev_ = dev;
+    if (stage_take(dev, nb, p->bufs)) return GCK_ENOMEM;
+    p->buf_ev.assign(nb, nullptr);
+    p->buf_busy.assign(nb, 0);
+    for (auto &e : p->buf_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return GCK_EDEVICE;
+    for (uint32_t t = 0; t < T; ++t) p->workers.emplace_back([this] {
+        (void)hipSetDevice(dev_);
+        p->work();
+    });
+    return GCK_OK;
+}
+
+void Copier::add(uint32_t group, const uint8_t *src, int fd, uint64_t off, uint64_t len, uint8_t *dst) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    for (uint64_t o = 0; o < len; o += kStageChunk) {
+        const uint64_t n = std::min(kStageChunk, len - o);
+        p->jobs.push_back(Impl::Job{src, fd, off + o, n, dst + o, group});
+        ++p->pending[group];
+    }
+    p->cv_job.notify_all();
+}
+
+int Copier::direct(const uint8_t *src, uint64_t len, uint8_t *dst) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, p->stream) != hipSuccess) return GCK_EDEVICE;
+    return GCK_OK;
+}
+
+void Copier::seal(uint32_t group) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    p->sealed[group] = 1;
+    p->maybe_record(group);
+}
+
+int Copier::wait_recorded(uint32_t group) {
+    std::unique_lock<std::mutex> lk(p->mu);
+    p->cv_group.wait(lk, [&] { return p->recorded[group] || p->err; });
+    return p->err;
+}
+
+int Copier::finish() {
+    {
+        std::lock_guard<std::mutex> lk(p->mu);
+        p->stop = true;
+        p->jobs.clear();  // (an error path: nothing waits for them any more)
+        p->cv_job.notify_all();
+    }
+    for (auto &t : p->workers)
+        if (t.joinable()) t.join();
+    p->workers.clear();
+    // the buffers go back once their last transfers are done
+    for (auto e : p->buf_ev)
+        if (e) (void)hipEventSynchronize(e);
+    stage_give(dev_, p->bufs);
+    return p->err;
+}
+
+}  // namespace gck

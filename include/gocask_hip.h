@@ -120,6 +120,16 @@ int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck
  * cap < out->n. */
 int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_rec *dst, uint64_t cap,
                     gck_result *out);
+/* A data file by name (filepath.Walk's path) for gck_replay_paths. */
+typedef struct gck_path {
+    const char *path;
+    uint8_t reset_after; /* Name() != activeFile.Name() (core/db.go:117) */
+} gck_path;
+/* gck_replay of files named by path: the library opens them, reads them with
+ * pread into page-locked staging buffers (host threads, GCK_COPY_THREADS) and
+ * streams them to the device, so nothing has to be mapped or registered;
+ * GCK_EIO when a file cannot be opened or read. */
+int gck_replay_paths(const gck_path *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
 void gck_result_free(gck_result *res);
 /* gck_replay / gck_replay_into keep their device contexts (arenas, tables) for
  * the next call with the same options, so a repeated Open allocates nothing;

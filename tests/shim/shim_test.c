@@ -24,6 +24,10 @@
  * gck_host_register inside the callback, gck_replay, gck_result_free,
  * unregister + munmap) and print one JSON line instead of the keys.
  * SHIM_MULTI=1: gck_replay_multi on device 0 (the live keydir comes back).
+ * SHIM_PIN=0: map the files but do not register them (the library stages the
+ * pageable mappings through its own page-locked buffers).
+ * SHIM_PATHS=1: gck_replay_paths -- the library opens and reads the files
+ * itself (the shim maps them only to print keys, never when timing).
  */
 #define _GNU_SOURCE
 #include <dirent.h>
@@ -40,12 +44,15 @@
 
 typedef struct {
     char name[256]; /* DiskFile.Name(): base name without the extension */
+    char *path;
     const uint8_t *map;
     uint64_t len;
+    int pinned;
 } mapped;
 
 static mapped *g_files;
 static size_t g_n, g_cap;
+static int g_pin = 1, g_map = 1;
 
 static int cmp_str(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
 
@@ -73,14 +80,16 @@ static int on_file(const char *path) {
     b = b ? b + 1 : path;
     snprintf(m->name, sizeof m->name, "%.*s", (int)(ext_of(b) - b), b);
     m->len = (uint64_t)st.st_size;
-    if (m->len) {
+    m->path = strdup(path);
+    if (m->len && g_map) {
         void *a = mmap(NULL, m->len, PROT_READ, MAP_SHARED, fd, 0);
         if (a == MAP_FAILED) {
             close(fd);
             return -1;
         }
         m->map = a;
-        if (gck_host_register(m->map, m->len) != GCK_OK) m->map = a; /* pinning is an optimisation only */
+        /* pinning is an optimisation only */
+        m->pinned = g_pin && gck_host_register(m->map, m->len) == GCK_OK;
     }
     close(fd); /* Disk.Walk: return file.Close() */
     return 0;
@@ -126,6 +135,14 @@ static int cmp_kd(const void *a, const void *b) {
     return c ? c : (x->klen > y->klen) - (x->klen < y->klen);
 }
 
+static void release_files(void) {
+    for (size_t i = 0; i < g_n; ++i) {
+        if (g_files[i].pinned) gck_host_unregister(g_files[i].map);
+        if (g_files[i].map) munmap((void *)g_files[i].map, g_files[i].len);
+        free(g_files[i].path);
+    }
+}
+
 static double now_ms(void) {
     struct timespec t;
     clock_gettime(CLOCK_MONOTONIC, &t);
@@ -135,6 +152,10 @@ static double now_ms(void) {
 int main(int argc, char **argv) {
     const int timing = getenv("SHIM_TIME") && atoi(getenv("SHIM_TIME"));
     const int multi = getenv("SHIM_MULTI") && atoi(getenv("SHIM_MULTI"));
+    const int by_path = getenv("SHIM_PATHS") && atoi(getenv("SHIM_PATHS"));
+    if (getenv("SHIM_PIN")) g_pin = atoi(getenv("SHIM_PIN"));
+    if (by_path) g_pin = 0;
+    if (by_path && timing) g_map = 0;
     if (argc < 2) {
         fprintf(stderr, "usage: %s <db dir> [active name]\n", argv[0]);
         return 2;
@@ -170,7 +191,15 @@ int main(int argc, char **argv) {
             gf[i].len = g_files[i].len;
             gf[i].reset_after = strcmp(g_files[i].name, active) != 0;
         }
-        if (multi) {
+        if (by_path) {
+            gck_path *gp = calloc(g_n, sizeof(gck_path));
+            for (size_t i = 0; i < g_n; ++i) {
+                gp[i].path = g_files[i].path;
+                gp[i].reset_after = gf[i].reset_after;
+            }
+            rc = gck_replay_paths(gp, (uint32_t)g_n, NULL, &res);
+            free(gp);
+        } else if (multi) {
             const int32_t dev0 = 0;
             rc = gck_replay_multi(gf, (uint32_t)g_n, &dev0, 1, NULL, &res);
         } else {
@@ -190,18 +219,15 @@ int main(int argc, char **argv) {
         const uint32_t last = res.final_last_offset, groups = res.n_groups, resident = res.n_resident;
         if (g_n) gck_result_free(&res);
         const double t3 = now_ms();
-        for (size_t i = 0; i < g_n; ++i)
-            if (g_files[i].len) {
-                gck_host_unregister(g_files[i].map);
-                munmap((void *)g_files[i].map, g_files[i].len);
-            }
+        release_files();
         const double t4 = now_ms();
         printf("{\"files\": %zu, \"bytes\": %llu, \"status\": %d, \"records\": %llu, \"crc_rejects\": %llu, "
                "\"last_offset\": %u, \"groups\": %u, \"resident\": %u, \"walk_mmap_register_ms\": %.2f, "
                "\"replay_ms\": %.2f, \"free_ms\": %.2f, \"unregister_unmap_ms\": %.2f, \"open_ms\": %.2f, "
-               "\"open_gib_s\": %.3f, \"multi\": %d}\n",
+               "\"open_gib_s\": %.3f, \"multi\": %d, \"mode\": \"%s\"}\n",
                g_n, (unsigned long long)bytes, rc, (unsigned long long)n, (unsigned long long)fail, last, groups,
-               resident, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0, bytes / ((t4 - t0) * 1e-3) / (1 << 30), multi);
+               resident, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0, bytes / ((t4 - t0) * 1e-3) / (1 << 30), multi,
+               by_path ? "paths" : g_pin ? "pinned" : "pageable");
         free(g_files);
         return 0;
     }
@@ -238,11 +264,7 @@ int main(int argc, char **argv) {
     }
     free(kd);
     if (g_n) gck_result_free(&res);
-    for (size_t i = 0; i < g_n; ++i)
-        if (g_files[i].len) {
-            gck_host_unregister(g_files[i].map);
-            munmap((void *)g_files[i].map, g_files[i].len);
-        }
+    release_files();
     free(g_files);
     return 0;
 }

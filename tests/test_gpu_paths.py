@@ -1,0 +1,110 @@
+"""Open by path (row f2): gck_replay_paths reads the data files itself --
+pread into page-locked staging buffers on host threads, streamed to the device
+file group by file group -- so a caller needs neither mmap nor
+gck_host_register (the cost of pinning a whole database).  The
+same staging copier now carries gck_replay's pageable (unregistered) memory.
+Results must equal the oracle's (core/db.go:110-178) for any ring size,
+thread count and staging-chunk split."""
+import os
+
+import numpy as np
+import pytest
+
+import golden_cases
+import oracle as orc_mod
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("rec_off", "file", "key_len", "value_pos", "value_size", "crc", "ts", "flags", "crc_calc")
+
+
+@pytest.fixture(scope="module")
+def g():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    import gocask_amd
+
+    assert gocask_amd.device_count() > 0, "no GPU visible"
+    return gocask_amd
+
+
+def _same(got, gst, want, wst):
+    for k in ("status", "err_file", "err_off", "files_walked", "final_last_offset"):
+        if k in ("err_file", "err_off") and not wst["status"]:
+            continue
+        assert gst[k] == wst[k], (k, gst, wst)
+    assert len(got) == len(want)
+    for f in FIELDS:
+        assert np.array_equal(got[f], want[f]), f
+
+
+def _write(tmp_path, files, tag="f"):
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"{tag}_{i:04d}.csk"
+        p.write_bytes(bytes(np.asarray(f, dtype=np.uint8)))
+        paths.append(str(p))
+    return paths
+
+
+def _corpus(orc, seed=93, n_files=12, fsize=2 << 20, active=4):
+    files, names = orc.gen_corpus(seed=seed, val_fixed=0, key_min=8, key_max=24, key_universe=3000,
+                                  tomb_permille=30, flip_permille=20, max_file_size=fsize, n_files=n_files)
+    walk = sorted(range(len(files)), key=lambda i: names[i])
+    wf = [files[i] for i in walk]
+    reset = [True] * len(wf)
+    reset[active] = False  # the active file mid-way: its lastOffset carries on
+    return wf, reset
+
+
+@pytest.mark.parametrize("budget", [0, 12 << 20, 1 << 20])
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_paths_equal_oracle(g, orc, tmp_path, monkeypatch, budget, threads):
+    monkeypatch.setenv("GCK_COPY_THREADS", threads)
+    wf, reset = _corpus(orc)
+    want, wst = orc.replay(wf, reset)
+    got, gst = g.replay_paths(_write(tmp_path, wf), reset, max_resident=budget)
+    _same(got, gst, want, wst)
+    if budget:
+        assert 1 <= gst["n_resident"] < gst["n_groups"], gst
+    # the same files from pageable memory (the staging copier's memcpy path)
+    got, gst = g.replay(wf, reset, max_resident=budget)
+    _same(got, gst, want, wst)
+
+
+@pytest.mark.parametrize("name", golden_cases.case_names())
+def test_paths_golden(g, orc, tmp_path, name):
+    meta, files, reset = golden_cases.load_case(name)
+    want, wst = orc.replay(files, reset)
+    got, gst = g.replay_paths(_write(tmp_path, files), reset)
+    _same(got, gst, want, wst)
+
+
+def test_paths_files_larger_than_a_staging_chunk(g, orc, tmp_path, monkeypatch):
+    # 32 MiB staging chunks: files of 70 and 33 MiB cross chunk edges, and the
+    # chunks of one file land in different buffers out of order
+    monkeypatch.setenv("GCK_COPY_THREADS", "4")
+    wf, reset = _corpus(orc, seed=94, n_files=3, fsize=70 << 20, active=2)
+    assert max(len(f) for f in wf) > (64 << 20)
+    want, wst = orc.replay(wf, reset)
+    got, gst = g.replay_paths(_write(tmp_path, wf), reset)
+    _same(got, gst, want, wst)
+
+
+def test_paths_startup_error_and_empty_files(g, orc, tmp_path):
+    wf, reset = _corpus(orc, seed=95, n_files=6)
+    bad = np.frombuffer(orc_mod.entry(1, b"user", b"x" * 10) + orc_mod.entry(2, b"key", b"yy")[:-4], np.uint8)
+    empty = np.zeros(0, np.uint8)
+    wf = wf[:2] + [empty] + wf[2:4] + [bad] + wf[4:]
+    reset = reset[:2] + [True] + reset[2:4] + [True] + reset[4:]
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] != 0
+    got, gst = g.replay_paths(_write(tmp_path, wf), reset, max_resident=4 << 20)
+    _same(got, gst, want, wst)
+
+
+def test_paths_missing_file(g, tmp_path):
+    with pytest.raises(g._lib.GckError):
+        g.replay_paths([str(tmp_path / "absent.csk")], [False])
+    assert not os.path.exists(tmp_path / "absent.csk")

@@ -26,8 +26,9 @@ def shim():
     return SHIM
 
 
-def run(shim, d, active=None, multi=False):
-    env = dict(os.environ, SHIM_MULTI="1" if multi else "0")
+def run(shim, d, active=None, multi=False, mode="pinned"):
+    env = dict(os.environ, SHIM_MULTI="1" if multi else "0", SHIM_PIN="1" if mode == "pinned" else "0",
+               SHIM_PATHS="1" if mode == "paths" else "0")
     p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120,
                        env=env)
     assert p.returncode == 0, p.stderr
@@ -119,3 +120,17 @@ def test_shim_multi_gpu_call_same_keydir(shim, orc, tmp_path, name):
     one = run(shim, tmp_path, meta["active"])
     many = run(shim, tmp_path, meta["active"], multi=True)
     assert one == many
+
+
+@pytest.mark.parametrize("name", ["existing_after_startup", "keys_in_order", "updated_values_across_files",
+                                  "datatxt_1000_puts", "crc_fail", "partial_write_desync"])
+def test_shim_pageable_and_by_path_same_keydir(shim, orc, tmp_path, name):
+    """Open without pinning: the mappings staged by the library (SHIM_PIN=0),
+    or the files named by path (gck_replay_paths, SHIM_PATHS=1), give the
+    keydir and status of the pinned call."""
+    meta, files, reset = load_case(name)
+    for w, f in zip(meta["walk"], files):
+        (tmp_path / (w + ".csk")).write_bytes(f.tobytes())
+    pinned = run(shim, tmp_path, meta["active"])
+    assert run(shim, tmp_path, meta["active"], mode="pageable") == pinned
+    assert run(shim, tmp_path, meta["active"], mode="paths") == pinned

@@ -4,7 +4,10 @@ files written to /dev/shm (page cache, as a warm database directory), then
 the shim walks, stats, mmaps and gck_host_register's every file inside the
 Walk callback, calls gck_replay (or gck_replay_multi on device 0), frees the
 tuples, unregisters and unmaps.  One JSON line per run; the directory is
-removed at the end.   python tools/shim_c3.py [reps]"""
+removed at the end.  Modes: by path (gck_replay_paths: the library preads the
+files into its staging buffers), pageable mappings (staged by the library),
+pinned mappings (the shim registers each mmap), pinned + gck_replay_multi.
+python tools/shim_c3.py [reps] [number of modes]"""
 import json
 import os
 import shutil
@@ -32,15 +35,23 @@ try:
             del buf
     shim = os.path.join(ROOT, "tests", "shim", "build", "shim_test")
     out = []
-    for mode in ("0", "1"):
+    modes = [dict(SHIM_PATHS="1"), dict(SHIM_PIN="0"), dict(SHIM_PIN="1"), dict(SHIM_PIN="1", SHIM_MULTI="1")]
+    if len(sys.argv) > 2:
+        modes = modes[:int(sys.argv[2])]
+    # SHIM_THREADS="4 8 16": the by-path / pageable modes at each copy-thread count
+    threads = os.environ.get("SHIM_THREADS", "").split()
+    if threads:
+        modes = [dict(m, GCK_COPY_THREADS=t) for t in threads for m in modes if m.get("SHIM_PIN") != "1"]
+    for mode in modes:
         for r in range(reps):
             p = subprocess.run([shim, d], capture_output=True, text=True, timeout=300,
-                               env=dict(os.environ, SHIM_TIME="1", SHIM_MULTI=mode))
+                               env=dict(os.environ, SHIM_TIME="1", **mode))
             if p.returncode:
                 raise SystemExit(p.stderr)
             row = json.loads(p.stdout.strip().splitlines()[-1])
             row["rep"] = r
-            tr = [l for l in p.stderr.splitlines() if l.startswith("gck_replay")]
+            row["copy_threads"] = mode.get("GCK_COPY_THREADS", os.environ.get("GCK_COPY_THREADS", "default"))
+            tr = [l for l in p.stderr.splitlines() if l.startswith(("gck_replay", "[gck_replay"))]
             if tr:  # GCK_REPLAY_TRACE=1: the library's phase marks
                 row["trace"] = tr
             out.append(row)
