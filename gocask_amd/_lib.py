@@ -60,6 +60,9 @@ EXPORTED = [
 ]
 
 
+OPT_KEYS = 1  # gck_opts.flags GCK_OPT_KEYS
+
+
 class GckFile(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("len", ctypes.c_uint64), ("reset_after", ctypes.c_uint8)]
 
@@ -92,6 +95,8 @@ class GckResult(ctypes.Structure):
         ("err_off", ctypes.c_uint64),
         ("n_groups", ctypes.c_uint32),
         ("n_resident", ctypes.c_uint32),
+        ("keys", ctypes.c_void_p),
+        ("keys_len", ctypes.c_uint64),
     ]
 
 

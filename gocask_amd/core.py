@@ -79,13 +79,13 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0, max_resident=0):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0, max_resident=0, keys=False):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = 0
+    o.flags = _lib.OPT_KEYS if keys else 0
     o.spec_window = spec_window
     o.max_resident = max_resident
     return o
@@ -220,9 +220,14 @@ def _result(res: GckResult):
     recs = np.zeros(n, dtype=REC_DTYPE)
     if n:
         ctypes.memmove(recs.ctypes.data, res.recs, n * REC_DTYPE.itemsize)
-    return recs, dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=n,
-                      n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset,
-                      files_walked=res.files_walked, n_groups=res.n_groups, n_resident=res.n_resident)
+    st = dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=n,
+              n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset,
+              files_walked=res.files_walked, n_groups=res.n_groups, n_resident=res.n_resident)
+    if res.keys:  # GCK_OPT_KEYS: the records' key bytes back to back
+        st["keys"] = np.zeros(res.keys_len, dtype=np.uint8)
+        if res.keys_len:
+            ctypes.memmove(st["keys"].ctypes.data, res.keys, res.keys_len)
+    return recs, st
 
 
 def host_register(arr):
@@ -235,7 +240,7 @@ def host_unregister(arr):
 
 
 def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0,
-           max_resident=0):
+           max_resident=0, keys=False):
     """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
     L = _lib.load()
     if reset_after is None:
@@ -243,7 +248,7 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
     rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window,
-                                                        max_resident)), ctypes.byref(res))
+                                                        max_resident, keys)), ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
         return _result(res)
@@ -251,7 +256,7 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0):
+def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False):
     """gck_replay_paths: the same replay of files named by path (read by the
     library with pread into page-locked staging buffers).  Returns (records,
     status)."""
@@ -264,7 +269,7 @@ def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=
         pa[i].path = p
         pa[i].reset_after = 1 if reset_after[i] else 0
     res = GckResult()
-    rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident)),
+    rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident, keys)),
                             ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
@@ -273,7 +278,7 @@ def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0):
+def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False):
     """gck_replay_into: host-in/host-out replay (pipelined over file groups)
     with the tuples written into recs (a REC_DTYPE array; register it with
     host_register for DMA rate).  Returns the status dict; recs[:n] hold the
@@ -283,12 +288,17 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resi
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
-    rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_resident=max_resident)),
+    rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_resident=max_resident,
+                                                             keys=keys)),
                            recs.ctypes.data if recs.size else None, recs.size, ctypes.byref(res))
-    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
-    return dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_recs=res.n,
-                n_crc_fail=res.n_crc_fail, final_last_offset=res.final_last_offset, files_walked=res.files_walked,
-                n_groups=res.n_groups, n_resident=res.n_resident)
+    try:
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+        n, res.n = res.n, 0  # (records are in recs, not in res)
+        st = _result(res)[1]
+        st["n_recs"] = n
+        return st
+    finally:
+        L.gck_result_free(ctypes.byref(res))
 
 
 def replay_multi(files, reset_after=None, devices=(0,), chunk_bytes=0):

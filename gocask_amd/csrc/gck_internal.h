@@ -134,6 +134,8 @@ struct Ctx {
     uint64_t kd_slots = 0;   // table slots (power of two; 0: no records)
     // batched Get / scrub (get.hip): query keys, per-item state, values
     DBuf d_gkeys, d_gkoff, d_gstat, d_gitem, d_gvsize, d_gexp, d_gcrc, d_gvoff, d_gvals;
+    // the key blob of gck_replay with GCK_OPT_KEYS: look-back words, offsets, bytes
+    DBuf d_klb, d_koff, d_keyblob;
 
     // results of the last run
     int32_t status = 0;
@@ -177,7 +179,14 @@ class Copier {
     int dev_ = 0;
 };
 void stage_release();  // frees the idle staging buffers (gck_replay_release_cache)
+uint32_t stage_buffers_wanted();             // staging buffers a Copier takes
+int stage_prealloc(int dev, uint32_t n);     // fill the idle pool ahead of a Copier
 bool host_pinned(const void *p);  // page-locked (registered or hipHostMalloc) host memory
+// gck_result arrays: page-locked or plain, both freed by res_free
+void *res_alloc(uint64_t bytes, bool pinned);
+void res_free(void *p);
+// dst = the segments back to back (host threads for large totals)
+void par_gather(uint8_t *dst, const std::vector<std::pair<const void *, uint64_t>> &segs);
 // n files into device memory through a Copier on stream, then waits for them
 int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, const uint64_t *len, uint8_t *const *dst,
                     uint32_t n);

@@ -349,9 +349,8 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
     for (uint64_t v : n_live) tot += v;
     gck_rec *h = nullptr;
     if (!rc && tot) {
-        void *hp = nullptr;
-        if (hipHostMalloc(&hp, tot * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) rc = GCK_ENOMEM;
-        h = static_cast<gck_rec *>(hp);
+        h = static_cast<gck_rec *>(res_alloc(tot * sizeof(gck_rec), false));  // filled by the host below
+        if (!h) rc = GCK_ENOMEM;
     }
     uint64_t at = 0;
     for (uint32_t p = 0; p < ndev && !rc; ++p) {
@@ -368,7 +367,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
     cleanup();
     mark("freed");
     if (rc) {
-        if (h) (void)hipHostFree(h);
+        res_free(h);
         memset(out, 0, sizeof(*out));
         return rc;
     }

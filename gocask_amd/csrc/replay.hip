@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "gck_internal.h"
 #include "gck_crc_lds.h"
@@ -549,6 +550,51 @@ __device__ void account_run(uint32_t nf, const uint64_t *__restrict__ flen, cons
 // loads where aligned).  rec_base[n] and *base_out = min(total, cap); a total
 // past cap is flagged in *overflow (the exact host path reruns).
 constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+// the wavefront's block index: arrival order (a ticket)
+__device__ __forceinline__ uint32_t lb_ticket(uint32_t *tickets) {
+    uint32_t tk = 0;
+    if ((threadIdx.x & 63) == 0) tk = atomicAdd(&tickets[0], 1u);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+}
+// block b's exclusive base: its total published at once, then the earlier
+// blocks' totals / inclusive prefixes read back until an inclusive one
+__device__ uint64_t lookback_excl(uint64_t *lb, uint32_t b, uint64_t btot) {
+    uint64_t excl = 0;
+    if ((threadIdx.x & 63) == 0) {
+        if (b == 0) {
+            __hip_atomic_store(&lb[0], btot | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&lb[b], btot | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t j = (int64_t)b - 1; j >= 0;) {
+                const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!(w & (kLbAgg | kLbInc))) {
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += w & kLbVal;
+                if (w & kLbInc) break;
+                --j;
+            }
+            __hip_atomic_store(&lb[b], (excl + btot) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(excl >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)excl, 0);
+}
+// true in the wavefront that finishes last (every block's output visible)
+__device__ bool lb_last_done(uint32_t *tickets, uint32_t nb) {
+    __threadfence();
+    uint32_t dn = 0;
+    if ((threadIdx.x & 63) == 0) dn = atomicAdd(&tickets[1], 1u);
+    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)dn) != nb - 1) return false;
+    __threadfence();
+    return true;
+}
+// 64-bit value of lane 63 in every lane
+__device__ __forceinline__ uint64_t lane63(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
 __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__ ch_count, uint64_t *rec_base,
                                                     uint32_t n, uint64_t *lb, uint64_t *base_out, uint64_t cap,
                                                     uint32_t *__restrict__ overflow,
@@ -564,9 +610,7 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__
     static_assert(kScanBlock == 64 * 64, "a lane owns 64 counts");
     const uint32_t lane = threadIdx.x, nb = gridDim.x;
     uint32_t *tickets = reinterpret_cast<uint32_t *>(lb + nb);
-    uint32_t tk = 0;
-    if (lane == 0) tk = atomicAdd(&tickets[0], 1u);
-    const uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    const uint32_t b = lb_ticket(tickets);
     const uint32_t i0 = b * kScanBlock + lane * 64;
     uint32_t v[64];
     const bool vec_in = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(ch_count + i0) & 15) == 0;
@@ -588,30 +632,8 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__
 #pragma unroll
     for (int k = 0; k < 64; ++k) tot += v[k];
     const uint64_t inc = wave_incl_sum64(tot);
-    const uint64_t btot = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(inc >> 32), 63) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)inc, 63);
-    // the block's exclusive base: look back over the published blocks
-    uint64_t excl = 0;
-    if (lane == 0) {
-        if (b == 0) {
-            __hip_atomic_store(&lb[0], btot | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&lb[b], btot | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = (int64_t)b - 1; j >= 0;) {
-                const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!(w & (kLbAgg | kLbInc))) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += w & kLbVal;
-                if (w & kLbInc) break;
-                --j;
-            }
-            __hip_atomic_store(&lb[b], (excl + btot) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    excl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(excl >> 32), 0) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)excl, 0);
+    const uint64_t btot = lane63(inc);
+    const uint64_t excl = lookback_excl(lb, b, btot);
     uint64_t run = excl + inc - tot;  // this lane's first base
     const bool vec_out = i0 + 64 <= n && (reinterpret_cast<uintptr_t>(rec_base + i0) & 15) == 0;
     if (vec_out) {
@@ -643,11 +665,7 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__
         *base_out = min(total, cap);
     }
     // the last wavefront to finish sees every block's bases
-    __threadfence();
-    uint32_t dn = 0;
-    if (lane == 0) dn = atomicAdd(&tickets[1], 1u);
-    if ((uint32_t)__builtin_amdgcn_readfirstlane((int)dn) != nb - 1) return;
-    __threadfence();
+    if (!lb_last_done(tickets, nb)) return;
     for (uint32_t f = lane; f < nfiles; f += 64) {
         const uint32_t fc = f_first_chunk[f], nc = f_nchunks[f];
         const uint64_t r0 = rec_base[fc], r1 = rec_base[fc + nc];
@@ -683,6 +701,60 @@ __global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb
     if (t < kGbWords) gb[t] = 0;
     if (t == kQueueCrc) queue[t] = 0;
     if (t == 0) row_first[0] = 0;
+}
+
+// Key offsets of a run's records for the key blob gck_replay returns with
+// GCK_OPT_KEYS: koff[i] = the key bytes of records before i (a record's key
+// is key_len bytes at its header + 16, a tombstone's included: KeySize 0,
+// the key is its "value", core/db.go:151-155), koff[n] = the total.  The same
+// single-pass look-back as k_scan_chunks (lb: its own zeroed words).
+__global__ __launch_bounds__(64) void k_scan_keys(const uint2 *__restrict__ rec_kv, uint64_t n,
+                                                  uint64_t *__restrict__ koff, uint64_t *lb) {
+    const uint32_t lane = threadIdx.x, nb = gridDim.x;
+    uint32_t *tickets = reinterpret_cast<uint32_t *>(lb + nb);
+    const uint32_t b = lb_ticket(tickets);
+    const uint64_t i0 = (uint64_t)b * kScanBlock + lane * 64;
+    uint32_t v[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        const uint2 kv = i0 + k < n ? rec_kv[i0 + k] : make_uint2(0u, 0u);
+        v[k] = kv.x ? kv.x : kv.y;
+    }
+    uint64_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) tot += v[k];
+    const uint64_t inc = wave_incl_sum64(tot);
+    const uint64_t btot = lane63(inc);
+    const uint64_t excl = lookback_excl(lb, b, btot);
+    uint64_t run = excl + inc - tot;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        if (i0 + k < n) koff[i0 + k] = run;
+        run += v[k];
+    }
+    if (b == nb - 1 && lane == 0) koff[n] = excl + btot;
+    if (!lb_last_done(tickets, nb)) return;
+    for (uint32_t k = lane; k < nb + 1; k += 64) lb[k] = 0;  // lb and both tickets
+}
+
+// The key bytes of records [0, n) back to back (koff from k_scan_keys): a lane
+// per record, dwords where source and destination allow, else bytes.
+__global__ void k_gather_keys(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off,
+                              const uint2 *__restrict__ rec_kv, const uint64_t *__restrict__ koff, uint64_t n,
+                              uint8_t *__restrict__ blob) {
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint2 kv = rec_kv[r];
+        const uint32_t len = kv.x ? kv.x : kv.y;
+        const uint8_t *src = arena + rec_off[r] + 16;
+        uint8_t *dst = blob + koff[r];
+        uint32_t i = 0;
+        if (((reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst)) & 3) == 0) {
+            for (; i < len && (reinterpret_cast<uintptr_t>(src + i) & 3); ++i) dst[i] = src[i];
+            for (; i + 4 <= len; i += 4)
+                *reinterpret_cast<uint32_t *>(dst + i) = *reinterpret_cast<const uint32_t *>(src + i);
+        }
+        for (; i < len; ++i) dst[i] = src[i];
+    }
 }
 
 // row_first[row] = the first record whose value ends after the row's first
@@ -1632,7 +1704,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
                    &c->d_gvoff, &c->d_gvals, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
-                   &c->d_cdata, &c->d_chint, &c->d_cjmp, &c->d_con};
+                   &c->d_cdata, &c->d_chint, &c->d_cjmp, &c->d_con, &c->d_klb, &c->d_koff, &c->d_keyblob};
     for (DBuf *b : all) b->release();
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
     c->h_mbox = c->d_mbox = nullptr;
@@ -2179,8 +2251,8 @@ int gck_ctx_fetch(gck_ctx *ctx, gck_result *out) {
         // pinned host memory: the D2H copy runs at DMA rate (and the caller
         // frees it with gck_result_free)
         GCK_HIP(hipSetDevice(c->device));
-        void *h = nullptr;
-        if (hipHostMalloc(&h, c->n_recs * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) return GCK_ENOMEM;
+        void *h = res_alloc(c->n_recs * sizeof(gck_rec), true);
+        if (!h) return GCK_ENOMEM;
         out->recs = static_cast<gck_rec *>(h);
         GCK_HIP(hipMemcpy(out->recs, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost));
     }
@@ -2268,7 +2340,8 @@ int gck_ctx_read_file(gck_ctx *ctx, uint32_t file, uint64_t off, uint8_t *dst, u
 // contribute nothing.  The tuples of the contributing groups (file indices
 // rebased) go into the caller's dst (cap records) when dst != NULL, else into
 // library-owned pinned memory.
-constexpr uint64_t kGroupBytes = 1ull << 30;  // group size target (smaller under a tight budget)
+constexpr uint64_t kGroupBytes = 1ull << 30;  // smallest group target (smaller under a tight budget)
+constexpr uint64_t kGroupsWanted = 4;          // groups a database is cut into when it fits
 constexpr double kAutoBudgetShare = 0.6;      // share of free HBM the ring may take by default
 
 __global__ void k_rebase_file(gck_rec *recs, uint64_t n, uint32_t base) {
@@ -2311,6 +2384,7 @@ gck_opts pool_key(const gck_opts *o) {
     gck_opts k{};
     if (o) k = *o;
     k.max_resident = 0;  // a budget, not a context setting
+    k.flags &= ~GCK_OPT_KEYS;  // a per-call output, not a context setting
     return k;
 }
 bool same_opts(const gck_opts &a, const gck_opts &b) {
@@ -2371,6 +2445,34 @@ void gck_replay_release_cache(void) {
     stage_release();
 }
 
+// The last run's key bytes, back to back in record order, into a new pinned
+// host buffer (*host, *len bytes) on the context's stream (the copy is
+// complete once the stream is).
+static int gather_keys(Ctx *c, void **host, uint64_t *len) {
+    const uint64_t n = c->n_recs;
+    const uint32_t nb = std::max<uint32_t>(1, (uint32_t)((n + kScanBlock - 1) / kScanBlock));
+    hipStream_t s = c->stream;
+    const size_t had = c->d_klb.cap;
+    int rc;
+    if ((rc = c->d_klb.ensure((nb + 2) * 8ull)) || (rc = c->d_koff.ensure((n + 1) * 8))) return rc;
+    if (c->d_klb.cap != had) GCK_HIP(hipMemsetAsync(c->d_klb.p, 0, c->d_klb.cap, s));  // then self-cleaning
+    k_scan_keys<<<nb, 64, 0, s>>>(c->d_rec_kv.as<uint2>(), n, c->d_koff.as<uint64_t>(), c->d_klb.as<uint64_t>());
+    uint64_t tot = 0;
+    GCK_HIP(hipMemcpyAsync(&tot, c->d_koff.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    if ((rc = c->d_keyblob.ensure(tot ? tot : 1))) return rc;
+    k_gather_keys<<<(uint32_t)c->n_cu * 4, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(),
+                                                        c->d_rec_kv.as<uint2>(), c->d_koff.as<uint64_t>(), n,
+                                                        c->d_keyblob.as<uint8_t>());
+    if (hipHostMalloc(host, tot ? tot : 1, hipHostMallocDefault) != hipSuccess) {
+        *host = nullptr;
+        return GCK_ENOMEM;
+    }
+    *len = tot;
+    if (tot) GCK_HIP(hipMemcpyAsync(*host, c->d_keyblob.p, tot, hipMemcpyDeviceToHost, s));
+    return GCK_OK;
+}
+
 // A data file to replay: caller memory (data), or an open file (fd, data null)
 struct Src {
     const uint8_t *data;
@@ -2386,9 +2488,16 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     for (uint32_t f = 0; f < nfiles; ++f)
         if (files[f].len && !files[f].data && files[f].fd < 0) return GCK_EINVAL;
     const uint64_t budget_opt = opts ? opts->max_resident : 0;
-    // group target: kGroupBytes, or a third of a tight budget (so at least
-    // two groups of files smaller than that fit at once)
-    const uint64_t tgt = budget_opt ? std::max<uint64_t>(1, std::min(kGroupBytes, budget_opt / 3)) : kGroupBytes;
+    // group target: about a quarter of the database (at least kGroupBytes),
+    // or a third of a tight budget (so at least two groups of files smaller
+    // than that fit at once).  Few groups: each is a device context, and
+    // creating 16 of them took 0.25-0.34 s of a 1.1 s Open of C3, while the
+    // replay a group hides under the next group's copy is ~100x shorter than
+    // that copy anyway.
+    uint64_t all_bytes = 0;
+    for (uint32_t f = 0; f < nfiles; ++f) all_bytes += files[f].len;
+    const uint64_t want = std::max<uint64_t>(kGroupBytes, all_bytes / kGroupsWanted);
+    const uint64_t tgt = budget_opt ? std::max<uint64_t>(1, std::min(want, budget_opt / 3)) : want;
     std::vector<uint32_t> cut{0};  // group g = files [cut[g], cut[g+1])
     {
         uint64_t acc = 0;
@@ -2428,10 +2537,15 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     std::vector<hipStream_t> own_s(R, nullptr);  // the contexts' own streams while they run on run_s
     std::vector<void *> chunks(G, nullptr);        // ring mode, gck_replay: each group's tuples (pinned)
     std::vector<uint64_t> chunk_n(G, 0);
+    const bool want_keys = opts && (opts->flags & GCK_OPT_KEYS);
+    std::vector<void *> kchunks(G, nullptr);  // GCK_OPT_KEYS: each group's key bytes (pinned)
+    std::vector<uint64_t> kchunk_n(G, 0);
     int rc = GCK_OK;
     Copier cp;  // the file copies (staging.hip)
     auto cleanup = [&](bool keep) {
         (void)cp.finish();
+        for (void *q : kchunks)
+            if (q) (void)hipHostFree(q);
         if (copy) (void)hipStreamSynchronize(copy);
         if (run_s) {
             (void)hipStreamSynchronize(run_s);
@@ -2454,11 +2568,19 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
                 gck_ctx_destroy(c);
         }
     };
+    // the staging buffers (pinned host memory, 0.15-0.25 s for 0.5-1 GiB on a
+    // process's first Open) are allocated on a helper thread while the
+    // contexts are created
+    int pre_rc = GCK_OK;
+    std::thread pre([&] { pre_rc = stage_prealloc(opts ? opts->device : 0, stage_buffers_wanted()); });
     for (uint32_t k = 0; k < R && !rc; ++k) rc = pool_take(opts, &cs[k]);
+    pre.join();
+    if (!rc) rc = pre_rc == GCK_ENOMEM ? GCK_OK : pre_rc;  // (the copier retries the allocation)
     if (rc) {
         cleanup(true);
         return rc;
     }
+    const auto t_ctx = std::chrono::steady_clock::now();
     const int dev = cs[0]->c.device;
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&copy, hipStreamNonBlocking) != hipSuccess) {
         cleanup(false);
@@ -2486,7 +2608,8 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
     if (trace)
-        fprintf(stderr, "[gck_replay] %u contexts ready, copier started at %.2f ms after the call\n", R,
+        fprintf(stderr, "[gck_replay] %u contexts ready at %.2f ms, copier started at %.2f ms after the call\n", R,
+                std::chrono::duration<double, std::milli>(t_ctx - t_call).count(),
                 std::chrono::duration<double, std::milli>(t_begin - t_call).count());
     hipEvent_t tev0 = nullptr;
     if (trace) {
@@ -2567,6 +2690,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
             rc = r;
             break;
         }
+        if (want_keys && c->n_recs && (rc = gather_keys(c, &kchunks[g], &kchunk_n[g]))) break;
         g_fail[g] = c->n_crc_fail;
         n_total += c->n_recs;
         st_status = c->status;
@@ -2590,9 +2714,11 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
                     rc = GCK_EDEVICE;
                 off += c->n_recs;
             }
-        } else if (c->n_recs && !into && R < G) {
-            // ring mode, library-owned output: the group's tuples into a pinned
-            // chunk now (its context is about to be reused), joined at the end
+        } else if (c->n_recs && !into) {
+            // library-owned output: the group's tuples into a pinned chunk now
+            // (written by the GPU through its mapping while later groups still
+            // copy; in ring mode the context is about to be reused), joined by
+            // the host at the end
             void *hp = nullptr, *dp = nullptr;
             if (hipHostMalloc(&hp, c->n_recs * sizeof(gck_rec), hipHostMallocMapped) != hipSuccess ||
                 hipHostGetDevicePointer(&dp, hp, 0) != hipSuccess) {
@@ -2638,44 +2764,52 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     out->files_walked = st_walked;
     out->final_last_offset = st_last;
     for (uint32_t g = 0; g < last; ++g) out->n_crc_fail += g_fail[g];
+    if (want_keys) {  // the groups' key bytes, in order
+        uint64_t kt = 0;
+        std::vector<std::pair<const void *, uint64_t>> segs;
+        for (uint32_t g = 0; g < last; ++g) {
+            kt += kchunk_n[g];
+            if (kchunk_n[g]) segs.emplace_back(kchunks[g], kchunk_n[g]);
+        }
+        if (hipStreamSynchronize(run_s) != hipSuccess) {
+            cleanup(false);
+            return GCK_EDEVICE;
+        }
+        void *kp = res_alloc(kt, false);
+        if (!kp) {
+            cleanup(true);
+            return GCK_ENOMEM;
+        }
+        par_gather(static_cast<uint8_t *>(kp), segs);
+        out->keys = static_cast<uint8_t *>(kp);
+        out->keys_len = kt;
+    }
     if (into) {
         cleanup(true);
         if (cap < n_total) return GCK_EINVAL;  // out->n says how many records to make room for
         return out->status;
     }
+    // the groups' pinned chunks into one plain array, in order
+    if (hipStreamSynchronize(run_s) != hipSuccess) {
+        cleanup(false);
+        return GCK_EDEVICE;
+    }
     gck_rec *h = nullptr;
     if (n_total) {
-        void *p = nullptr;
-        if (hipHostMalloc(&p, n_total * sizeof(gck_rec), hipHostMallocDefault) != hipSuccess) {
+        h = static_cast<gck_rec *>(res_alloc(n_total * sizeof(gck_rec), false));
+        if (!h) {
             cleanup(true);
             return GCK_ENOMEM;
         }
-        h = static_cast<gck_rec *>(p);
-    }
-    if (R < G) {  // the groups' chunks, in order
-        if (hipStreamSynchronize(run_s) != hipSuccess) rc = GCK_EDEVICE;
-        for (uint32_t g = 0; g < last && !rc; ++g) {
-            if (chunk_n[g]) memcpy(h + off, chunks[g], chunk_n[g] * sizeof(gck_rec));
-            off += chunk_n[g];
-        }
-    } else {
-        for (uint32_t g = 0; g < last && !rc; ++g) {
-            Ctx *c = &cs[g]->c;
-            if (!c->n_recs) continue;
-            if (cut[g]) k_rebase_file<<<(uint32_t)c->n_cu * 4, 256, 0, c->stream>>>(c->d_out.as<gck_rec>(), c->n_recs, cut[g]);
-            if (hipMemcpyAsync(h + off, c->d_out.p, c->n_recs * sizeof(gck_rec), hipMemcpyDeviceToHost, c->stream) !=
-                hipSuccess)
-                rc = GCK_EDEVICE;
-            off += c->n_recs;
-        }
-        if (hipStreamSynchronize(run_s) != hipSuccess) rc = GCK_EDEVICE;
-    }
-    if (rc) {
-        if (h) (void)hipHostFree(h);
-        cleanup(false);
-        return rc;
+        std::vector<std::pair<const void *, uint64_t>> segs;
+        for (uint32_t g = 0; g < last; ++g)
+            if (chunk_n[g]) segs.emplace_back(chunks[g], chunk_n[g] * sizeof(gck_rec));
+        par_gather(reinterpret_cast<uint8_t *>(h), segs);
     }
     out->recs = h;
+    if (trace)
+        fprintf(stderr, "[gck_replay] results in host memory at %.2f ms after the call\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count());
     cleanup(true);
     return out->status;
 }
@@ -2726,9 +2860,12 @@ int gck_replay_paths(const gck_path *files, uint32_t nfiles, const gck_opts *opt
 
 void gck_result_free(gck_result *res) {
     if (!res) return;
-    if (res->recs) (void)hipHostFree(res->recs);
+    res_free(res->recs);
+    res_free(res->keys);
     res->recs = nullptr;
+    res->keys = nullptr;
     res->n = 0;
+    res->keys_len = 0;
 }
 
 int gck_host_register(const void *p, uint64_t len) {

@@ -23,6 +23,7 @@
 #include <deque>
 #include <mutex>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "gck_internal.h"
@@ -30,7 +31,15 @@
 namespace gck {
 
 namespace {
-constexpr uint64_t kStageChunk = 32ull << 20;  // bytes per staging buffer
+// bytes per staging buffer (GCK_STAGE_MIB overrides, for measurements)
+uint64_t stage_chunk() {
+    static const uint64_t v = [] {
+        const char *e = getenv("GCK_STAGE_MIB");
+        const int m = e ? atoi(e) : 0;
+        return (uint64_t)(m >= 1 && m <= 256 ? m : 32) << 20;  // 8 MiB: 39-46 GB/s, 32 MiB: 53-55 GB/s
+    }();
+    return v;
+}
 
 // Page-locked staging buffers kept for the process, per device: a copier
 // takes the buffers it needs from the free list and gives them back when it
@@ -53,7 +62,7 @@ int stage_take(int dev, size_t n, std::vector<void *> &out) {
         }
     while (out.size() < n) {
         void *q = nullptr;
-        if (hipHostMalloc(&q, kStageChunk, hipHostMallocDefault) != hipSuccess) return GCK_ENOMEM;
+        if (hipHostMalloc(&q, stage_chunk(), hipHostMallocDefault) != hipSuccess) return GCK_ENOMEM;
         out.push_back(q);
     }
     return GCK_OK;
@@ -106,6 +115,72 @@ int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, cons
     if (hipStreamSynchronize(stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
     (void)hipEventDestroy(ev[0]);
     return rc;
+}
+
+uint32_t stage_buffers_wanted() { return 2 * copy_threads(); }
+
+int stage_prealloc(int dev, uint32_t n) {
+    std::vector<void *> b;
+    if (hipSetDevice(dev) != hipSuccess) return GCK_EDEVICE;
+    const int rc = stage_take(dev, n, b);
+    std::lock_guard<std::mutex> lk(g_stage.mu);
+    for (void *q : b) g_stage.idle.emplace_back(dev, q);
+    return rc;
+}
+
+// Host arrays handed to callers in gck_result (recs, keys): page-locked
+// (hipHostMalloc: D2H targets) or plain (malloc: assembled by the host from
+// page-locked pieces -- pinning a 0.4 GB array at the end of an Open took
+// 0.4-0.5 s); gck_result_free frees either.
+namespace {
+std::mutex g_res_mu;
+std::unordered_set<void *> g_res_pinned;
+}  // namespace
+
+void *res_alloc(uint64_t bytes, bool pinned) {
+    if (!bytes) bytes = 1;
+    if (!pinned) return malloc(bytes);
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_res_mu);
+    g_res_pinned.insert(p);
+    return p;
+}
+
+void res_free(void *p) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_res_mu);
+        auto it = g_res_pinned.find(p);
+        if (it != g_res_pinned.end()) {
+            g_res_pinned.erase(it);
+            (void)hipHostFree(p);
+            return;
+        }
+    }
+    free(p);
+}
+
+void par_gather(uint8_t *dst, const std::vector<std::pair<const void *, uint64_t>> &segs) {
+    uint64_t total = 0;
+    for (auto &s : segs) total += s.second;
+    const uint32_t T = total >= (64ull << 20) ? copy_threads() : 1;
+    auto part = [&](uint64_t lo, uint64_t hi) {  // destination bytes [lo, hi)
+        uint64_t at = 0;
+        for (auto &s : segs) {
+            const uint64_t a = std::max(lo, at), b = std::min(hi, at + s.second);
+            if (a < b) memcpy(dst + a, static_cast<const uint8_t *>(s.first) + (a - at), b - a);
+            at += s.second;
+            if (at >= hi) break;
+        }
+    };
+    if (T == 1) {
+        part(0, total);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; ++t) th.emplace_back(part, total * t / T, total * (t + 1) / T);
+    for (auto &x : th) x.join();
 }
 
 void stage_release() {
@@ -214,7 +289,7 @@ int Copier::start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev
     p->recorded.assign(G, 0);
     p->sealed.assign(G, 0);
     const uint32_t T = copy_threads();
-    const size_t nb = 2 * (size_t)T;
+    const size_t nb = stage_buffers_wanted();
     dev_ = dev;
     if (stage_take(dev, nb, p->bufs)) return GCK_ENOMEM;
     p->buf_ev.assign(nb, nullptr);
@@ -230,8 +305,9 @@ int Copier::start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev
 
 void Copier::add(uint32_t group, const uint8_t *src, int fd, uint64_t off, uint64_t len, uint8_t *dst) {
     std::lock_guard<std::mutex> lk(p->mu);
-    for (uint64_t o = 0; o < len; o += kStageChunk) {
-        const uint64_t n = std::min(kStageChunk, len - o);
+    const uint64_t C = stage_chunk();
+    for (uint64_t o = 0; o < len; o += C) {
+        const uint64_t n = std::min(C, len - o);
         p->jobs.push_back(Impl::Job{src, fd, off + o, n, dst + o, group});
         ++p->pending[group];
     }

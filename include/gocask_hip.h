@@ -75,13 +75,19 @@ typedef struct gck_rec {
     uint32_t crc_calc;   /* CRC-32/IEEE of the record's last ValueSize bytes               */
 } gck_rec;
 
-/* Tuning knobs; zero fields take the defaults.  Results never depend on them. */
+/* gck_opts.flags: gck_replay / gck_replay_into / gck_replay_paths also return
+ * the records' key bytes (gck_result.keys), so a caller that never maps the
+ * files (gck_replay_paths) can fill its keydir map. */
+#define GCK_OPT_KEYS 1u
+
+/* Tuning knobs; zero fields take the defaults.  Results never depend on them
+ * (GCK_OPT_KEYS adds an output). */
 typedef struct gck_opts {
     int32_t device;        /* HIP device ordinal (default 0)                               */
     uint32_t chunk_bytes;  /* boundary-speculation chunk (pow2 >= 4 KiB; default 512 KiB)  */
     uint32_t max_key;      /* speculation plausibility bound on key length (default 64K)  */
     uint32_t chunk_cap;    /* records staged per chunk before a re-walk (default 1024)    */
-    uint32_t flags;        /* reserved, 0                                                  */
+    uint32_t flags;        /* GCK_OPT_*                                                    */
     uint32_t spec_window;  /* bytes from a chunk's start searched for its first record    */
                            /* (rounded up to 4 KiB; default 0 = the whole chunk).  A      */
                            /* chunk whose first record lies further in is covered by the  */
@@ -92,7 +98,7 @@ typedef struct gck_opts {
 } gck_opts;
 
 typedef struct gck_result {
-    gck_rec *recs;              /* library-owned pinned host array; free with gck_result_free */
+    gck_rec *recs;              /* library-owned host array; free with gck_result_free  */
     uint64_t n;                 /* records in recs                                      */
     uint64_t n_crc_fail;        /* records whose verdict is a reject                    */
     uint32_t final_last_offset; /* keyDir.lastOffset after replay (later Puts use it)   */
@@ -102,6 +108,9 @@ typedef struct gck_result {
     uint64_t err_off;           /* header offset of the record that hit the error       */
     uint32_t n_groups;          /* gck_replay*: file groups the files were cut into     */
     uint32_t n_resident;        /* gck_replay*: groups resident at once (the ring)      */
+    uint8_t *keys;              /* GCK_OPT_KEYS: the records' key bytes back to back in */
+    uint64_t keys_len;          /* record order (record i's key_len bytes); freed by    */
+                                /* gck_result_free (gck_replay_into callers too)        */
 } gck_result;
 
 /* One-shot host-in/host-out replay: H2D, device pipeline, D2H.  Pipelined over

@@ -60,7 +60,8 @@ def test_abi_struct_layouts():
 
     assert L.REC_DTYPE.itemsize == 40
     assert ctypes.sizeof(L.GckFile) == 24
-    assert ctypes.sizeof(L.GckResult) == 56
+    assert ctypes.sizeof(L.GckResult) == 72  # + keys, keys_len (GCK_OPT_KEYS)
+    assert ctypes.sizeof(L.GckPath) == 16
     assert ctypes.sizeof(L.GckOpts) == 32
     assert ctypes.sizeof(L.GckCorpusCfg) == 72
 

@@ -108,3 +108,48 @@ def test_paths_missing_file(g, tmp_path):
     with pytest.raises(g._lib.GckError):
         g.replay_paths([str(tmp_path / "absent.csk")], [False])
     assert not os.path.exists(tmp_path / "absent.csk")
+
+
+def _want_keys(files, want):
+    """The oracle records' key bytes back to back (record i: key_len bytes at
+    its header + 16; a tombstone's key is its value, core/db.go:151-155)."""
+    out = bytearray()
+    for r in want:
+        f = np.asarray(files[int(r["file"])], dtype=np.uint8)
+        o = int(r["rec_off"]) + 16
+        out += bytes(f[o:o + int(r["key_len"])])
+    return np.frombuffer(bytes(out), np.uint8)
+
+
+@pytest.mark.parametrize("budget", [0, 1 << 20])
+def test_keys_blob(g, orc, tmp_path, budget):
+    # GCK_OPT_KEYS: a caller that never maps the files gets the key bytes with
+    # the records (the Go map needs them), for every entry point
+    wf, reset = _corpus(orc, seed=96)
+    want, wst = orc.replay(wf, reset)
+    wk = _want_keys(wf, want)
+    got, gst = g.replay_paths(_write(tmp_path, wf), reset, max_resident=budget, keys=True)
+    _same(got, gst, want, wst)
+    assert np.array_equal(gst["keys"], wk)
+    got, gst = g.replay(wf, reset, max_resident=budget, keys=True)
+    assert np.array_equal(gst["keys"], wk)
+    recs = np.zeros(len(want), dtype=g.REC_DTYPE)
+    st = g.replay_into(wf, recs, reset, max_resident=budget, keys=True)
+    _same(recs, st, want, wst)
+    assert np.array_equal(st["keys"], wk)
+    # without the flag: no blob
+    _, gst = g.replay(wf, reset, max_resident=budget)
+    assert "keys" not in gst
+
+
+def test_keys_blob_with_startup_error(g, orc, tmp_path):
+    # only the records the reference applies before the error, and their keys
+    wf, reset = _corpus(orc, seed=97, n_files=5)
+    bad = np.frombuffer(orc_mod.entry(1, b"user", b"x" * 10) + orc_mod.entry(2, b"key", b"yy")[:-4], np.uint8)
+    wf = wf[:3] + [bad] + wf[3:]
+    reset = reset[:3] + [True] + reset[3:]
+    want, wst = orc.replay(wf, reset)
+    assert wst["status"] != 0
+    got, gst = g.replay_paths(_write(tmp_path, wf), reset, max_resident=2 << 20, keys=True)
+    _same(got, gst, want, wst)
+    assert np.array_equal(gst["keys"], _want_keys(wf, want))
