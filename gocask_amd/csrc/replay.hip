@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         found = 0;
     } else {
         // The scan loop only computes candidate masks (no dependent loads in
-        // it, so the next windows' loads stay in flight: windows A/B/C rotate,
+        // it, so the next window's loads stay in flight: windows A/B rotate,
         // unrolled so none is copied); a window with candidates leaves the
         // loop for the chain tests and the scan resumes after it if none holds.
         // Lane L scans positions [64 L, 64 L + 64) of a 4 KiB window and
@@ -245,29 +245,27 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
             }
             return cm;
         };
-        // positions searched: [cs, lim).  The windows are loaded up to two
-        // ahead unconditionally (the arena is padded past every file; a
-        // branch around a load would cost the prefetch its place).
+        // positions searched: [cs, lim).  The next window is loaded one ahead,
+        // unconditionally (the arena is padded past every file; a branch
+        // around a load would cost the prefetch its place).  Two ahead read a
+        // sixth more (a chunk's entry is 4.3 windows in on C3, the prefetch
+        // past it is wasted) and measured 2 % slower: 0.289-0.291 against
+        // 0.284 ms; the first window alone before any prefetch, 0.302-0.310.
         const uint64_t lim = ce - cs > window ? cs + window : ce;
         uint64_t from = cs;
         while (found == kNone && from < lim) {
             uint64_t wb = kNone, cm = 0;
-            u32x4 A[5], B[5], C[5];
+            u32x4 A[5], B[5];
             load(from, A);
-            load(from + 4096, B);
-            for (uint64_t b0 = from;; b0 += 3 * 4096) {
-                load(b0 + 2 * 4096, C);
+            for (uint64_t b0 = from;; b0 += 2 * 4096) {
+                load(b0 + 4096, B);
                 cm = cands(A);
                 if (__ballot(cm != 0)) { wb = b0; break; }
                 if (b0 + 4096 >= lim) break;
-                load(b0 + 3 * 4096, A);
+                load(b0 + 2 * 4096, A);
                 cm = cands(B);
                 if (__ballot(cm != 0)) { wb = b0 + 4096; break; }
                 if (b0 + 2 * 4096 >= lim) break;
-                load(b0 + 4 * 4096, B);
-                cm = cands(C);
-                if (__ballot(cm != 0)) { wb = b0 + 2 * 4096; break; }
-                if (b0 + 3 * 4096 >= lim) break;
             }
             if (wb == kNone) break;
             // Candidates in scan order are lane l's bits, then lane l + 1's.
