@@ -8,7 +8,7 @@ from .core import (GB, KB, MB, TB, Config, DB, DefaultConfig, ErrCRCFailed, ErrI
                    ErrKeyNotFound, ErrPartialWrite, ErrUnexpectedEOF, GoCaskError, InMemoryDB, NewDB, NewDisk,
                    NewInMemory, Open, ReplayContext, StartupError, WithDataDir, WithMaxDataFileSize, device_count,
                    host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into, replay_paths,
-                   replay_multi, zipf_table)
+                   replay_multi, replay_multi_paths, zipf_table)
 from ._lib import F_CRC_OK, F_TOMBSTONE, REC_DTYPE
 
 __all__ = [
@@ -16,5 +16,5 @@ __all__ = [
     "ErrKeyNotFound", "ErrPartialWrite", "ErrUnexpectedEOF", "GoCaskError", "InMemoryDB", "NewDB", "NewDisk",
     "NewInMemory", "Open", "ReplayContext", "StartupError", "WithDataDir", "WithMaxDataFileSize", "device_count",
     "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into", "replay_paths",
-    "replay_multi", "zipf_table", "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
+    "replay_multi", "replay_multi_paths", "zipf_table", "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
 ]

@@ -301,18 +301,40 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resi
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_multi(files, reset_after=None, devices=(0,), chunk_bytes=0):
+def replay_multi(files, reset_after=None, devices=(0,), chunk_bytes=0, keys=False):
     """gck_replay_multi: the files sharded over `devices` (one rank each), the
     keydir merged across them with RCCL inside the library.  Returns (live
-    keydir records, REC_DTYPE with global file indices; status dict)."""
+    keydir records, REC_DTYPE with global file indices; status dict, with the
+    live entries' key bytes under "keys" when keys=True)."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     devs = np.ascontiguousarray(devices, dtype=np.int32)
     res = GckResult()
-    rc = L.gck_replay_multi(fa, len(arrs), devs.ctypes.data, len(devs), ctypes.byref(_opts(int(devs[0]), chunk_bytes)),
-                            ctypes.byref(res))
+    rc = L.gck_replay_multi(fa, len(arrs), devs.ctypes.data, len(devs),
+                            ctypes.byref(_opts(int(devs[0]), chunk_bytes, keys=keys)), ctypes.byref(res))
+    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+    try:
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
+def replay_multi_paths(paths, reset_after=None, devices=(0,), chunk_bytes=0, keys=False):
+    """gck_replay_multi_paths: replay_multi of files named by path."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(paths)
+    enc = [os.fsencode(p) for p in paths]
+    pa = (_lib.GckPath * max(1, len(enc)))()
+    for i, p in enumerate(enc):
+        pa[i].path = p
+        pa[i].reset_after = 1 if reset_after[i] else 0
+    devs = np.ascontiguousarray(devices, dtype=np.int32)
+    res = GckResult()
+    rc = L.gck_replay_multi_paths(pa, len(enc), devs.ctypes.data, len(devs),
+                                  ctypes.byref(_opts(int(devs[0]), chunk_bytes, keys=keys)), ctypes.byref(res))
     check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
     try:
         return _result(res)

@@ -187,9 +187,21 @@ void *res_alloc(uint64_t bytes, bool pinned);
 void res_free(void *p);
 // dst = the segments back to back (host threads for large totals)
 void par_gather(uint8_t *dst, const std::vector<std::pair<const void *, uint64_t>> &segs);
+// A data file to replay: caller memory (data), or an open file (fd, data null)
+struct Src {
+    const uint8_t *data;
+    int fd;
+    uint64_t len;
+    bool reset_after;
+};
+std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles);
+// opens and stats every path (GCK_EIO when one fails; then none stays open)
+int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &out);
+void close_srcs(std::vector<Src> &v);
 // n files into device memory through a Copier on stream, then waits for them
-int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, const uint64_t *len, uint8_t *const *dst,
-                    uint32_t n);
+int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const *dst, uint32_t n);
+// gck_ctx_load of sources: layout, then the copies
+int ctx_load_srcs(Ctx *c, const Src *src, uint32_t n);
 
 }  // namespace gck
 

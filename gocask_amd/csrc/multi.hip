@@ -153,13 +153,12 @@ extern "C" int gck_plan_shards(const uint64_t *sizes, const uint8_t *reset_after
     return GCK_OK;
 }
 
-extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
-                                const gck_opts *opts, gck_result *out) {
-    if (!out) return GCK_EINVAL;
-    memset(out, 0, sizeof(*out));
+static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
+                        const gck_opts *opts, gck_result *out) {
     if ((nfiles && !files) || !devices || ndev == 0 || ndev > 64) return GCK_EINVAL;
     for (uint32_t f = 0; f < nfiles; ++f)
-        if (files[f].len && !files[f].data) return GCK_EINVAL;
+        if (files[f].len && !files[f].data && files[f].fd < 0) return GCK_EINVAL;
+    const bool want_keys = opts && (opts->flags & GCK_OPT_KEYS);
     std::vector<int> devs(devices, devices + ndev);
     {
         std::vector<int> s = devs;
@@ -211,7 +210,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         if (opts) o = *opts;
         o.device = devs[s];
         if ((x.rc = gck_ctx_create(&o, &x.ctx))) return;
-        if ((x.rc = gck_ctx_load(x.ctx, files + x.a, x.b - x.a))) return;
+        if ((x.rc = ctx_load_srcs(&x.ctx->c, files + x.a, x.b - x.a))) return;
         if (x.b > x.a) {
             x.rc = gck_ctx_run(x.ctx);
             if (x.rc == GCK_EUNEXPECTED_EOF) x.rc = GCK_OK;  // the run's outcome is in its stats
@@ -353,6 +352,7 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         if (!h) rc = GCK_ENOMEM;
     }
     uint64_t at = 0;
+    std::vector<uint8_t> kblob;  // GCK_OPT_KEYS: the entries' key bytes in output order
     for (uint32_t p = 0; p < ndev && !rc; ++p) {
         uint64_t n = 0, nk = 0;
         if ((rc = gck_kd_fetch_merged(sh[p].ctx, nullptr, 0, nullptr, 0, &n, &nk))) break;
@@ -360,18 +360,51 @@ extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const in
         std::vector<gck_kd_entry> ents(n);
         std::vector<uint8_t> keys(nk + 1);
         if ((rc = gck_kd_fetch_merged(sh[p].ctx, ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
-        for (uint64_t i = 0; i < n; ++i) h[at + i] = ents[i].rec;
+        for (uint64_t i = 0; i < n; ++i) {
+            h[at + i] = ents[i].rec;
+            if (want_keys) kblob.insert(kblob.end(), keys.begin() + (ptrdiff_t)ents[i].key_off,
+                                        keys.begin() + (ptrdiff_t)(ents[i].key_off + ents[i].key_len));
+        }
         at += n;
+    }
+    if (!rc && want_keys) {
+        out->keys = static_cast<uint8_t *>(res_alloc(kblob.size(), false));
+        if (!out->keys) rc = GCK_ENOMEM;
+        else if (!kblob.empty()) memcpy(out->keys, kblob.data(), kblob.size());
+        out->keys_len = kblob.size();
     }
     mark("merged+fetched");
     cleanup();
     mark("freed");
     if (rc) {
         res_free(h);
+        res_free(out->keys);
         memset(out, 0, sizeof(*out));
         return rc;
     }
     out->recs = h;
     out->n = tot;
     return out->status;
+}
+
+extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
+                                const gck_opts *opts, gck_result *out) {
+    if (!out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    if (nfiles && !files) return GCK_EINVAL;
+    const std::vector<Src> v = mem_srcs(files, nfiles);
+    return replay_multi(v.data(), nfiles, devices, ndev, opts, out);
+}
+
+extern "C" int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
+                                      const gck_opts *opts, gck_result *out) {
+    if (!out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    if (nfiles && !files) return GCK_EINVAL;
+    std::vector<Src> v;
+    int rc = open_srcs(files, nfiles, v);
+    if (rc) return rc;
+    rc = replay_multi(v.data(), nfiles, devices, ndev, opts, out);
+    close_srcs(v);
+    return rc;
 }

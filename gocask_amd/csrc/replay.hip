@@ -2207,26 +2207,31 @@ void gck_ctx_destroy(gck_ctx *ctx) {
     delete ctx;
 }
 
-int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles) {
-    if (!ctx || (nfiles && !files)) return GCK_EINVAL;
+}  // extern "C"
+
+int gck::ctx_load_srcs(Ctx *c, const Src *src, uint32_t nfiles) {
     std::vector<uint64_t> lens(nfiles);
     std::vector<uint8_t> reset(nfiles);
     for (uint32_t f = 0; f < nfiles; ++f) {
-        if (files[f].len && !files[f].data) return GCK_EINVAL;
-        lens[f] = files[f].len;
-        reset[f] = files[f].reset_after ? 1 : 0;
+        if (src[f].len && !src[f].data && src[f].fd < 0) return GCK_EINVAL;
+        lens[f] = src[f].len;
+        reset[f] = src[f].reset_after ? 1 : 0;
     }
-    int rc = ctx_layout(&ctx->c, lens.data(), nfiles, reset.data());
+    int rc = ctx_layout(c, lens.data(), nfiles, reset.data());
     if (rc) return rc;
-    // pageable memory through the staging copier (host threads, page-locked
-    // buffers), registered memory by DMA as is
-    std::vector<const uint8_t *> src(nfiles);
+    // pageable memory and files through the staging copier (host threads,
+    // page-locked buffers), registered memory by DMA as is
     std::vector<uint8_t *> dst(nfiles);
-    for (uint32_t f = 0; f < nfiles; ++f) {
-        src[f] = files[f].data;
-        dst[f] = ctx->c.arena.as<uint8_t>() + ctx->c.f_base[f];
-    }
-    return copy_files_sync(ctx->c.device, ctx->c.stream, src.data(), lens.data(), dst.data(), nfiles);
+    for (uint32_t f = 0; f < nfiles; ++f) dst[f] = c->arena.as<uint8_t>() + c->f_base[f];
+    return copy_files_sync(c->device, c->stream, src, dst.data(), nfiles);
+}
+
+extern "C" {
+
+int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles) {
+    if (!ctx || (nfiles && !files)) return GCK_EINVAL;
+    const std::vector<Src> v = mem_srcs(files, nfiles);
+    return ctx_load_srcs(&ctx->c, v.data(), nfiles);
 }
 
 int gck_ctx_run(gck_ctx *ctx) {
@@ -2470,14 +2475,6 @@ static int gather_keys(Ctx *c, void **host, uint64_t *len) {
     if (tot) GCK_HIP(hipMemcpyAsync(*host, c->d_keyblob.p, tot, hipMemcpyDeviceToHost, s));
     return GCK_OK;
 }
-
-// A data file to replay: caller memory (data), or an open file (fd, data null)
-struct Src {
-    const uint8_t *data;
-    int fd;
-    uint64_t len;
-    bool reset_after;
-};
 
 static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
                           uint64_t cap, gck_result *out) {
@@ -2812,12 +2809,6 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     return out->status;
 }
 
-static std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles) {
-    std::vector<Src> v(nfiles);
-    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, -1, files[f].len, files[f].reset_after != 0};
-    return v;
-}
-
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
@@ -2837,22 +2828,11 @@ int gck_replay_paths(const gck_path *files, uint32_t nfiles, const gck_opts *opt
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
     if (nfiles && !files) return GCK_EINVAL;
-    std::vector<Src> v(nfiles, Src{nullptr, -1, 0, false});
-    auto close_all = [&] {
-        for (auto &s : v)
-            if (s.fd >= 0) close(s.fd);
-    };
-    for (uint32_t f = 0; f < nfiles; ++f) {
-        struct stat st;
-        if (!files[f].path || (v[f].fd = open(files[f].path, O_RDONLY | O_CLOEXEC)) < 0 || fstat(v[f].fd, &st) != 0) {
-            close_all();
-            return GCK_EIO;
-        }
-        v[f].len = (uint64_t)st.st_size;
-        v[f].reset_after = files[f].reset_after != 0;
-    }
-    const int rc = replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
-    close_all();
+    std::vector<Src> v;
+    int rc = open_srcs(files, nfiles, v);
+    if (rc) return rc;
+    rc = replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
+    close_srcs(v);
     return rc;
 }
 

@@ -13,6 +13,7 @@
 // than the transfer itself: 1.3 s + 0.5-1.3 s against 0.6 s of PCIe for C3
 // (DESIGN.md §9b).
 #include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -91,8 +92,7 @@ bool host_pinned(const void *p) {
     return false;
 }
 
-int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, const uint64_t *len, uint8_t *const *dst,
-                    uint32_t n) {
+int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const *dst, uint32_t n) {
     std::vector<hipEvent_t> ev(1, nullptr);
     if (hipSetDevice(dev) != hipSuccess || hipEventCreateWithFlags(&ev[0], hipEventDisableTiming) != hipSuccess)
         return GCK_EDEVICE;
@@ -101,11 +101,11 @@ int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, cons
         Copier cp;
         rc = cp.start(dev, stream, &ev);
         for (uint32_t f = 0; f < n && !rc; ++f) {
-            if (!len[f]) continue;
-            if (host_pinned(src[f]))
-                rc = cp.direct(src[f], len[f], dst[f]);
+            if (!src[f].len) continue;
+            if (src[f].data && host_pinned(src[f].data))
+                rc = cp.direct(src[f].data, src[f].len, dst[f]);
             else
-                cp.add(0, src[f], -1, 0, len[f], dst[f]);
+                cp.add(0, src[f].data, src[f].fd, 0, src[f].len, dst[f]);
         }
         cp.seal(0);
         if (!rc) rc = cp.wait_recorded(0);
@@ -115,6 +115,34 @@ int copy_files_sync(int dev, hipStream_t stream, const uint8_t *const *src, cons
     if (hipStreamSynchronize(stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
     (void)hipEventDestroy(ev[0]);
     return rc;
+}
+
+std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles) {
+    std::vector<Src> v(nfiles);
+    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, -1, files[f].len, files[f].reset_after != 0};
+    return v;
+}
+
+int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &v) {
+    v.assign(nfiles, Src{nullptr, -1, 0, false});
+    for (uint32_t f = 0; f < nfiles; ++f) {
+        struct stat st;
+        if (!files[f].path || (v[f].fd = open(files[f].path, O_RDONLY | O_CLOEXEC)) < 0 || fstat(v[f].fd, &st) != 0) {
+            close_srcs(v);
+            return GCK_EIO;
+        }
+        v[f].len = (uint64_t)st.st_size;
+        v[f].reset_after = files[f].reset_after != 0;
+    }
+    return GCK_OK;
+}
+
+void close_srcs(std::vector<Src> &v) {
+    for (auto &s : v)
+        if (s.fd >= 0) {
+            close(s.fd);
+            s.fd = -1;
+        }
 }
 
 uint32_t stage_buffers_wanted() { return 2 * copy_threads(); }

@@ -304,6 +304,11 @@ int gck_kd_fetch_merged(gck_ctx *ctx, gck_kd_entry *dst, uint64_t cap, uint8_t *
  * gck_result_free.  GCK_EDEVICE when RCCL cannot be loaded or a device fails. */
 int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
                      const gck_opts *opts, gck_result *out);
+/* gck_replay_multi of files named by path (read by the library, as
+ * gck_replay_paths); with GCK_OPT_KEYS the live entries' key bytes come back
+ * in out->keys, in the order of out->recs (either call). */
+int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
+                           const gck_opts *opts, gck_result *out);
 /* The shard plan (host only, no device): shard s = files [ranges[2 s],
  * ranges[2 s + 1]); empty shards when there are fewer allowed cuts than
  * shards.  A cut at i needs reset_after[i - 1] (core/db.go:117-119). */

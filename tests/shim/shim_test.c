@@ -26,8 +26,9 @@
  * SHIM_MULTI=1: gck_replay_multi on device 0 (the live keydir comes back).
  * SHIM_PIN=0: map the files but do not register them (the library stages the
  * pageable mappings through its own page-locked buffers).
- * SHIM_PATHS=1: gck_replay_paths -- the library opens and reads the files
- * itself (the shim maps them only to print keys, never when timing).
+ * SHIM_PATHS=1: gck_replay_paths (with SHIM_MULTI=1 gck_replay_multi_paths)
+ * -- the library opens and reads the files itself (the shim maps them only
+ * to print keys, never when timing).
  */
 #define _GNU_SOURCE
 #include <dirent.h>
@@ -197,7 +198,12 @@ int main(int argc, char **argv) {
                 gp[i].path = g_files[i].path;
                 gp[i].reset_after = gf[i].reset_after;
             }
-            rc = gck_replay_paths(gp, (uint32_t)g_n, NULL, &res);
+            if (multi) {
+                const int32_t dev0 = 0;
+                rc = gck_replay_multi_paths(gp, (uint32_t)g_n, &dev0, 1, NULL, &res);
+            } else {
+                rc = gck_replay_paths(gp, (uint32_t)g_n, NULL, &res);
+            }
             free(gp);
         } else if (multi) {
             const int32_t dev0 = 0;

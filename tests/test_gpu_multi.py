@@ -102,3 +102,31 @@ def test_multi_rejects_a_device_twice(g):
     files = [np.frombuffer(orc_mod.entry(1, b"k", b"v"), np.uint8)]
     with pytest.raises(g._lib.GckError):
         g.replay_multi(files, [False], devices=[0, 0])
+
+
+def _keys_of(files, got):
+    out = bytearray()
+    for r in got:
+        o = int(r["rec_off"]) + 16
+        out += bytes(np.asarray(files[int(r["file"])], dtype=np.uint8)[o:o + int(r["key_len"])])
+    return np.frombuffer(bytes(out), np.uint8)
+
+
+@pytest.mark.parametrize("name", ["keys_in_order", "updated_values_across_files", "deleted_after_startup",
+                                  "datatxt_1000_puts", "partial_write_desync"])
+def test_multi_by_path_with_keys(g, orc, tmp_path, name):
+    """gck_replay_multi_paths (the library reads the files) and GCK_OPT_KEYS
+    (the live entries' key bytes in the order of the records): the same
+    keydir as from memory, and the keys those records point at."""
+    _, files, reset = load_case(name)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"{i:03d}.csk"
+        p.write_bytes(f.tobytes())
+        paths.append(str(p))
+    want, wst = orc.replay(files, reset)
+    got, gst = g.replay_multi_paths(paths, reset, devices=[0], keys=True)
+    _check(files, got, gst, want, wst)
+    assert np.array_equal(gst["keys"], _keys_of(files, got))
+    got2, gst2 = g.replay_multi(files, reset, devices=[0], keys=True)
+    assert np.array_equal(got2, got) and np.array_equal(gst2["keys"], gst["keys"])

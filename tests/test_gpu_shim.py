@@ -134,3 +134,4 @@ def test_shim_pageable_and_by_path_same_keydir(shim, orc, tmp_path, name):
     pinned = run(shim, tmp_path, meta["active"])
     assert run(shim, tmp_path, meta["active"], mode="pageable") == pinned
     assert run(shim, tmp_path, meta["active"], mode="paths") == pinned
+    assert run(shim, tmp_path, meta["active"], mode="paths", multi=True) == pinned

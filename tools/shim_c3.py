@@ -35,7 +35,8 @@ try:
             del buf
     shim = os.path.join(ROOT, "tests", "shim", "build", "shim_test")
     out = []
-    modes = [dict(SHIM_PATHS="1"), dict(SHIM_PIN="0"), dict(SHIM_PIN="1"), dict(SHIM_PIN="1", SHIM_MULTI="1")]
+    modes = [dict(SHIM_PATHS="1"), dict(SHIM_PIN="0"), dict(SHIM_PIN="1"), dict(SHIM_PIN="1", SHIM_MULTI="1"),
+             dict(SHIM_PATHS="1", SHIM_MULTI="1")]
     if len(sys.argv) > 2:
         modes = modes[:int(sys.argv[2])]
     # SHIM_THREADS="4 8 16": the by-path / pageable modes at each copy-thread count
