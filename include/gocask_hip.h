@@ -114,10 +114,12 @@ typedef struct gck_result {
 } gck_result;
 
 /* One-shot host-in/host-out replay: H2D, device pipeline, D2H.  Pipelined over
- * groups of files (>= 1 GiB, or a third of opts->max_resident; cut after files
- * that reset lastOffset): each group replays as soon as its own files are
- * resident, while later groups still cross PCIe (register the files with
- * gck_host_register for asynchronous DMA).  A ring of groups bounds the device
+ * groups of files (about a quarter of the database, >= 1 GiB, or a third of
+ * opts->max_resident; cut after files that reset lastOffset): each group
+ * replays as soon as its own files are resident, while later groups still
+ * cross PCIe.  Registered memory (gck_host_register) goes by DMA as is; other
+ * memory is staged by the library's host threads through page-locked buffers
+ * (no registration needed).  A ring of groups bounds the device
  * memory (opts->max_resident): a database larger than it streams through.
  * Results are those of one replay of all files in walk order.  GCK_ENOMEM:
  * the device could not hold even one group (a caller may fall back to the CPU
