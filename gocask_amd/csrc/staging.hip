@@ -288,7 +288,10 @@ struct Copier::Impl {
                 }
             }
             std::lock_guard<std::mutex> lk(mu);
-            if (!ok && !err) err = GCK_EINVAL;  // the file shrank or could not be read
+            if (!ok && !err) {  // the file shrank or could not be read
+                err = GCK_EIO;
+                set_error("pread", hipSuccess, __FILE__, __LINE__);
+            }
             if (ok && (hipMemcpyAsync(j.dst, stage, j.len, hipMemcpyHostToDevice, stream) != hipSuccess ||
                        hipEventRecord(buf_ev[b], stream) != hipSuccess) &&
                 !err)

@@ -104,10 +104,19 @@ def test_paths_startup_error_and_empty_files(g, orc, tmp_path):
     _same(got, gst, want, wst)
 
 
-def test_paths_missing_file(g, tmp_path):
-    with pytest.raises(g._lib.GckError):
+def test_paths_missing_or_unreadable_file(g, tmp_path):
+    with pytest.raises(g._lib.GckError) as e:
         g.replay_paths([str(tmp_path / "absent.csk")], [False])
+    assert e.value.code == g._lib.GCK_EIO
     assert not os.path.exists(tmp_path / "absent.csk")
+    # a directory opens and stats but cannot be read: the copier's pread fails
+    d = tmp_path / "adir.csk"
+    d.mkdir()
+    (d / "x").write_bytes(b"y" * 100)
+    if os.stat(d).st_size > 0:
+        with pytest.raises(g._lib.GckError) as e:
+            g.replay_paths([str(d)], [False])
+        assert e.value.code == g._lib.GCK_EIO
 
 
 def _want_keys(files, want):
