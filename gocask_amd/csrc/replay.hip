@@ -338,6 +338,10 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
 // instead of 64 scattered partial lines (measured: those cost half of the
 // walk), and k_compact still reads a chunk's slots at a short stride.
 constexpr uint32_t kStageIl = 8;
+#ifndef GCK_PRE_BATCHES
+#define GCK_PRE_BATCHES 3
+#endif
+constexpr uint32_t kPreBatches = GCK_PRE_BATCHES;  // stage batches of 64 k_compact loads up front (C3: 154 records per chunk on average)
 __host__ __device__ __forceinline__ uint64_t stage_slot(uint32_t c, uint32_t i, uint32_t cap) {
     return ((uint64_t)(c / kStageIl) * (cap + 1) + (i < cap ? i : cap)) * kStageIl + (c % kStageIl);
 }
@@ -803,22 +807,35 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
     if (c >= n_chunks) return;
+    // everything a chunk needs in one round trip: its entry, count, record
+    // base and file, and the first kPreBatches batches of its stage (slots
+    // past the count or the capacity read the chunk's scratch slot, which
+    // exists); then the file's base.  (Loaded in turn, these were four
+    // dependent round trips before the first record.)
     const uint64_t entry = ch_entry[c];
     const uint32_t cnt = ch_count[c];
     const uint64_t rb = rec_base[c];
-    if (entry == kNone || cnt == 0 || rb >= n_total) return;
     const uint32_t f = ch_file[c];
+    uint2 pre[kPreBatches];
+#pragma unroll
+    for (uint32_t k = 0; k < kPreBatches; ++k) pre[k] = s_kv[stage_slot(c0 + c, 64 * k + lane, cap)];
+    if (entry == kNone || cnt == 0 || rb >= n_total) return;
     const uint64_t base = fbase[f];
     if (cnt <= cap) {
         uint64_t run = base + entry;  // arena offset of the next record
-        // the next batch's stage entries are loaded while this batch is
-        // written (a batch per round trip otherwise: ~3 per chunk on C3)
-        uint2 nxt = lane < cnt ? s_kv[stage_slot(c0 + c, lane, cap)] : make_uint2(0u, 0u);
+        // batches past the preloaded ones: the next batch's stage entries
+        // are loaded while this batch is written
+        uint2 nxt = make_uint2(0u, 0u);
         for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
             const uint32_t i = i0 + lane;
             const bool in = i < cnt;
-            const uint2 kv = nxt;
-            nxt = i + 64 < cnt ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
+            const uint32_t b = i0 / 64;  // (uniform)
+            uint2 kv = nxt;
+#pragma unroll
+            for (uint32_t k = 0; k < kPreBatches; ++k)
+                if (b == k) kv = pre[k];
+            if (!in) kv = make_uint2(0u, 0u);
+            if (b + 1 >= kPreBatches) nxt = i + 64 < cnt ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
             // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
             // inclusive scan is exact in 24-bit halves (entries < 2^33)
             const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
