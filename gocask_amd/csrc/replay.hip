@@ -502,6 +502,11 @@ __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
     const uint32_t lo = wave_incl_sum((uint32_t)(v & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(v >> 24));
     return ((uint64_t)hi << 24) + lo;
 }
+// 64-bit value of lane 63 in every lane
+__device__ __forceinline__ uint64_t lane63(uint64_t v) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
 
 // The host bookkeeping of a run (core/db.go:110-140) on the device, so a run
 // needs no host round trip.  Per file the lastOffset carried in (reset after
@@ -561,27 +566,37 @@ __device__ __forceinline__ uint32_t lb_ticket(uint32_t *tickets) {
 // block b's exclusive base: its total published at once, then the earlier
 // blocks' totals / inclusive prefixes read back until an inclusive one
 __device__ uint64_t lookback_excl(uint64_t *lb, uint32_t b, uint64_t btot) {
-    uint64_t excl = 0;
-    if ((threadIdx.x & 63) == 0) {
-        if (b == 0) {
-            __hip_atomic_store(&lb[0], btot | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_store(&lb[b], btot | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = (int64_t)b - 1; j >= 0;) {
-                const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (!(w & (kLbAgg | kLbInc))) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                excl += w & kLbVal;
-                if (w & kLbInc) break;
-                --j;
-            }
-            __hip_atomic_store(&lb[b], (excl + btot) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    const uint32_t lane = threadIdx.x & 63;
+    if (b == 0) {
+        if (lane == 0) __hip_atomic_store(&lb[0], btot | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
     }
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(excl >> 32), 0) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)excl, 0);
+    if (lane == 0) __hip_atomic_store(&lb[b], btot | kLbAgg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // lane k reads block top - k: up to 64 predecessors per round trip
+    // (one at a time, a block waited for one L2 round trip per predecessor)
+    uint64_t excl = 0;
+    for (int64_t top = (int64_t)b - 1; top >= 0;) {
+        const int64_t j = top - (int64_t)lane;
+        const uint64_t w = j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : kLbInc;  // before block 0: an inclusive prefix of 0
+        const uint64_t inc = __ballot((w & kLbInc) != 0), nready = __ballot((w & (kLbAgg | kLbInc)) == 0);
+        // the nearest inclusive prefix (lane fi) ends the look-back; every
+        // block between must have published its total
+        const uint32_t fi = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+        const uint64_t need = fi < 64 ? (2ull << fi) - 1 : ~0ull;
+        if (nready & need) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = lane <= fi ? (w & kLbVal) : 0;
+        // sum over the lanes (values < 2^48: two 24-bit halves)
+        const uint64_t sv = lane63(wave_incl_sum64(v));
+        excl += sv;
+        if (fi < 64) break;
+        top -= 64;
+    }
+    if (lane == 0) __hip_atomic_store(&lb[b], (excl + btot) | kLbInc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
 }
 // true in the wavefront that finishes last (every block's output visible)
 __device__ bool lb_last_done(uint32_t *tickets, uint32_t nb) {
@@ -591,11 +606,6 @@ __device__ bool lb_last_done(uint32_t *tickets, uint32_t nb) {
     if ((uint32_t)__builtin_amdgcn_readfirstlane((int)dn) != nb - 1) return false;
     __threadfence();
     return true;
-}
-// 64-bit value of lane 63 in every lane
-__device__ __forceinline__ uint64_t lane63(uint64_t v) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
 }
 __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__ ch_count, uint64_t *rec_base,
                                                     uint32_t n, uint64_t *lb, uint64_t *base_out, uint64_t cap,
