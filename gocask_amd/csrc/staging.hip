@@ -290,7 +290,8 @@ struct Copier::Impl {
             std::lock_guard<std::mutex> lk(mu);
             if (!ok && !err) {  // the file shrank or could not be read
                 err = GCK_EIO;
-                set_error("pread", hipSuccess, __FILE__, __LINE__);
+                set_error("pread of a data file failed (unreadable, or shorter than its stat size)", hipSuccess, __FILE__,
+                          __LINE__);
             }
             if (ok && (hipMemcpyAsync(j.dst, stage, j.len, hipMemcpyHostToDevice, stream) != hipSuccess ||
                        hipEventRecord(buf_ev[b], stream) != hipSuccess) &&
