@@ -43,14 +43,20 @@ try:
     threads = os.environ.get("SHIM_THREADS", "").split()
     if threads:
         modes = [dict(m, GCK_COPY_THREADS=t) for t in threads for m in modes if m.get("SHIM_PIN") != "1"]
-    for mode in modes:
-        for r in range(reps):
-            p = subprocess.run([shim, d], capture_output=True, text=True, timeout=300,
-                               env=dict(os.environ, SHIM_TIME="1", **mode))
+    # SHIM_AB_DIRS="dir1 dir2": each mode with the libgocask_hip.so of each directory, interleaved
+    libdirs = os.environ.get("SHIM_AB_DIRS", "").split() or [None]
+    runs = [(m, r, ld) for m in modes for r in range(reps) for ld in libdirs]
+    for mode, r, ld in runs:
+        if True:
+            env = dict(os.environ, SHIM_TIME="1", **mode)
+            if ld:
+                env["LD_LIBRARY_PATH"] = os.path.abspath(ld) + ":" + env.get("LD_LIBRARY_PATH", "")
+            p = subprocess.run([shim, d], capture_output=True, text=True, timeout=300, env=env)
             if p.returncode:
                 raise SystemExit(p.stderr)
             row = json.loads(p.stdout.strip().splitlines()[-1])
             row["rep"] = r
+            row["libdir"] = ld
             row["copy_threads"] = mode.get("GCK_COPY_THREADS", os.environ.get("GCK_COPY_THREADS", "default"))
             tr = [l for l in p.stderr.splitlines() if l.startswith(("gck_replay", "[gck_replay"))]
             if tr:  # GCK_REPLAY_TRACE=1: the library's phase marks
