@@ -468,7 +468,7 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         const uint64_t todo = __ballot(have && !small);
         if (todo) {
             const uint32_t c = wave_crcs<false>(
-                todo, [&](int it) { return (__shfl((int)del, it) ? keys : vals) + __shfl(po, it); }, L, *T, lb0,
+                todo, [&](int it) { return (lane_u32(del, it) ? keys : vals) + lane_u64(po, it); }, L, *T, lb0,
                 lb1, [&](uint32_t A) { return lanes_combine_gmul(kl_shift, A); });
             if ((todo >> lane) & 1) crc = c;
         }

@@ -95,6 +95,18 @@ __device__ __forceinline__ uint32_t lanes_combine_gmul(uint32_t kl, uint32_t A) 
     return ~((uint32_t)__builtin_amdgcn_readlane((int)f, 31) ^ (uint32_t)__builtin_amdgcn_readlane((int)f, 63));
 }
 
+// Lane it's x, it wave-uniform: v_readlane into a scalar register, so the
+// values derived from it (a value's stripe count, padding, shift and base) and
+// the branches on them stay scalar.  __shfl would be a ds_bpermute whose
+// result the compiler treats as divergent: the per-value bookkeeping then ran
+// in VALU 64-bit arithmetic and every branch on it under an exec mask.
+__device__ __forceinline__ uint32_t lane_u32(uint32_t x, int it) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, it);
+}
+__device__ __forceinline__ uint64_t lane_u64(uint64_t x, int it) {
+    return ((uint64_t)lane_u32((uint32_t)(x >> 32), it) << 32) | lane_u32((uint32_t)x, it);
+}
+
 // The 16 bytes of virtual position v (value p[0, L) zero-padded in front by
 // pad bytes), plus the next dword for the byte shift: one 16 B and one 4 B
 // load (dword aligned), unconditional.  A lane wholly in the padding loads
@@ -194,7 +206,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
                               uint32_t lb1, Combine combine) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t out = 0;
-    auto job = [&](int it) { return CrcJob(ptr_of(it), __shfl(len, it)); };
+    auto job = [&](int it) { return CrcJob(ptr_of(it), lane_u32(len, it)); };
     // load cursor
     uint64_t lrem = todo;
     int lt = __builtin_ctzll(todo);
