@@ -8,7 +8,7 @@
 namespace gck {
 
 // LDS tables: the conflict-free slicing-by-4 image (gck_crc_lds.h, 128 KiB,
-// from the context's global tables); multiplication by the constant Z_1008
+// from the context's global tables); multiplication by the constant Z_1024
 // as four byte tables, Z(A) = XOR_k Zs[k][byte k of A] (Z is linear in A);
 // the lane shifts Z_{16 (31 - (l & 31))} as eight nibble tables per lane
 // (entry (q, v) of lane l at word 512 q + 32 v + (l & 31): each lane of a
@@ -26,7 +26,7 @@ struct CrcTabs {
     uint32_t Z512[4][256];
 };
 __device__ inline void fill_zs(CrcTabs &t) {
-    const uint32_t z = xpow8n(1008);
+    const uint32_t z = xpow8n(1024);
     for (uint32_t e = threadIdx.x; e < 1024; e += blockDim.x) t.Zs[e >> 8][e & 0xFF] = multmodp(z, (e & 0xFF) << (8 * (e >> 8)));
 }
 
@@ -160,8 +160,9 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32
 // crc32.ChecksumIEEE of a value by one wavefront.  The value is read as a
 // virtual buffer of J stripes of 1 KiB, zero-padded at the FRONT (F(0, .)
 // ignores leading zeros), lane l taking the 16 bytes at 16 l of every stripe
-// (coalesced loads).  Lane state: A <- F(Z_1008(A), chunk), i.e. Horner over
-// the lane's chunks 1 KiB apart.  The 0xFFFFFFFF init is the complement of the
+// (coalesced loads).  Lane state: A <- Z_1024(A) ^ F(0, chunk), i.e. Horner
+// over the lane's chunks 1 KiB apart (= F(Z_1008(A), chunk); the chunk's CRC
+// does not wait for A, whose only dependent step is the one Z_1024 multiply).  The 0xFFFFFFFF init is the complement of the
 // value's first 4 bytes (F(~0, V) = F(0, V with bytes 0..3 ^ 0xFF)).  Lane l's
 // part is finally shifted past the 16 (63-l) bytes after it and the lanes
 // XOR-reduced (lanes_combine): F(~0, V); crc = ~that.
@@ -176,7 +177,8 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
     for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], jb.sh);
     // (uniform) the stripes that hold the value's first 4 bytes; then per lane:
     // bytes before the value are zero, its first 4 complemented
-    if ((j << 10) < jb.pad + 4 && v < jb.pad + 4) {
+    if ((j << 10) < jb.pad + 4) {  // (a scalar branch, then the lanes)
+      if (v < jb.pad + 4) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
@@ -185,12 +187,12 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, co
             const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
             w[i] = (w[i] & keep) ^ (flip & keep);
         }
+      }
     }
-    uint32_t c = zmul(t.Zs, A) ^ w[0];
-    c = slice4x(t.S, lb0, lb1, c, w[1]);
+    uint32_t c = slice4x(t.S, lb0, lb1, w[0], w[1]);
     c = slice4x(t.S, lb0, lb1, c, w[2]);
     c = slice4x(t.S, lb0, lb1, c, w[3]);
-    return slice4x(t.S, lb0, lb1, c, 0u);
+    return slice4x(t.S, lb0, lb1, c, zmul(t.Zs, A));
 }
 
 // The large values of a wavefront's 64 items (mask todo; ptr_of(i) = item i's
