@@ -131,9 +131,9 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
         if (dst) {  // the values that passed, copied by the whole wave
             for (uint64_t cp = __ballot(ok && crc == want); cp; cp &= cp - 1) {
                 const int t = __builtin_ctzll(cp);
-                uint8_t *d = dst + __shfl(doff, t);
-                const uint8_t *src = arena + __shfl(off, t);
-                const uint32_t L = __shfl(len, t);
+                uint8_t *d = dst + lane_u64(doff, t);  // (t wave-uniform: scalars)
+                const uint8_t *src = arena + lane_u64(off, t);
+                const uint32_t L = lane_u32(len, t);
                 for (uint64_t j = lane; j < L; j += 64) d[j] = src[j];
             }
         }
