@@ -268,7 +268,11 @@ constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
 
 // crc32.ChecksumIEEE of a small value by one lane (lanes run different
 // values): aligned dwords, 64 bytes of loads in flight per round, slicing-by-4
-// per word, the last 0..3 bytes one at a time.
+// per word, the last 0..3 bytes one at a time.  Wide: the round's dwords as
+// four 16 B loads (each lane's address is its own line, so one instruction
+// per 16 B instead of per 4 B); reads up to 12 bytes past the value's last
+// dword, so only for buffers padded past their end (the replay arena).
+template <bool Wide = false>
 __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
@@ -276,8 +280,21 @@ __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, cons
     uint32_t c = 0xFFFFFFFFu, pos = 0;
     for (uint32_t b = 0; __ballot(b < nw); b += 16) {
         uint32_t d[17];
+        if constexpr (Wide) {
 #pragma unroll
-        for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
+            for (int k = 0; k < 4; ++k) {
+                u32x4_a4 x = {0u, 0u, 0u, 0u};
+                if (b + 4 * k < nw) x = *reinterpret_cast<const u32x4_a4 *>(a + b + 4 * k);
+                d[4 * k] = x.x;
+                d[4 * k + 1] = x.y;
+                d[4 * k + 2] = x.z;
+                d[4 * k + 3] = x.w;
+            }
+            d[16] = b + 16 < nw ? a[b + 16] : 0u;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
+        }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
