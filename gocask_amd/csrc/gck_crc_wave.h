@@ -121,24 +121,29 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // wave-uniform, so the byte shift sh and the dword-aligned base b of the
 // virtual buffer (b + v = the dword holding virtual byte v, sh its offset)
 // are scalars.
+// Stripe indices and in-value positions are 32-bit (L < 2^32, so J <= 2^22
+// and j << 10 < 2^32): gfx9's scalar unit has no 64-bit less-than, and the
+// 64-bit head-stripe test (j << 10) < pad + 4 was a VALU compare on every
+// stripe.  head4 / head16: the stripes that hold bytes of [0, pad + 4) /
+// [0, pad + 16) (1 or 2).
 struct CrcJob {
     const uint8_t *p, *b;
-    uint64_t L, J, pad;
-    uint32_t sh;
-    __device__ CrcJob(const uint8_t *p_, uint64_t L_)
-        : p(p_), L(L_), J((L_ + 1023) >> 10), pad((J << 10) - L_),
-          sh((uint32_t)((reinterpret_cast<uintptr_t>(p_) - pad) & 3)) {
+    uint32_t J, pad, sh, head4, head16;
+    __device__ CrcJob(const uint8_t *p_, uint32_t L)
+        : p(p_), J((uint32_t)(((uint64_t)L + 1023) >> 10)), pad((J << 10) - L),
+          sh((uint32_t)((reinterpret_cast<uintptr_t>(p_) - pad) & 3)),
+          head4((pad + 4 + 1023) >> 10), head16((pad + 16 + 1023) >> 10) {
         b = p - pad - sh;
     }
 };
 // NT: non-temporal stripe loads (bytes read once); without, the lines stay in
 // L2 for a second read of the same bytes (the fused encoder's copy).
 template <bool NT = true>
-__device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32_t d[5]) {
+__device__ __forceinline__ void stripe_load(const CrcJob &jb, uint32_t j, uint32_t d[5]) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t v = (j << 10) + 16ull * lane;
+    const uint32_t v = (j << 10) + 16u * lane;
     const uint8_t *a = jb.b + v;
-    if ((j << 10) < jb.pad + 16) {  // (uniform) the value's first stripe(s): lanes wholly in the padding
+    if (j < jb.head16) {  // (uniform) the value's first stripe(s): lanes wholly in the padding
         const uint8_t *p0 = jb.p - (reinterpret_cast<uintptr_t>(jb.p) & 3);
         a = v + 16 <= jb.pad ? p0 : a;
     }
@@ -168,22 +173,22 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint64_t j, uint32
 // XOR-reduced (lanes_combine): F(~0, V); crc = ~that.
 //
 // One stripe of the value at virtual stripe j into A:
-__device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint64_t j, const uint32_t d[5], uint32_t A,
+__device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint32_t j, const uint32_t d[5], uint32_t A,
                                                 const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t v = (j << 10) + 16ull * lane;  // virtual position of this lane's chunk
+    const uint32_t v = (j << 10) + 16u * lane;  // virtual position of this lane's chunk
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], jb.sh);
     // (uniform) the stripes that hold the value's first 4 bytes; then per lane:
     // bytes before the value are zero, its first 4 complemented
-    if ((j << 10) < jb.pad + 4) {  // (a scalar branch, then the lanes)
+    if (j < jb.head4) {  // (a scalar branch, then the lanes)
       if (v < jb.pad + 4) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int64_t lead = (int64_t)jb.pad - (int64_t)(v + 4 * i);  // bytes of dword i before the value
+            const int32_t lead = (int32_t)jb.pad - (int32_t)(v + 4 * i);  // bytes of dword i before the value (v < 2 KiB here)
             const uint32_t keep = lead >= 4 ? 0u : lead <= 0 ? 0xFFFFFFFFu : 0xFFFFFFFFu << (8 * lead);
-            const int64_t cl = lead + 4;  // bytes of dword i before the value's byte 4
+            const int32_t cl = lead + 4;  // bytes of dword i before the value's byte 4
             const uint32_t flip = cl <= 0 ? 0u : cl >= 4 ? 0xFFFFFFFFu : 0xFFFFFFFFu >> (8 * (4 - cl));
             w[i] = (w[i] & keep) ^ (flip & keep);
         }
@@ -213,7 +218,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
     uint64_t lrem = todo;
     int lt = __builtin_ctzll(todo);
     CrcJob lj = job(lt);
-    uint64_t ls = 0;
+    uint32_t ls = 0;
     auto load_next = [&](uint32_t d[5]) {
         stripe_load<NT>(lj, ls, d);
         if (lrem && ++ls == lj.J) {  // the next value (or stay on the last stripe: dummy reloads)
@@ -234,7 +239,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
     uint64_t crem = todo;
     int ct = __builtin_ctzll(todo);
     CrcJob cj = job(ct);
-    uint64_t cs = 0;
+    uint32_t cs = 0;
     uint32_t A = 0;
     while (crem) {
 #pragma unroll
