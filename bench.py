@@ -7,7 +7,10 @@ chain walk, validation, record table, CRC of every value, verdict + tuples
 into HBM by the device encoder before timing starts.
 
   python bench.py [--gpus N --steps K --warmup W --config c3]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+  N>1: python bench.py --gpus N starts the N rank processes itself (a
+       torch.distributed.run child, launched before this process touches a
+       GPU; rank 0's JSON line passes through), or under a launcher:
+       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 N = 1 times C3 (BASELINE's metric config).  N > 1 times C4: one corpus of
 16 x N files of 2 GiB (per-file seed 4 + n), cut into N contiguous walk-order
@@ -244,26 +247,49 @@ def shard_config(cfg_name, rank):
     return cfg
 
 
-def c4_spec(world, rank, files_per_rank=C4_FILES_PER_GPU):
+def c4_spec(world, rank, files_per_rank=C4_FILES_PER_GPU, file_bytes=2 << 30):
     """(file ids, last_is_active, kw) of rank's C4 shard: the corpus has
-    files_per_rank x world files, its key universe C4_KEYS_PER_FILE per file."""
+    files_per_rank x world files, its key universe C4_KEYS_PER_FILE per 2 GiB
+    file (scaled with file_bytes: --c4-file-mib shrinks the files of a
+    rehearsal, not the spec)."""
     from gocask_amd import shard
 
     ids, last_active = shard.c4_file_ids(world, rank, files_per_rank)
-    kw = dict(CONFIGS["c4"], key_universe=C4_KEYS_PER_FILE * files_per_rank * world)
+    per_file = max(1, C4_KEYS_PER_FILE * file_bytes // (2 << 30))
+    kw = dict(CONFIGS["c4"], key_universe=per_file * files_per_rank * world, max_file_size=file_bytes)
     return ids, last_active, kw
 
 
-def encode_workload(ctx, cfg_name, world, rank):
+def encode_workload(ctx, cfg_name, world, rank, files_per_rank=C4_FILES_PER_GPU, file_bytes=2 << 30):
     """Encode this rank's files into its context.  C4: the rank's contiguous
     walk-order range of the one global corpus (no data-path collective: the
     files are independent)."""
     if cfg_name == "c4":
-        from gocask_amd import shard
-
-        ids, last_active, kw = c4_spec(world, rank)
+        ids, last_active, kw = c4_spec(world, rank, files_per_rank, file_bytes)
         return ctx.encode_files(ids, last_is_active=last_active, **kw)
     return ctx.encode(**shard_config(cfg_name, rank))
+
+
+def launcher_cmd(n, port, argv, script=None):
+    """The torch.distributed.run command that starts n rank processes of this
+    script with the same arguments (one node, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+
+
+def relaunch(n, argv):
+    """--gpus N > 1 with no launcher around this process: run the N ranks as a
+    child torch.distributed.run (nothing here has touched a GPU yet: only the
+    argument parser ran), pass its output through (rank 0 prints the JSON
+    line) and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, GCK_BENCH_LAUNCHED="1")
+    return subprocess.run(launcher_cmd(n, port, argv), env=env).returncode
 
 
 def reduce_over_ranks(dist, elapsed, nbytes, device):
@@ -299,9 +325,17 @@ def main():
                     help="N=1: time the keydir merge too (a one-rank RCCL group)")
     ap.add_argument("--host-inclusive", type=int, default=0, metavar="K",
                     help="also time K host-in/host-out replays (pinned H2D + run + D2H of the tuples)")
+    ap.add_argument("--c4-files-per-gpu", type=int, default=C4_FILES_PER_GPU,
+                    help="C4: files per rank (16: BASELINE's C4; fewer only for rehearsals)")
+    ap.add_argument("--c4-file-mib", type=int, default=2048,
+                    help="C4: file size in MiB (2048: BASELINE's C4; smaller only for rehearsals)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} rank processes")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -326,7 +360,7 @@ def main():
     t_setup = time.perf_counter()
     ctx = g.ReplayContext(device=device, chunk_bytes=args.chunk_kib << 10, spec_window=args.spec_kib << 10,
                           chunk_cap=args.chunk_cap)
-    info = encode_workload(ctx, args.config, world, rank)
+    info = encode_workload(ctx, args.config, world, rank, args.c4_files_per_gpu, args.c4_file_mib << 20)
     setup_s = time.perf_counter() - t_setup
 
     def barrier():
@@ -349,7 +383,18 @@ def main():
     # timed steps themselves
     assert st["n_runs"] - s0["n_runs"] == args.steps
     crc_avg = (st["ms_crc_rows_sum"] - s0["ms_crc_rows_sum"]) / args.steps
+    rank_elapsed = elapsed
     elapsed, total_bytes = reduce_over_ranks(dist, elapsed, my_bytes, "cpu" if backend == "gloo" else "cuda")
+    # every rank's own figures (N > 1: the roofline of each rank's k_crc_rows)
+    per_rank = [dict(rank=0, crc_rows_ms=crc_avg, step_ms=rank_elapsed / args.steps * 1e3, bytes=my_bytes)]
+    if dist is not None:
+        dev = "cpu" if backend == "gloo" else "cuda"
+        mine = torch.tensor([crc_avg, rank_elapsed / args.steps * 1e3, float(my_bytes)], dtype=torch.float64,
+                            device=dev)
+        allr = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [dict(rank=r, crc_rows_ms=float(t[0].item()), step_ms=float(t[1].item()), bytes=int(t[2].item()))
+                    for r, t in enumerate(allr)]
     # per-phase device times of a few more, untimed steps with an event between
     # every phase (the timed steps record only the events around k_crc_rows)
     phases_sum, n_phase = {}, 3
@@ -384,7 +429,8 @@ def main():
         achieved = my_bytes / (crc_avg * 1e-3) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-        if os.path.exists(tf):
+        rehearsal = args.config == "c4" and (args.c4_file_mib != 2048 or args.c4_files_per_gpu != C4_FILES_PER_GPU)
+        if os.path.exists(tf) and not rehearsal:
             traffic = json.load(open(tf)).get("crc_rows_hbm_bytes_per_launch")
         out = {
             "metric": "device-resident data-file GiB/s CRC-verified+header-decoded, 1 GPU (+2/4/8)",
@@ -400,7 +446,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic (device-encoded GoCask records, DESIGN.md Corpus)",
             "config": {
-                "workload": DESCR[args.config].format(n=C4_FILES_PER_GPU * world, g=world)
+                "workload": DESCR[args.config].format(n=args.c4_files_per_gpu * world, g=world)
+                + (f" ({args.c4_file_mib} MiB files: a rehearsal, not BASELINE's C4)"
+                   if args.config == "c4" and (args.c4_file_mib != 2048 or args.c4_files_per_gpu != C4_FILES_PER_GPU)
+                   else "")
                 + (" per GPU" if world > 1 and args.config != "c4" else ""),
                 "bytes_per_gpu": my_bytes,
                 "records_per_gpu": st["n_recs"],
@@ -427,6 +476,16 @@ def main():
             },
             "phase_ms": {k: round(v / n_phase, 4) for k, v in phases_sum.items()},
         }
+        if world > 1:
+            # each rank's k_crc_rows over its own shard (rank 0's is the line's achieved / frac)
+            out["roofline"]["per_rank"] = [
+                dict(rank=p["rank"], crc_rows_ms=round(p["crc_rows_ms"], 4), step_ms=round(p["step_ms"], 3),
+                     bytes=p["bytes"], achieved=round(p["bytes"] / (p["crc_rows_ms"] * 1e-3) / 1e9, 1),
+                     frac=round(p["bytes"] / (p["crc_rows_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4))
+                for p in per_rank]
+            fr = [p["frac"] for p in out["roofline"]["per_rank"]]
+            out["roofline"]["frac_min_over_ranks"] = min(fr)
+            out["roofline"]["frac_max_over_ranks"] = max(fr)
         if args.keydir:
             ctx.keydir()  # warm-up (allocations)
             live, kd_ms = ctx.keydir()

@@ -271,6 +271,13 @@ def load_diag():
     D.gck_diag_stream_pattern.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
     D.gck_diag_chunks.restype = ctypes.c_int
     D.gck_diag_chunks.argtypes = [vp, vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]
+    D.gck_diag_multi_resolve.restype = ctypes.c_int
+    D.gck_diag_multi_resolve.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, P(GckResult), vp]
+    D.gck_diag_multi_recv_offsets.restype = ctypes.c_int
+    D.gck_diag_multi_recv_offsets.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp]
+    D.gck_diag_replay_multi_loopback.restype = ctypes.c_int
+    D.gck_diag_replay_multi_loopback.argtypes = [P(GckFile), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32,
+                                                 P(GckOpts), P(GckResult)]
     _diag = D
     return D
 

@@ -249,8 +249,8 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
     res = GckResult()
     rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window,
                                                         max_resident, keys)), ctypes.byref(res))
-    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
-    try:
+    try:  # (an error return may still hand back memory: freed either way)
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
         return _result(res)
     finally:
         L.gck_result_free(ctypes.byref(res))
@@ -271,8 +271,8 @@ def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=
     res = GckResult()
     rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident, keys)),
                             ctypes.byref(res))
-    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
-    try:
+    try:  # (an error return may still hand back memory: freed either way)
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
         return _result(res)
     finally:
         L.gck_result_free(ctypes.byref(res))
@@ -314,8 +314,8 @@ def replay_multi(files, reset_after=None, devices=(0,), chunk_bytes=0, keys=Fals
     res = GckResult()
     rc = L.gck_replay_multi(fa, len(arrs), devs.ctypes.data, len(devs),
                             ctypes.byref(_opts(int(devs[0]), chunk_bytes, keys=keys)), ctypes.byref(res))
-    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
-    try:
+    try:  # (an error return may still hand back memory: freed either way)
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
         return _result(res)
     finally:
         L.gck_result_free(ctypes.byref(res))
@@ -335,8 +335,62 @@ def replay_multi_paths(paths, reset_after=None, devices=(0,), chunk_bytes=0, key
     res = GckResult()
     rc = L.gck_replay_multi_paths(pa, len(enc), devs.ctypes.data, len(devs),
                                   ctypes.byref(_opts(int(devs[0]), chunk_bytes, keys=keys)), ctypes.byref(res))
-    check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
-    try:
+    try:  # (an error return may still hand back memory: freed either way)
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
+OUTCOME_DTYPE = np.dtype([("status", "<i4"), ("nfiles", "<u4"), ("err_file", "<u4"), ("files_walked", "<u4"),
+                          ("final_last_offset", "<u4"), ("_pad", "<u4"), ("err_off", "<u8"), ("n_crc_fail", "<u8")])
+
+
+def multi_resolve(outcomes, nfiles):
+    """gck_replay_multi's global outcome (libgocask_diag.so, host only):
+    outcomes = per shard dicts (status, nfiles, err_file, files_walked,
+    final_last_offset, err_off, n_crc_fail) in walk order.  Returns (status
+    dict, contributes per shard)."""
+    D = _lib.load_diag()
+    a = np.zeros(max(1, len(outcomes)), dtype=OUTCOME_DTYPE)
+    for i, o in enumerate(outcomes):
+        for k, v in o.items():
+            a[i][k] = v
+    contrib = np.zeros(max(1, len(outcomes)), dtype=np.uint8)
+    res = GckResult()
+    check(D.gck_diag_multi_resolve(a.ctypes.data, len(outcomes), nfiles, ctypes.byref(res), contrib.ctypes.data))
+    st = dict(status=res.status, err_file=res.err_file, err_off=res.err_off, n_crc_fail=res.n_crc_fail,
+              final_last_offset=res.final_last_offset, files_walked=res.files_walked)
+    return st, [bool(x) for x in contrib[:len(outcomes)]]
+
+
+def multi_recv_offsets(counts):
+    """The exchange's receive layout (libgocask_diag.so, host only): counts
+    [nsrc][nown] -> offsets [nown][nsrc + 1]."""
+    D = _lib.load_diag()
+    c = np.ascontiguousarray(counts, dtype=np.uint64)
+    nsrc, nown = c.shape
+    off = np.zeros((nown, nsrc + 1), dtype=np.uint64)
+    check(D.gck_diag_multi_recv_offsets(c.ctypes.data if c.size else None, nsrc, nown, off.ctypes.data))
+    return off
+
+
+def replay_multi_loopback(files, reset_after=None, nshards=2, device=0, chunk_bytes=0, max_resident=0, keys=False):
+    """gck_replay_multi's orchestration with nshards logical shards on one
+    device, the partitions moved by device copies (libgocask_diag.so test
+    entry): the same plan, ring replays, keydir packs, status resolution,
+    receive layout and per-owner merges as the N-GPU call."""
+    D = _lib.load_diag()
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(files)
+    fa, arrs = _files_struct(files, reset_after)
+    res = GckResult()
+    rc = D.gck_diag_replay_multi_loopback(fa, len(arrs), nshards, device,
+                                          ctypes.byref(_opts(device, chunk_bytes, max_resident=max_resident, keys=keys)),
+                                          ctypes.byref(res))
+    try:  # (an error return may still hand back memory: freed either way)
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
         return _result(res)
     finally:
         L.gck_result_free(ctypes.byref(res))

@@ -7,6 +7,8 @@
 // the practical HBM read ceiling that k_crc_rows is compared against in
 // bench.py / DESIGN.md (SURVEY.md §8d asks for the fraction of a measured
 // streaming-read kernel besides the spec peak).
+#include <cstring>
+
 #include "gck_internal.h"
 #include "gck_diag.h"
 
@@ -232,4 +234,29 @@ extern "C" int gck_diag_chunks(gck_ctx *ctx, uint32_t *count, uint64_t *entry, u
         GCK_HIP(hipMemcpy(entry, c->d_ch_entry.p, (uint64_t)c->n_chunks * 8, hipMemcpyDeviceToHost));
     }
     return GCK_OK;
+}
+
+static_assert(sizeof(gck_diag_outcome) == sizeof(gck::MultiOutcome), "gck_diag_outcome mirrors gck::MultiOutcome");
+
+extern "C" int gck_diag_multi_resolve(const gck_diag_outcome *sh, uint32_t n, uint32_t nfiles, gck_result *out,
+                                      uint8_t *contrib) {
+    if ((n && (!sh || !contrib)) || !out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    gck::multi_resolve(reinterpret_cast<const gck::MultiOutcome *>(sh), n, nfiles, out, contrib);
+    return GCK_OK;
+}
+
+extern "C" int gck_diag_multi_recv_offsets(const uint64_t *counts, uint32_t nsrc, uint32_t nown, uint64_t *off) {
+    if (!off || nown == 0 || (nsrc && !counts)) return GCK_EINVAL;
+    gck::multi_recv_offsets(counts, nsrc, nown, off);
+    return GCK_OK;
+}
+
+extern "C" int gck_diag_replay_multi_loopback(const gck_file *files, uint32_t nfiles, uint32_t nshards,
+                                              int32_t device, const gck_opts *opts, gck_result *out) {
+    if (!out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    if ((nfiles && !files) || nshards == 0 || nshards > 64) return GCK_EINVAL;
+    const std::vector<gck::Src> v = gck::mem_srcs(files, nfiles);
+    return gck::replay_multi(v.data(), nfiles, std::vector<int>(nshards, device), opts, out, true);
 }

@@ -23,6 +23,26 @@ int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per
 /* Per-chunk chain length (records k_walk staged) and final entry of the last
  * run; count / entry NULL: *n = chunks only. */
 int gck_diag_chunks(gck_ctx *ctx, uint32_t *count, uint64_t *entry, uint64_t cap, uint64_t *n);
+/* ---- gck_replay_multi's orchestration, testable on one GPU / the CPU ----
+ * One shard's outcome as gck_replay reports it (gck::MultiOutcome). */
+typedef struct gck_diag_outcome {
+    int32_t status;
+    uint32_t nfiles, err_file, files_walked, final_last_offset;
+    uint64_t err_off, n_crc_fail;
+} gck_diag_outcome;
+/* The global outcome over n shards in walk order (host only): out's status,
+ * err_file / err_off (rebased), files_walked, final_last_offset, n_crc_fail;
+ * contrib[s] = 1 for the shards whose records count. */
+int gck_diag_multi_resolve(const gck_diag_outcome *sh, uint32_t n, uint32_t nfiles, gck_result *out,
+                           uint8_t *contrib);
+/* Receive offsets of the exchange (host only): off[p * (nsrc + 1) + i] = items
+ * owner p receives from sources before i; counts[i * nown + p]. */
+int gck_diag_multi_recv_offsets(const uint64_t *counts, uint32_t nsrc, uint32_t nown, uint64_t *off);
+/* gck_replay_multi with nshards logical shards on one device: the same plan,
+ * ring replays, keydir packs, status resolution, receive layout and merges,
+ * the partitions moved by device copies instead of RCCL (test entry). */
+int gck_diag_replay_multi_loopback(const gck_file *files, uint32_t nfiles, uint32_t nshards, int32_t device,
+                                   const gck_opts *opts, gck_result *out);
 #ifdef __cplusplus
 }
 #endif

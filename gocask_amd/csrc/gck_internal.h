@@ -167,7 +167,7 @@ class Copier {
     Copier();
     ~Copier();
     int start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev);
-    void add(uint32_t group, const uint8_t *src, int fd, uint64_t off, uint64_t len, uint8_t *dst);
+    void add(uint32_t group, const uint8_t *src, const char *path, uint64_t off, uint64_t len, uint8_t *dst);
     int direct(const uint8_t *src, uint64_t len, uint8_t *dst);
     void seal(uint32_t group);
     int wait_recorded(uint32_t group);
@@ -188,14 +188,42 @@ void res_free(void *p);
 // dst = the segments back to back (host threads for large totals)
 void par_gather(uint8_t *dst, const std::vector<std::pair<const void *, uint64_t>> &segs);
 // A data file to replay: caller memory (data), or an open file (fd, data null)
+// A data file: caller memory (data), or a path the copier opens per chunk it
+// reads (no descriptor is held across the call: a database with more files
+// than RLIMIT_NOFILE still opens, as the reference's Walk does, one at a time)
 struct Src {
     const uint8_t *data;
-    int fd;
+    const char *path;
     uint64_t len;
     bool reset_after;
 };
 std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles);
-// opens and stats every path (GCK_EIO when one fails; then none stays open)
+// gck_replay's ring of file groups with a hook instead of tuple delivery:
+// group(g, first file of the group, its context) runs after each group has
+// replayed (on the context's stream, which the hook may use and synchronise);
+// out receives the outcome (status, err_file / err_off / files_walked relative
+// to files, final_last_offset, n_crc_fail, n_groups / n_resident), no records.
+struct GroupSink {
+    virtual ~GroupSink() = default;
+    virtual int group(uint32_t g, uint32_t file0, gck_ctx *ctx) = 0;
+};
+int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, GroupSink *sink, gck_result *out);
+// gck_replay_multi (multi.hip): one shard's outcome, the global outcome over
+// shards in walk order, the exchange's receive offsets, and the call itself
+// (loopback: several shards may share a device; every pair is a device copy)
+struct MultiOutcome {
+    int32_t status;
+    uint32_t nfiles, err_file, files_walked, final_last_offset;
+    uint64_t err_off, n_crc_fail;
+};
+void multi_resolve(const MultiOutcome *sh, uint32_t n, uint32_t nfiles, gck_result *out, uint8_t *contrib);
+void multi_recv_offsets(const uint64_t *counts, uint32_t nsrc, uint32_t nown, uint64_t *off);
+int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs, const gck_opts *opts,
+                 gck_result *out, bool loopback);
+// the pool of idle contexts behind gck_replay (per device, one options key each)
+int pool_take(const gck_opts *o, gck_ctx **out);
+void pool_give(const gck_opts *o, gck_ctx *c);
+// stats every path (GCK_EIO when one fails); the paths must outlive the call
 int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &out);
 void close_srcs(std::vector<Src> &v);
 // n files into device memory through a Copier on stream, then waits for them

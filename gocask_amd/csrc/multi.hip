@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -72,11 +73,19 @@ const Rccl &rccl() {
 }
 
 // Communicators over a device list, kept for the next call with the same list
-// (ncclCommInitAll costs far more than a replay of a small database).
+// (ncclCommInitAll costs far more than a replay of a small database).  A set is
+// used by one call at a time: its mutex is held from ncclGroupStart until the
+// exchange's streams are synchronised (NCCL forbids concurrent use of a
+// communicator from several threads; two Opens would otherwise interleave).
+struct CommSet {
+    std::vector<int> devs;
+    std::vector<ncclComm_t> comms;
+    std::shared_ptr<std::mutex> mu;
+};
 std::mutex g_comm_mu;
-std::vector<std::pair<std::vector<int>, std::vector<ncclComm_t>>> g_comms;
+std::vector<CommSet> g_comms;
 
-int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
+int comms_for(const std::vector<int> &devs, CommSet &out) {
     const Rccl &R = rccl();
     if (!R.ok) {
         gck::set_error("dlopen librccl.so.1", hipErrorSharedObjectInitFailed, __FILE__, __LINE__);
@@ -84,29 +93,59 @@ int comms_for(const std::vector<int> &devs, std::vector<ncclComm_t> &out) {
     }
     std::lock_guard<std::mutex> lk(g_comm_mu);
     for (auto &e : g_comms)
-        if (e.first == devs) {
-            out = e.second;
+        if (e.devs == devs) {
+            out = e;
             return GCK_OK;
         }
-    std::vector<ncclComm_t> c(devs.size(), nullptr);
-    const ncclResult_t r = R.init_all(c.data(), (int)devs.size(), devs.data());
+    CommSet c{devs, std::vector<ncclComm_t>(devs.size(), nullptr), std::make_shared<std::mutex>()};
+    const ncclResult_t r = R.init_all(c.comms.data(), (int)devs.size(), devs.data());
     if (r != ncclSuccess) {
         gck::set_error(R.err(r), hipErrorUnknown, __FILE__, __LINE__);
         return GCK_EDEVICE;
     }
-    g_comms.emplace_back(devs, c);
+    g_comms.push_back(c);
     out = c;
     return GCK_OK;
 }
 
-struct Shard {
-    uint32_t a = 0, b = 0;  // files [a, b)
-    gck_ctx *ctx = nullptr;
+// One replayed file group's keydir (tombstones kept), packed over the owners:
+// entries and key bytes partition-major, in its own device buffers (the
+// group's ring context is reused for a later group as soon as this is done).
+struct Part {
+    uint32_t file0 = 0;  // global walk index of the group's first file
+    uint64_t counts[64] = {}, kbytes[64] = {};
+    void *d_ents = nullptr, *d_keys = nullptr;
+};
+
+// A shard's replay through gck_replay's ring (replay_groups_to): after each
+// group has replayed, its keydir is built and packed on the device.
+struct ShardRun : gck::GroupSink {
+    uint32_t shard = 0, a = 0, b = 0, nown = 1;
+    int dev = 0;
     int rc = GCK_OK;
-    gck_stats st{};
-    uint64_t counts[64] = {}, kbytes[64] = {};  // per owner
-    void *d_ents = nullptr, *d_keys = nullptr;  // packed partitions (device of the shard)
-    void *r_ents = nullptr, *r_keys = nullptr;  // what this device owns, sources in shard order
+    gck_result res{};
+    std::vector<Part> parts;
+    int group(uint32_t, uint32_t file0, gck_ctx *ctx) override {
+        uint64_t n = 0;
+        int r;
+        if ((r = gck_ctx_keydir(ctx, GCK_KD_KEEP_TOMBSTONES, &n, nullptr))) return r;
+        parts.emplace_back();
+        Part &p = parts.back();
+        p.file0 = a + file0;
+        if ((r = gck_kd_pack_sizes(ctx, nown, p.counts, p.kbytes))) return r;
+        uint64_t ne = 0, nk = 0;
+        for (uint32_t o = 0; o < nown; ++o) {
+            ne += p.counts[o];
+            nk += p.kbytes[o];
+        }
+        if (hipSetDevice(dev) != hipSuccess || hipMalloc(&p.d_ents, ne * sizeof(gck_kd_entry) + 64) != hipSuccess ||
+            hipMalloc(&p.d_keys, nk + 64) != hipSuccess) {
+            (void)hipGetLastError();
+            return GCK_ENOMEM;
+        }
+        return gck_kd_pack(ctx, shard, p.file0, static_cast<gck_kd_entry *>(p.d_ents), ne,
+                           static_cast<uint8_t *>(p.d_keys), nk);
+    }
 };
 
 }  // namespace
@@ -153,14 +192,64 @@ extern "C" int gck_plan_shards(const uint64_t *sizes, const uint8_t *reset_after
     return GCK_OK;
 }
 
-static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
-                        const gck_opts *opts, gck_result *out) {
-    if ((nfiles && !files) || !devices || ndev == 0 || ndev > 64) return GCK_EINVAL;
+namespace gck {
+
+// The global outcome of a sharded replay (gocask_amd/shard.py resolve_status;
+// core/db.go:110-138, internal/fs/disk.go:134-141): shards in walk order until
+// the first startup error, which is the global status (its file and offset
+// rebased to the whole walk); later shards contribute nothing.  CRC rejects
+// sum over the contributing shards; final_last_offset is the last
+// contributing shard's (cuts follow files that reset it).
+void multi_resolve(const MultiOutcome *sh, uint32_t n, uint32_t nfiles, gck_result *out, uint8_t *contrib) {
+    out->status = GCK_OK;
+    out->err_file = 0;
+    out->err_off = 0;
+    out->n_crc_fail = 0;
+    out->final_last_offset = 0;
+    uint32_t base = 0;
+    bool failed = false;
+    for (uint32_t s = 0; s < n; ++s) {
+        contrib[s] = !failed;
+        if (failed) continue;
+        const MultiOutcome &st = sh[s];
+        if (st.nfiles) out->n_crc_fail += st.n_crc_fail;
+        if (st.nfiles && st.status == GCK_EUNEXPECTED_EOF) {
+            failed = true;
+            out->status = GCK_EUNEXPECTED_EOF;
+            out->err_file = base + st.err_file;
+            out->err_off = st.err_off;
+            out->files_walked = base + st.files_walked;
+            out->final_last_offset = st.final_last_offset;
+        } else if (st.nfiles) {
+            out->final_last_offset = st.final_last_offset;
+        }
+        base += st.nfiles;
+    }
+    if (!failed) out->files_walked = nfiles;
+}
+
+// Receive layout of the exchange: owner p gets partition p of every source in
+// source (= walk) order; off[p * (nsrc + 1) + i] = the items of sources before
+// i (counts[i * nown + p] items from source i).
+void multi_recv_offsets(const uint64_t *counts, uint32_t nsrc, uint32_t nown, uint64_t *off) {
+    for (uint32_t p = 0; p < nown; ++p) {
+        uint64_t *o = off + (uint64_t)p * (nsrc + 1);
+        o[0] = 0;
+        for (uint32_t i = 0; i < nsrc; ++i) o[i + 1] = o[i] + counts[(uint64_t)i * nown + p];
+    }
+}
+
+// devs[s]: the device of shard s (distinct devices; loopback: several shards
+// on one device, their partitions moved by device copies -- the N-owner
+// orchestration without RCCL, libgocask_diag.so's test entry).
+int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs, const gck_opts *opts,
+                 gck_result *out, bool loopback) {
+    const uint32_t ndev = (uint32_t)devs.size();
+    if ((nfiles && !files) || ndev == 0 || ndev > 64) return GCK_EINVAL;
     for (uint32_t f = 0; f < nfiles; ++f)
-        if (files[f].len && !files[f].data && files[f].fd < 0) return GCK_EINVAL;
+        if (files[f].len && !files[f].data && !files[f].path) return GCK_EINVAL;
     const bool want_keys = opts && (opts->flags & GCK_OPT_KEYS);
-    std::vector<int> devs(devices, devices + ndev);
-    {
+    if (!loopback) {
         std::vector<int> s = devs;
         std::sort(s.begin(), s.end());
         if (std::adjacent_find(s.begin(), s.end()) != s.end()) return GCK_EINVAL;  // one rank per device
@@ -174,7 +263,6 @@ static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *device
     std::vector<uint32_t> ranges(2 * ndev);
     int rc = gck_plan_shards(sizes.data(), reset.data(), nfiles, ndev, ranges.data());
     if (rc) return rc;
-    std::vector<Shard> sh(ndev);
     // GCK_REPLAY_TRACE=1: the phases' wall times on stderr
     const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
@@ -183,40 +271,58 @@ static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *device
             fprintf(stderr, "gck_replay_multi %-14s %9.2f ms\n", what,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     };
-    // the communicators come up on their own thread while the shards replay
-    // (ncclCommInitAll takes about a second; a later call with the same
-    // device list reuses them)
-    std::vector<ncclComm_t> comm;
+    // RCCL carries the pairs whose source and owner devices differ; a pair on
+    // one device is a device copy (GCK_MULTI_RCCL_SELF=1: RCCL's self send /
+    // receive instead, so a one-device box exercises the library's RCCL path).
+    // The communicators come up on their own thread while the shards replay.
+    const bool rccl_self = !loopback && getenv("GCK_MULTI_RCCL_SELF") != nullptr;
+    const bool need_rccl = !loopback && (ndev > 1 || rccl_self);
+    CommSet cset;
     int comm_rc = GCK_OK;
-    std::thread comm_th([&]() { comm_rc = comms_for(devs, comm); });
+    std::thread comm_th;
+    if (need_rccl) comm_th = std::thread([&]() { comm_rc = comms_for(devs, cset); });
     auto join_comm = [&]() {
         if (comm_th.joinable()) comm_th.join();
     };
+    std::vector<ShardRun> sr(ndev);
+    std::vector<gck_ctx *> mctx(ndev, nullptr);      // per owner: the merge context (pooled)
+    std::vector<void *> r_ents(ndev, nullptr), r_keys(ndev, nullptr);
+    std::vector<gck_opts> dopt(ndev);
+    for (uint32_t s = 0; s < ndev; ++s) {
+        if (opts) dopt[s] = *opts;
+        else memset(&dopt[s], 0, sizeof(gck_opts));
+        dopt[s].device = devs[s];
+        dopt[s].flags &= ~GCK_OPT_KEYS;
+    }
     auto cleanup = [&]() {
         join_comm();
         for (uint32_t s = 0; s < ndev; ++s) {
-            if (sh[s].ctx) (void)hipSetDevice(sh[s].ctx->c.device);
-            for (void *p : {sh[s].d_ents, sh[s].d_keys, sh[s].r_ents, sh[s].r_keys})
-                if (p) (void)hipFree(p);
-            if (sh[s].ctx) gck_ctx_destroy(sh[s].ctx);
+            (void)hipSetDevice(devs[s]);
+            if (mctx[s]) (void)hipStreamSynchronize(mctx[s]->c.stream);
+            for (auto &p : sr[s].parts)
+                for (void *q : {p.d_ents, p.d_keys})
+                    if (q) (void)hipFree(q);
+            for (void *q : {r_ents[s], r_keys[s]})
+                if (q) (void)hipFree(q);
+            if (mctx[s]) pool_give(&dopt[s], mctx[s]);
         }
     };
-    // 1. every shard on its device, a host thread each (H2D + replay)
+    // 1. every shard on its device, a host thread each: its files stream
+    // through gck_replay's ring of contexts (H2D of later groups overlapping
+    // the replay of earlier ones, bounded by max_resident), and each group's
+    // keydir is packed as soon as the group has replayed
     auto replay_shard = [&](uint32_t s) {
-        Shard &x = sh[s];
+        ShardRun &x = sr[s];
+        x.shard = s;
         x.a = ranges[2 * s];
         x.b = ranges[2 * s + 1];
-        gck_opts o{};
-        if (opts) o = *opts;
-        o.device = devs[s];
-        if ((x.rc = gck_ctx_create(&o, &x.ctx))) return;
-        if ((x.rc = ctx_load_srcs(&x.ctx->c, files + x.a, x.b - x.a))) return;
+        x.nown = ndev;
+        x.dev = devs[s];
         if (x.b > x.a) {
-            x.rc = gck_ctx_run(x.ctx);
-            if (x.rc == GCK_EUNEXPECTED_EOF) x.rc = GCK_OK;  // the run's outcome is in its stats
-            if (x.rc) return;
+            x.rc = replay_groups_to(files + x.a, x.b - x.a, &dopt[s], &x, &x.res);
+            if (x.rc == GCK_EUNEXPECTED_EOF) x.rc = GCK_OK;  // the run's outcome is in res
         }
-        x.rc = gck_ctx_stats(x.ctx, &x.st);
+        if (!x.rc) x.rc = pool_take(&dopt[s], &mctx[s]);  // the owner's merge context
     };
     {
         std::vector<std::thread> th;
@@ -226,123 +332,136 @@ static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *device
     }
     mark("replayed");
     for (uint32_t s = 0; s < ndev; ++s)
-        if (sh[s].rc) {
-            rc = sh[s].rc;
+        if (sr[s].rc) {
+            rc = sr[s].rc;
             cleanup();
             return rc;
         }
-    // 2. the global outcome (gocask_amd/shard.py resolve_status): shards in walk
-    // order until the first startup error, which is the global status
-    std::vector<bool> contrib(ndev, false);
-    out->status = GCK_OK;
-    uint32_t base = 0;
-    bool failed = false;
+    // 2. the global outcome
+    std::vector<MultiOutcome> oc(ndev);
     for (uint32_t s = 0; s < ndev; ++s) {
-        if (failed) continue;
-        contrib[s] = true;
-        const gck_stats &st = sh[s].st;
-        const uint32_t nf = sh[s].b - sh[s].a;
-        out->n_crc_fail += nf ? st.n_crc_fail : 0;
-        if (nf && st.status == GCK_EUNEXPECTED_EOF) {
-            failed = true;
-            out->status = GCK_EUNEXPECTED_EOF;
-            out->err_file = base + st.err_file;
-            out->err_off = st.err_off;
-            out->files_walked = base + st.files_walked;
-            out->final_last_offset = st.final_last_offset;
-        } else if (nf) {
-            out->final_last_offset = st.final_last_offset;  // cuts follow resetting files: the last shard's
-        }
-        base += nf;
+        const gck_result &r = sr[s].res;
+        oc[s] = MultiOutcome{r.status, sr[s].b - sr[s].a, r.err_file, r.files_walked, r.final_last_offset, r.err_off,
+                             r.n_crc_fail};
     }
-    if (!failed) out->files_walked = nfiles;
-    out->n_groups = ndev;
-    out->n_resident = ndev;
-    // 3. keydir with tombstones per contributing shard, partitioned over the owners
-    for (uint32_t s = 0; s < ndev && !rc; ++s) {
-        Shard &x = sh[s];
-        if (!contrib[s] || x.b == x.a) continue;
-        uint64_t n = 0;
-        if ((rc = gck_ctx_keydir(x.ctx, GCK_KD_KEEP_TOMBSTONES, &n, nullptr))) break;
-        if ((rc = gck_kd_pack_sizes(x.ctx, ndev, x.counts, x.kbytes))) break;
-        uint64_t ne = 0, nk = 0;
+    std::vector<uint8_t> contrib(ndev, 0);
+    multi_resolve(oc.data(), ndev, nfiles, out, contrib.data());
+    uint32_t ng = 0, nr = 0;
+    for (uint32_t s = 0; s < ndev; ++s) {
+        ng += sr[s].res.n_groups;
+        nr += sr[s].res.n_resident;
+    }
+    out->n_groups = ng;
+    out->n_resident = nr;
+    // 3. the sources in walk order: every packed group of the contributing
+    // shards (a failing shard's groups end with the one that failed)
+    struct SrcRef {
+        uint32_t shard;
+        const Part *part;
+    };
+    std::vector<SrcRef> srcs;
+    for (uint32_t s = 0; s < ndev; ++s)
+        if (contrib[s])
+            for (const Part &p : sr[s].parts) srcs.push_back(SrcRef{s, &p});
+    const uint32_t nsrc = (uint32_t)srcs.size();
+    if (nsrc > 65536) {
+        cleanup();
+        return GCK_EINVAL;
+    }
+    std::vector<uint64_t> cnt((uint64_t)nsrc * ndev), kb((uint64_t)nsrc * ndev);
+    for (uint32_t i = 0; i < nsrc; ++i)
         for (uint32_t p = 0; p < ndev; ++p) {
-            ne += x.counts[p];
-            nk += x.kbytes[p];
+            cnt[(uint64_t)i * ndev + p] = srcs[i].part->counts[p];
+            kb[(uint64_t)i * ndev + p] = srcs[i].part->kbytes[p];
         }
-        if (hipSetDevice(devs[s]) != hipSuccess || hipMalloc(&x.d_ents, ne * sizeof(gck_kd_entry) + 64) != hipSuccess ||
-            hipMalloc(&x.d_keys, nk + 64) != hipSuccess) {
+    std::vector<uint64_t> e_off((uint64_t)ndev * (nsrc + 1)), k_off((uint64_t)ndev * (nsrc + 1));
+    multi_recv_offsets(cnt.data(), nsrc, ndev, e_off.data());
+    multi_recv_offsets(kb.data(), nsrc, ndev, k_off.data());
+    auto EO = [&](uint32_t p, uint32_t i) { return e_off[(uint64_t)p * (nsrc + 1) + i]; };
+    auto KO = [&](uint32_t p, uint32_t i) { return k_off[(uint64_t)p * (nsrc + 1) + i]; };
+    for (uint32_t p = 0; p < ndev && !rc; ++p) {
+        if (hipSetDevice(devs[p]) != hipSuccess ||
+            hipMalloc(&r_ents[p], EO(p, nsrc) * sizeof(gck_kd_entry) + 64) != hipSuccess ||
+            hipMalloc(&r_keys[p], KO(p, nsrc) + 64) != hipSuccess) {
+            (void)hipGetLastError();
             rc = GCK_ENOMEM;
-            break;
         }
-        rc = gck_kd_pack(x.ctx, s, x.a, static_cast<gck_kd_entry *>(x.d_ents), ne, static_cast<uint8_t *>(x.d_keys), nk);
     }
     mark("packed");
-    // receive buffers: owner p gets partition p of every shard, in shard order
-    std::vector<std::vector<uint64_t>> e_off(ndev, std::vector<uint64_t>(ndev + 1, 0)),
-        k_off(ndev, std::vector<uint64_t>(ndev + 1, 0));
-    for (uint32_t p = 0; p < ndev && !rc; ++p) {
-        for (uint32_t s = 0; s < ndev; ++s) {
-            e_off[p][s + 1] = e_off[p][s] + sh[s].counts[p];
-            k_off[p][s + 1] = k_off[p][s] + sh[s].kbytes[p];
-        }
-        if (hipSetDevice(devs[p]) != hipSuccess ||
-            hipMalloc(&sh[p].r_ents, e_off[p][ndev] * sizeof(gck_kd_entry) + 64) != hipSuccess ||
-            hipMalloc(&sh[p].r_keys, k_off[p][ndev] + 64) != hipSuccess)
-            rc = GCK_ENOMEM;
-    }
-    // 4. the exchange: RCCL send / recv of every (shard, owner) pair in one group
+    // 4. the exchange: partition p of source i into owner p's buffers at
+    // (p, i); device copies on one device, RCCL send / receive pairs in one
+    // group across devices (every count is known here: no size exchange)
     join_comm();
     mark("comms");
+    if (!rc && need_rccl) rc = comm_rc;
     if (!rc) {
-        rc = comm_rc;
-        for (uint32_t s = 0; s < ndev && !rc; ++s) {  // packs done before the sends
-            (void)hipSetDevice(devs[s]);
-            if (hipStreamSynchronize((hipStream_t)gck_ctx_stream(sh[s].ctx)) != hipSuccess) rc = GCK_EDEVICE;
-        }
-        if (!rc) {
-            const Rccl &R = rccl();
-            ncclResult_t r = R.group_start();
-            for (uint32_t s = 0; s < ndev && r == ncclSuccess; ++s) {
-                uint64_t eo = 0, ko = 0;  // shard s's pack offsets of partition p
-                for (uint32_t p = 0; p < ndev && r == ncclSuccess; ++p) {
-                    const uint64_t ne = sh[s].counts[p], nk = sh[s].kbytes[p];
-                    hipStream_t ss = (hipStream_t)gck_ctx_stream(sh[s].ctx), sp = (hipStream_t)gck_ctx_stream(sh[p].ctx);
-                    const uint8_t *se = static_cast<const uint8_t *>(sh[s].d_ents) + eo * sizeof(gck_kd_entry);
-                    const uint8_t *sk = static_cast<const uint8_t *>(sh[s].d_keys) + ko;
-                    uint8_t *re = static_cast<uint8_t *>(sh[p].r_ents) + e_off[p][s] * sizeof(gck_kd_entry);
-                    uint8_t *rk = static_cast<uint8_t *>(sh[p].r_keys) + k_off[p][s];
-                    if (ne) {
-                        r = R.send(se, ne * sizeof(gck_kd_entry), ncclUint8, (int)p, comm[s], ss);
-                        if (r == ncclSuccess) r = R.recv(re, ne * sizeof(gck_kd_entry), ncclUint8, (int)s, comm[p], sp);
-                    }
-                    if (nk && r == ncclSuccess) {
-                        r = R.send(sk, nk, ncclUint8, (int)p, comm[s], ss);
-                        if (r == ncclSuccess) r = R.recv(rk, nk, ncclUint8, (int)s, comm[p], sp);
-                    }
-                    eo += ne;
-                    ko += nk;
+        std::unique_lock<std::mutex> lk;
+        if (need_rccl) lk = std::unique_lock<std::mutex>(*cset.mu);
+        const Rccl &R = rccl();
+        bool grouped = false;
+        ncclResult_t r = ncclSuccess;
+        for (uint32_t i = 0; i < nsrc && !rc && r == ncclSuccess; ++i) {
+            const uint32_t s = srcs[i].shard;
+            const Part &pt = *srcs[i].part;
+            uint64_t eo = 0, ko = 0;  // the part's offsets of partition p
+            for (uint32_t p = 0; p < ndev && !rc && r == ncclSuccess; ++p) {
+                const uint64_t ne = pt.counts[p], nk = pt.kbytes[p];
+                const uint8_t *se = static_cast<const uint8_t *>(pt.d_ents) + eo * sizeof(gck_kd_entry);
+                const uint8_t *sk = static_cast<const uint8_t *>(pt.d_keys) + ko;
+                uint8_t *re = static_cast<uint8_t *>(r_ents[p]) + EO(p, i) * sizeof(gck_kd_entry);
+                uint8_t *rk = static_cast<uint8_t *>(r_keys[p]) + KO(p, i);
+                hipStream_t sp = mctx[p]->c.stream, ss = mctx[s]->c.stream;
+                eo += ne;
+                ko += nk;
+                if (devs[s] == devs[p] && !rccl_self) {
+                    (void)hipSetDevice(devs[p]);
+                    if ((ne && hipMemcpyAsync(re, se, ne * sizeof(gck_kd_entry), hipMemcpyDeviceToDevice, sp) != hipSuccess) ||
+                        (nk && hipMemcpyAsync(rk, sk, nk, hipMemcpyDeviceToDevice, sp) != hipSuccess))
+                        rc = GCK_EDEVICE;
+                    continue;
+                }
+                if (!grouped) {
+                    r = R.group_start();
+                    grouped = true;
+                    if (r != ncclSuccess) break;
+                }
+                if (ne) {
+                    r = R.send(se, ne * sizeof(gck_kd_entry), ncclUint8, (int)p, cset.comms[s], ss);
+                    if (r == ncclSuccess) r = R.recv(re, ne * sizeof(gck_kd_entry), ncclUint8, (int)s, cset.comms[p], sp);
+                }
+                if (nk && r == ncclSuccess) {
+                    r = R.send(sk, nk, ncclUint8, (int)p, cset.comms[s], ss);
+                    if (r == ncclSuccess) r = R.recv(rk, nk, ncclUint8, (int)s, cset.comms[p], sp);
                 }
             }
+        }
+        if (grouped) {
             const ncclResult_t r2 = R.group_end();
             if (r == ncclSuccess) r = r2;
-            if (r != ncclSuccess) {
-                set_error(R.err(r), hipErrorUnknown, __FILE__, __LINE__);
-                rc = GCK_EDEVICE;
-            }
+        }
+        if (r != ncclSuccess) {
+            set_error(R.err ? R.err(r) : "rccl", hipErrorUnknown, __FILE__, __LINE__);
+            rc = GCK_EDEVICE;
+        }
+        // the exchange is complete (and the communicators free for another
+        // call) once every owner's stream is
+        for (uint32_t p = 0; p < ndev; ++p) {
+            (void)hipSetDevice(devs[p]);
+            if (hipStreamSynchronize(mctx[p]->c.stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
         }
     }
     mark("exchanged");
-    // 5. per owner, the merge; the live entries gathered in owner order
+    // 5. per owner, the merge (sources in walk order: the last writer wins, a
+    // winning tombstone drops the key); the live entries gathered in owner order
     std::vector<uint64_t> n_live(ndev, 0);
     for (uint32_t p = 0; p < ndev && !rc; ++p) {
-        std::vector<uint64_t> sc(ndev), sk(ndev);
-        for (uint32_t s = 0; s < ndev; ++s) {
-            sc[s] = sh[s].counts[p];
-            sk[s] = sh[s].kbytes[p];
+        std::vector<uint64_t> sc(nsrc ? nsrc : 1, 0), sk(nsrc ? nsrc : 1, 0);
+        for (uint32_t i = 0; i < nsrc; ++i) {
+            sc[i] = cnt[(uint64_t)i * ndev + p];
+            sk[i] = kb[(uint64_t)i * ndev + p];
         }
-        rc = gck_kd_merge(sh[p].ctx, static_cast<const gck_kd_entry *>(sh[p].r_ents),
-                          static_cast<const uint8_t *>(sh[p].r_keys), sc.data(), sk.data(), ndev, &n_live[p], nullptr);
+        rc = gck_kd_merge(mctx[p], static_cast<const gck_kd_entry *>(r_ents[p]), static_cast<const uint8_t *>(r_keys[p]),
+                          sc.data(), sk.data(), nsrc ? nsrc : 1, &n_live[p], nullptr);
     }
     uint64_t tot = 0;
     for (uint64_t v : n_live) tot += v;
@@ -355,11 +474,11 @@ static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *device
     std::vector<uint8_t> kblob;  // GCK_OPT_KEYS: the entries' key bytes in output order
     for (uint32_t p = 0; p < ndev && !rc; ++p) {
         uint64_t n = 0, nk = 0;
-        if ((rc = gck_kd_fetch_merged(sh[p].ctx, nullptr, 0, nullptr, 0, &n, &nk))) break;
+        if ((rc = gck_kd_fetch_merged(mctx[p], nullptr, 0, nullptr, 0, &n, &nk))) break;
         if (!n) continue;
         std::vector<gck_kd_entry> ents(n);
         std::vector<uint8_t> keys(nk + 1);
-        if ((rc = gck_kd_fetch_merged(sh[p].ctx, ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
+        if ((rc = gck_kd_fetch_merged(mctx[p], ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
         for (uint64_t i = 0; i < n; ++i) {
             h[at + i] = ents[i].rec;
             if (want_keys) kblob.insert(kblob.end(), keys.begin() + (ptrdiff_t)ents[i].key_off,
@@ -387,13 +506,16 @@ static int replay_multi(const Src *files, uint32_t nfiles, const int32_t *device
     return out->status;
 }
 
+}  // namespace gck
+
 extern "C" int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
                                 const gck_opts *opts, gck_result *out) {
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
     if (nfiles && !files) return GCK_EINVAL;
+    if (!devices || ndev == 0 || ndev > 64) return GCK_EINVAL;
     const std::vector<Src> v = mem_srcs(files, nfiles);
-    return replay_multi(v.data(), nfiles, devices, ndev, opts, out);
+    return replay_multi(v.data(), nfiles, std::vector<int>(devices, devices + ndev), opts, out, false);
 }
 
 extern "C" int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
@@ -401,10 +523,11 @@ extern "C" int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, co
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
     if (nfiles && !files) return GCK_EINVAL;
+    if (!devices || ndev == 0 || ndev > 64) return GCK_EINVAL;
     std::vector<Src> v;
     int rc = open_srcs(files, nfiles, v);
     if (rc) return rc;
-    rc = replay_multi(v.data(), nfiles, devices, ndev, opts, out);
+    rc = replay_multi(v.data(), nfiles, std::vector<int>(devices, devices + ndev), opts, out, false);
     close_srcs(v);
     return rc;
 }

@@ -914,6 +914,51 @@ constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue 
 constexpr uint32_t kStaticEighths = 4;     // eighths of k_crc_rows' full rounds assigned statically
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
 
+// Diagnostic build only (make EXTRA=-DGCK_CLOCK_STAMPS OUT=../var/...): every
+// wavefront of k_crc_rows and of k_clk_stream stamps the shader clock and the
+// 100 MHz real-time counter when its loop starts and when it leaves, into
+// buffers of their own that nothing else reads; the in-kernel clock is
+// d(shader clock) / d(real time) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
+// gck_xp_clock() reads them back.  The product build has no stamp.
+#ifdef GCK_CLOCK_STAMPS
+constexpr uint32_t kClkWaves = 16384;
+__device__ uint64_t g_clk[2][4 * kClkWaves];
+__device__ __forceinline__ void clk_put(int which, uint32_t wi, uint64_t t0, uint64_t r0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0 && wi < kClkWaves) {
+        u32x4 a, b;
+        a.x = (uint32_t)t0, a.y = (uint32_t)(t0 >> 32), a.z = (uint32_t)r0, a.w = (uint32_t)(r0 >> 32);
+        b.x = (uint32_t)t1, b.y = (uint32_t)(t1 >> 32), b.z = (uint32_t)r1, b.w = (uint32_t)(r1 >> 32);
+        u32x4 *d = reinterpret_cast<u32x4 *>(&g_clk[which][4 * wi]);
+        d[0] = a;
+        d[1] = b;
+    }
+}
+#define GCK_CLK_BEGIN() const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime()
+#define GCK_CLK_END(which, wi) clk_put(which, wi, clk_t0, clk_r0)
+// the plain non-temporal stream read (diag.hip's k_stream_read<true>), stamped
+__global__ __launch_bounds__(256) void k_clk_stream(const uint4 *__restrict__ p, uint64_t n16, uint32_t *sink) {
+    GCK_CLK_BEGIN();
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x * 4;
+    uint32_t acc = 0;
+    auto ld = [&](uint64_t i) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(p + i));
+        return v.x ^ v.y ^ v.z ^ v.w;
+    };
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x * 4 + threadIdx.x; i < n16; i += stride) {
+        const uint32_t a = ld(i), b = i + 256 < n16 ? ld(i + 256) : 0u, c = i + 512 < n16 ? ld(i + 512) : 0u,
+                       d = i + 768 < n16 ? ld(i + 768) : 0u;
+        acc ^= a ^ b ^ c ^ d;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+    GCK_CLK_END(1, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+#else
+#define GCK_CLK_BEGIN() ((void)0)
+#define GCK_CLK_END(which, wi) ((void)0)
+#endif
+
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ uint32_t dpp(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWMASK, 0xF, false);
@@ -1188,8 +1233,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     };
 
     // prologue: this wave's first two blocks, their plans, the first batch
+    GCK_CLK_BEGIN();
     uint64_t q = grab();
-    if (q >= n_blocks) return;
+    if (q >= n_blocks) {
+        GCK_CLK_END(0, w);
+        return;
+    }
     uint64_t qn = grab();
     Plan pc, pn;
     Batch bc, bn;
@@ -1242,7 +1291,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
         *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
-        if (qn >= n_blocks) return;
+        if (qn >= n_blocks) {
+            GCK_CLK_END(0, w);
+            return;
+        }
         q = qn;
         qn = qnn;
         pc = pn;
@@ -2240,7 +2292,7 @@ int gck::ctx_load_srcs(Ctx *c, const Src *src, uint32_t nfiles) {
     std::vector<uint64_t> lens(nfiles);
     std::vector<uint8_t> reset(nfiles);
     for (uint32_t f = 0; f < nfiles; ++f) {
-        if (src[f].len && !src[f].data && src[f].fd < 0) return GCK_EINVAL;
+        if (src[f].len && !src[f].data && !src[f].path) return GCK_EINVAL;
         lens[f] = src[f].len;
         reset[f] = src[f].reset_after ? 1 : 0;
     }
@@ -2400,8 +2452,10 @@ __global__ void k_push_recs(const uint4 *__restrict__ src, uint4 *__restrict__ d
 
 // Contexts of the grouped replay are kept for the next call: their arenas
 // and tables stay allocated, so a repeated Open pays no hipMalloc and no table
-// upload.  Bounded: at most kPoolMax contexts, all for one options key (a
-// call with other options evicts them).  gck_replay_release_cache frees them.
+// upload.  Bounded: at most kPoolMax contexts per device, all for one options
+// key (a call with other options on that device evicts them; calls on other
+// devices -- gck_replay_multi's device threads -- keep theirs).
+// gck_replay_release_cache frees them.
 namespace {
 constexpr size_t kPoolMax = 4;
 struct PoolEntry {
@@ -2421,7 +2475,7 @@ bool same_opts(const gck_opts &a, const gck_opts &b) {
     return a.device == b.device && a.chunk_bytes == b.chunk_bytes && a.max_key == b.max_key &&
            a.chunk_cap == b.chunk_cap && a.spec_window == b.spec_window && a.flags == b.flags;
 }
-int pool_take(const gck_opts *o, gck_ctx **out) {
+int pool_take_(const gck_opts *o, gck_ctx **out) {
     const gck_opts k = pool_key(o);
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
@@ -2434,20 +2488,22 @@ int pool_take(const gck_opts *o, gck_ctx **out) {
     }
     return gck_ctx_create(o, out);
 }
-void pool_give(const gck_opts *o, gck_ctx *c) {
+void pool_give_(const gck_opts *o, gck_ctx *c) {
     if (!c) return;
     const gck_opts k = pool_key(o);
     std::vector<gck_ctx *> drop;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
+        size_t same_dev = 0;
         for (size_t i = 0; i < g_pool.size();)
-            if (!same_opts(g_pool[i].key, k)) {
+            if (g_pool[i].key.device == k.device && !same_opts(g_pool[i].key, k)) {
                 drop.push_back(g_pool[i].ctx);
                 g_pool.erase(g_pool.begin() + (ptrdiff_t)i);
             } else {
+                same_dev += g_pool[i].key.device == k.device;
                 ++i;
             }
-        if (g_pool.size() < kPoolMax)
+        if (same_dev < kPoolMax)
             g_pool.push_back(PoolEntry{k, c});
         else
             drop.push_back(c);
@@ -2503,12 +2559,15 @@ static int gather_keys(Ctx *c, void **host, uint64_t *len) {
     return GCK_OK;
 }
 
+// sink: gck_replay_multi's hook (GroupSink, gck_internal.h): each group's
+// context is handed to it after the group has replayed, and no tuples or keys
+// are delivered (out carries the outcome only).
 static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opts, bool into, gck_rec *dst,
-                          uint64_t cap, gck_result *out) {
+                          uint64_t cap, gck_result *out, GroupSink *sink = nullptr) {
     const auto t_call = std::chrono::steady_clock::now();
     memset(out, 0, sizeof(*out));
     for (uint32_t f = 0; f < nfiles; ++f)
-        if (files[f].len && !files[f].data && files[f].fd < 0) return GCK_EINVAL;
+        if (files[f].len && !files[f].data && !files[f].path) return GCK_EINVAL;
     const uint64_t budget_opt = opts ? opts->max_resident : 0;
     // group target: about a quarter of the database (at least kGroupBytes),
     // or a third of a tight budget (so at least two groups of files smaller
@@ -2559,15 +2618,14 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     std::vector<hipStream_t> own_s(R, nullptr);  // the contexts' own streams while they run on run_s
     std::vector<void *> chunks(G, nullptr);        // ring mode, gck_replay: each group's tuples (pinned)
     std::vector<uint64_t> chunk_n(G, 0);
-    const bool want_keys = opts && (opts->flags & GCK_OPT_KEYS);
+    const bool want_keys = !sink && opts && (opts->flags & GCK_OPT_KEYS);
+    if (sink) into = false;
     std::vector<void *> kchunks(G, nullptr);  // GCK_OPT_KEYS: each group's key bytes (pinned)
     std::vector<uint64_t> kchunk_n(G, 0);
     int rc = GCK_OK;
     Copier cp;  // the file copies (staging.hip)
     auto cleanup = [&](bool keep) {
         (void)cp.finish();
-        for (void *q : kchunks)
-            if (q) (void)hipHostFree(q);
         if (copy) (void)hipStreamSynchronize(copy);
         if (run_s) {
             (void)hipStreamSynchronize(run_s);
@@ -2580,12 +2638,16 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         if (copy) (void)hipStreamDestroy(copy);
+        // (after the stream synchronisations: a key gather's D2H may still be
+        // writing a kchunk on an error path)
+        for (void *q : kchunks)
+            if (q) (void)hipHostFree(q);
         for (void *p : chunks)
             if (p) (void)hipHostFree(p);
         for (auto *c : cs) {
             if (!c) continue;
             if (keep)
-                pool_give(opts, c);
+                pool_give_(opts, c);
             else
                 gck_ctx_destroy(c);
         }
@@ -2595,7 +2657,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     // contexts are created
     int pre_rc = GCK_OK;
     std::thread pre([&] { pre_rc = stage_prealloc(opts ? opts->device : 0, stage_buffers_wanted()); });
-    for (uint32_t k = 0; k < R && !rc; ++k) rc = pool_take(opts, &cs[k]);
+    for (uint32_t k = 0; k < R && !rc; ++k) rc = pool_take_(opts, &cs[k]);
     pre.join();
     if (!rc) rc = pre_rc == GCK_ENOMEM ? GCK_OK : pre_rc;  // (the copier retries the allocation)
     if (rc) {
@@ -2669,7 +2731,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
             if (pinned[f0 + k]) {
                 if ((r = cp.direct(f.data, f.len, d))) return r;
             } else {
-                cp.add(g, f.data, f.fd, 0, f.len, d);
+                cp.add(g, f.data, f.path, 0, f.len, d);
             }
         }
         cp.seal(g);  // its event follows its last chunk on the copy stream
@@ -2713,6 +2775,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
             break;
         }
         if (want_keys && c->n_recs && (rc = gather_keys(c, &kchunks[g], &kchunk_n[g]))) break;
+        if (sink && (rc = sink->group(g, cut[g], cs[g % R]))) break;
         g_fail[g] = c->n_crc_fail;
         n_total += c->n_recs;
         st_status = c->status;
@@ -2736,7 +2799,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
                     rc = GCK_EDEVICE;
                 off += c->n_recs;
             }
-        } else if (c->n_recs && !into) {
+        } else if (c->n_recs && !into && !sink) {
             // library-owned output: the group's tuples into a pinned chunk now
             // (written by the GPU through its mapping while later groups still
             // copy; in ring mode the context is about to be reused), joined by
@@ -2806,14 +2869,28 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
         out->keys = static_cast<uint8_t *>(kp);
         out->keys_len = kt;
     }
+    auto drop_keys = [&]() {  // an error return hands back no key blob
+        res_free(out->keys);
+        out->keys = nullptr;
+        out->keys_len = 0;
+    };
     if (into) {
         cleanup(true);
-        if (cap < n_total) return GCK_EINVAL;  // out->n says how many records to make room for
+        if (cap < n_total) {  // out->n says how many records to make room for
+            drop_keys();
+            return GCK_EINVAL;
+        }
+        return out->status;
+    }
+    if (sink) {  // the outcome only: the sink took what it needed from each group
+        out->n = 0;
+        cleanup(true);
         return out->status;
     }
     // the groups' pinned chunks into one plain array, in order
     if (hipStreamSynchronize(run_s) != hipSuccess) {
         cleanup(false);
+        drop_keys();
         return GCK_EDEVICE;
     }
     gck_rec *h = nullptr;
@@ -2821,6 +2898,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
         h = static_cast<gck_rec *>(res_alloc(n_total * sizeof(gck_rec), false));
         if (!h) {
             cleanup(true);
+            drop_keys();
             return GCK_ENOMEM;
         }
         std::vector<std::pair<const void *, uint64_t>> segs;
@@ -2894,5 +2972,59 @@ int gck_device_count(void) {
 const char *gck_version(void) { return "gocask_hip 0.1 (gfx950)"; }
 
 const char *gck_last_error(void) { return gck::last_error(); }
+
+}  // extern "C"
+
+namespace gck {
+int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, GroupSink *sink, gck_result *out) {
+    if (!out || !sink || (nfiles && !files)) return GCK_EINVAL;
+    return replay_grouped(files, nfiles, opts, false, nullptr, 0, out, sink);
+}
+int pool_take(const gck_opts *o, gck_ctx **out) { return pool_take_(o, out); }
+void pool_give(const gck_opts *o, gck_ctx *c) { pool_give_(o, c); }
+}  // namespace gck
+
+extern "C" {
+
+#ifdef GCK_CLOCK_STAMPS
+// Diagnostic build only: which 0 = k_crc_rows' stamps of the last run, 1 =
+// k_clk_stream's; out receives 4 u64 per wavefront (clock, real time at the
+// loop start, then at the end), kClkWaves entries; zeroed by reset.
+int gck_xp_clock_reset(void) {
+    static const uint64_t zero[2][4 * kClkWaves] = {};
+    GCK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_clk), zero, sizeof zero));
+    return GCK_OK;
+}
+int gck_xp_clock_read(int which, uint64_t *out) {
+    if (which < 0 || which > 1 || !out) return GCK_EINVAL;
+    GCK_HIP(hipDeviceSynchronize());
+    GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(uint64_t) * 4 * kClkWaves,
+                                sizeof(uint64_t) * 4 * kClkWaves * which));
+    return GCK_OK;
+}
+// iters back-to-back stamped stream reads of the context's arena; *ms = per launch
+int gck_xp_clock_stream(gck_ctx *ctx, int iters, double *ms) {
+    if (!ctx || iters <= 0) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    const uint64_t n16 = c->arena_len / 16;
+    if (!n16) return GCK_EINVAL;
+    const uint32_t grid = (uint32_t)c->n_cu * 8;
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) k_clk_stream<<<grid, 256, 0, c->stream>>>(c->arena.as<uint4>(), n16, sink);
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float t = 0;
+    GCK_HIP(hipEventElapsedTime(&t, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (ms) *ms = t / iters;
+    return GCK_OK;
+}
+#endif
 
 }  // extern "C"

@@ -105,7 +105,7 @@ int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const 
             if (src[f].data && host_pinned(src[f].data))
                 rc = cp.direct(src[f].data, src[f].len, dst[f]);
             else
-                cp.add(0, src[f].data, src[f].fd, 0, src[f].len, dst[f]);
+                cp.add(0, src[f].data, src[f].path, 0, src[f].len, dst[f]);
         }
         cp.seal(0);
         if (!rc) rc = cp.wait_recorded(0);
@@ -119,31 +119,28 @@ int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const 
 
 std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles) {
     std::vector<Src> v(nfiles);
-    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, -1, files[f].len, files[f].reset_after != 0};
+    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, nullptr, files[f].len, files[f].reset_after != 0};
     return v;
 }
 
 int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &v) {
-    v.assign(nfiles, Src{nullptr, -1, 0, false});
+    v.assign(nfiles, Src{nullptr, nullptr, 0, false});
     for (uint32_t f = 0; f < nfiles; ++f) {
         struct stat st;
-        if (!files[f].path || (v[f].fd = open(files[f].path, O_RDONLY | O_CLOEXEC)) < 0 || fstat(v[f].fd, &st) != 0) {
-            close_srcs(v);
+        if (!files[f].path || stat(files[f].path, &st) != 0 || !S_ISREG(st.st_mode)) {
+            if (files[f].path) set_error("stat of a data file failed (missing, or not a regular file)", hipSuccess,
+                                         __FILE__, __LINE__);
+            v.clear();
             return GCK_EIO;
         }
+        v[f].path = files[f].path;
         v[f].len = (uint64_t)st.st_size;
         v[f].reset_after = files[f].reset_after != 0;
     }
     return GCK_OK;
 }
 
-void close_srcs(std::vector<Src> &v) {
-    for (auto &s : v)
-        if (s.fd >= 0) {
-            close(s.fd);
-            s.fd = -1;
-        }
-}
+void close_srcs(std::vector<Src> &v) { v.clear(); }
 
 uint32_t stage_buffers_wanted() { return 2 * copy_threads(); }
 
@@ -219,8 +216,8 @@ void stage_release() {
 
 struct Copier::Impl {
     struct Job {
-        const uint8_t *src;  // caller memory, or nullptr: pread(fd, off)
-        int fd;
+        const uint8_t *src;  // caller memory, or nullptr: pread of path at off
+        const char *path;
         uint64_t off, len;
         uint8_t *dst;
         uint32_t group;
@@ -277,15 +274,20 @@ struct Copier::Impl {
             if (j.src) {
                 memcpy(stage, j.src + j.off, j.len);
             } else {
+                // the file is opened per chunk: at most one descriptor per
+                // copy thread is ever open
+                const int fd = open(j.path, O_RDONLY | O_CLOEXEC);
                 uint64_t got = 0;
-                while (got < j.len) {
-                    const ssize_t r = pread(j.fd, stage + got, j.len - got, (off_t)(j.off + got));
+                ok = fd >= 0;
+                while (ok && got < j.len) {
+                    const ssize_t r = pread(fd, stage + got, j.len - got, (off_t)(j.off + got));
                     if (r <= 0) {
                         ok = false;
                         break;
                     }
                     got += (uint64_t)r;
                 }
+                if (fd >= 0) close(fd);
             }
             std::lock_guard<std::mutex> lk(mu);
             if (!ok && !err) {  // the file shrank or could not be read
@@ -335,12 +337,12 @@ int Copier::start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev
     return GCK_OK;
 }
 
-void Copier::add(uint32_t group, const uint8_t *src, int fd, uint64_t off, uint64_t len, uint8_t *dst) {
+void Copier::add(uint32_t group, const uint8_t *src, const char *path, uint64_t off, uint64_t len, uint8_t *dst) {
     std::lock_guard<std::mutex> lk(p->mu);
     const uint64_t C = stage_chunk();
     for (uint64_t o = 0; o < len; o += C) {
         const uint64_t n = std::min(C, len - o);
-        p->jobs.push_back(Impl::Job{src, fd, off + o, n, dst + o, group});
+        p->jobs.push_back(Impl::Job{src, path, off + o, n, dst + o, group});
         ++p->pending[group];
     }
     p->cv_job.notify_all();

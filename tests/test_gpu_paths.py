@@ -109,14 +109,37 @@ def test_paths_missing_or_unreadable_file(g, tmp_path):
         g.replay_paths([str(tmp_path / "absent.csk")], [False])
     assert e.value.code == g._lib.GCK_EIO
     assert not os.path.exists(tmp_path / "absent.csk")
-    # a directory opens and stats but cannot be read: the copier's pread fails
+    # a directory named as a data file is not a regular file: GCK_EIO
     d = tmp_path / "adir.csk"
     d.mkdir()
     (d / "x").write_bytes(b"y" * 100)
-    if os.stat(d).st_size > 0:
-        with pytest.raises(g._lib.GckError) as e:
-            g.replay_paths([str(d)], [False])
-        assert e.value.code == g._lib.GCK_EIO
+    with pytest.raises(g._lib.GckError) as e:
+        g.replay_paths([str(d)], [False])
+    assert e.value.code == g._lib.GCK_EIO
+
+
+def test_paths_more_files_than_descriptors(g, orc, tmp_path):
+    """no descriptor is held per file across the call (the copier
+    opens a file per chunk it reads), so a database with more data files than
+    the soft RLIMIT_NOFILE left to the process still replays, as the
+    reference's Walk opens one file at a time (internal/fs/disk.go:122-145)."""
+    import resource
+
+    wf, reset = _corpus(orc, seed=97, n_files=1)
+    files = [wf[0][: (i % 7) * 900 + 200] for i in range(160)]  # prefixes: some end mid-record
+    reset = [True] * 159 + [False]
+    want, wst = orc.replay(files, reset)
+    paths = _write(tmp_path, files)
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    open_now = len(os.listdir("/proc/self/fd"))
+    lim = open_now + 48  # fewer free descriptors than files
+    assert lim < len(files) + open_now
+    resource.setrlimit(resource.RLIMIT_NOFILE, (min(lim, soft), hard))
+    try:
+        got, gst = g.replay_paths(paths, reset)
+    finally:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+    _same(got, gst, want, wst)
 
 
 def _want_keys(files, want):
