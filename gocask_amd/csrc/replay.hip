@@ -1011,7 +1011,14 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 // without a record end to an out-of-range offset, dropped), so the compiler's
 // vmcnt waits count the same stores on every path and stay a row behind the
 // loads.
+#define GCK_SPLAN 2
+#define GCK_EPACC 0
+#define GCK_ARENA_AUX kArenaAux
+constexpr int kPrefetch = 1;
+constexpr int kRowsPerStep = 1;
+template <int MODE, int NR>
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
+                                                   const uint4 *__restrict__ plan,
                                                    const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
@@ -1020,9 +1027,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    uint32_t *__restrict__ queue,
                                                    const uint64_t *__restrict__ rec_off,
                                                    const uint2 *__restrict__ rec_kv, uint64_t row0) {
-    constexpr int kSteps = kBlockRows;  // rows per block, one per step
+    static_assert(kBlockRows % (4 * NR) == 0, "a block is whole quads of steps");
+    constexpr int kSteps = kBlockRows / NR;  // steps per block
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
-    fill_crc_lds(lds, g_slice, g_nib);
+    if constexpr ((MODE & 64) == 0) fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     static_assert(kNibBase * 4 == 0x20000, "shift-table addresses: byte 2 of the v_perm base");
     const uint32_t nbase = kNibBase * 4 + lane * 4;  // byte 0: the lane's bank, byte 2: the region
@@ -1055,7 +1063,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     // compute, a fully static split loses to the queue's balance (6.02 vs
     // 5.82 ms), half static / half queue is best (5.77).
     const uint32_t W = gridDim.x * kWaves, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    const uint32_t n_static = (uint32_t)(n_blocks / W) * kStaticEighths / 8;
+    const uint32_t n_static = (MODE & 128) ? (uint32_t)((n_blocks + W - 1) / W) : (uint32_t)(n_blocks / W) * kStaticEighths / 8;
     uint32_t st_k = 0;
     uint32_t last = kClaim - 1;
     auto grab = [&]() -> uint32_t {  // next block index
@@ -1070,20 +1078,31 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         return last;
     };
     struct Plan {
-        uint32_t ra;  // row_first of row `lane` of the block
-        uint32_t re;  // row_first of the block's end
+#if !GCK_SPLAN
+        uint4 a, b;  // the lane's 64 row nibbles
+#endif
+        uint32_t ra; // row_first of row lane
+        uint32_t re; // row_first of the block's end (GCK_SPLAN)
     };
     auto load_plan = [&](uint64_t q, Plan &p) {
         const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
+#if !GCK_SPLAN
+        const uint4 *src = plan + qc * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
+        p.a = src[0];
+        p.b = src[1];
+#else
         p.re = row_first[min(qc * kBlockRows + kBlockRows, n_rows)];
+#endif
         p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
     };
-    // The block's nibbles from its record ends (records [ra0, re) end in its
-    // rows, in offset order): a lane per record computes (row, slab, block) of
-    // its last byte, then a uniform loop hands each end to the slab's lane
-    // (nibble dword chosen by a uniform index).  The first 64 record ends of a
-    // block are loaded one block ahead (Batch); later ones (blocks with more
-    // than 64 ends) on the spot.
+#if GCK_SPLAN
+    // The block's plan nibbles from its record ends (records [ra0, re) end in
+    // its rows, in offset order), instead of k_row_plan's dense 32 B per row:
+    // a lane per record computes (row, slab, block) of its last byte, then a
+    // uniform loop hands each end to the slab's lane (nibble dword chosen by
+    // a uniform index).
+    // GCK_SPLAN 2: the first 64 record ends of a block are loaded one block
+    // ahead (Batch); later ones (blocks with more than 64 ends) on the spot
     struct Batch {
         uint64_t off;
         uint2 kv;
@@ -1093,7 +1112,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         b.off = rec_off[r];
         b.kv = rec_kv[r];
     };
-    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch &first, uint32_t (&nb)[8]) {
+    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch *first, uint32_t (&nb)[8]) {
 #pragma unroll
         for (int d = 0; d < 8; ++d) nb[d] = 0;
         const uint64_t base = (row0 + row_b) * kRow;
@@ -1101,8 +1120,8 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             const uint32_t r = b0 + lane;
             uint32_t code = 0;
             if (r < re_) {
-                const uint64_t end = b0 == ra0_ ? first.off + 16 + (uint64_t)first.kv.x + first.kv.y
-                                                : value_end(rec_off, rec_kv, r);
+                const uint64_t end = first && b0 == ra0_ ? first->off + 16 + (uint64_t)first->kv.x + first->kv.y
+                                                         : value_end(rec_off, rec_kv, r);
                 const uint64_t rel = end - 1 - base;  // < 64 rows
                 code = ((uint32_t)(rel >> 12) << 8) | ((uint32_t)(rel >> 6) & 63u) << 2 | ((uint32_t)(rel >> 4) & 3u);
             }
@@ -1125,114 +1144,216 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             }
         }
     };
-    auto issue = [&](uint64_t row, u32x4 (&x)[4]) {
-        // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
-        const uint32_t r = min((uint32_t)row, (uint32_t)(n_rows - 1));
-        const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kArenaAux);
+#endif
+    struct RowBuf {
+        u32x4 x[4];
     };
-    // one row: row j of the block; m = its nibble in this lane
-    auto process = [&](uint32_t j, uint32_t m, uint32_t ra_reg, const u32x4 (&x)[4], uint32_t &rend_buf) {
-        // w[4 k + c] = dword c of load k; M[b][k] = lane (p + 16 b)'s load k
-        // (= row bytes 1024 k + 64 p + 16 b).  permlane32_swap on (k, k+2)
-        // then permlane16_swap on (k, k+1) transpose M over each lane group
-        // {p, p+16, p+32, p+48}: lane p + 16 r ends with M[0..3][r] = the
-        // bytes 1024 r + 64 p + 16 b, b = 0..3, i.e. slab 16 r + p.
-        uint32_t w[16];
+    auto issue = [&](uint64_t row0, RowBuf (&bs)[NR]) {
+        if constexpr ((MODE & 8) != 0) return;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w[4 * k] = x[k].x;
-            w[4 * k + 1] = x[k].y;
-            w[4 * k + 2] = x[k].z;
-            w[4 * k + 3] = x[k].w;
+        for (int i = 0; i < NR; ++i) {
+            // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
+            const uint32_t r = min((uint32_t)(row0 + i), (uint32_t)(n_rows - 1));
+            const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
+            constexpr int kAux = (MODE & 32) ? 0 : GCK_ARENA_AUX;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
         }
+    };
+    // GCK_EPACC: (c, pre) of consecutive record slots gathered in two
+    // registers (lane l = slot acc_base + l) and stored 64 at a time, at the
+    // block end or when full, instead of one 64-lane store per row
+    uint32_t acc_c = 0, acc_p = 0, acc_n = 0, acc_base = 0;
+    auto acc_flush = [&]() {
+        store_ep(lane < acc_n ? (acc_base + lane - ra0) * 8u : kDrop, acc_c, acc_p);
+        acc_base += acc_n;
+        acc_n = 0;
+    };
+    // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
+    // nib holds their plan nibbles from bit 0 up
+    auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t ra_reg, const RowBuf (&bs)[NR],
+                       uint32_t &rend_buf) {
+        uint32_t w[NR][16];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int i = 0; i < NR; ++i) {
+            // w[i][4 k + c] = dword c of load k; M[b][k] = lane (p + 16 b)'s load k
+            // (= row bytes 1024 k + 64 p + 16 b).  permlane32_swap on (k, k+2)
+            // then permlane16_swap on (k, k+1) transpose M over each lane group
+            // {p, p+16, p+32, p+48}: lane p + 16 r ends with M[0..3][r] = the
+            // bytes 1024 r + 64 p + 16 b, b = 0..3, i.e. slab 16 r + p.
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const auto r = __builtin_amdgcn_permlane32_swap(w[4 * k + c], w[4 * (k + 2) + c], false, false);
-                w[4 * k + c] = r[0];
-                w[4 * (k + 2) + c] = r[1];
+            for (int k = 0; k < 4; ++k) {
+                w[i][4 * k] = bs[i].x[k].x;
+                w[i][4 * k + 1] = bs[i].x[k].y;
+                w[i][4 * k + 2] = bs[i].x[k].z;
+                w[i][4 * k + 3] = bs[i].x[k].w;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(w[i][4 * k + c], w[i][4 * (k + 2) + c], false, false);
+                    w[i][4 * k + c] = r[0];
+                    w[i][4 * (k + 2) + c] = r[1];
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+#pragma unroll
+                for (int k = 0; k < 4; k += 2) {
+                    const auto r = __builtin_amdgcn_permlane16_swap(w[i][4 * k + c], w[i][4 * (k + 1) + c], false, false);
+                    w[i][4 * k + c] = r[0];
+                    w[i][4 * (k + 1) + c] = r[1];
+                }
+            }
+            if constexpr ((MODE & 8) != 0) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) w[i][j] = (uint32_t)(row0 + i) * 2654435761u + lane * 97u + j;
             }
         }
+        // NR independent chains interleaved: NR table reads in flight per step
+        uint32_t a[NR], c1[NR], c2[NR], c3[NR], G[NR];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
+        for (int i = 0; i < NR; ++i) a[i] = w[i][0];
 #pragma unroll
-            for (int k = 0; k < 4; k += 2) {
-                const auto r = __builtin_amdgcn_permlane16_swap(w[4 * k + c], w[4 * (k + 1) + c], false, false);
-                w[4 * k + c] = r[0];
-                w[4 * (k + 1) + c] = r[1];
+        for (int j = 0; j < 16; ++j) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) {
+                const uint32_t nx = j < 15 ? w[i][j < 15 ? j + 1 : 15] : 0u;
+                if constexpr ((MODE & 2) != 0) {
+                    a[i] = (__builtin_amdgcn_alignbit(a[i], a[i], 5) + 0x9E3779B9u) ^ nx;
+                    if (j == 3) c1[i] = a[i];
+                    if (j == 7) c2[i] = a[i];
+                    if (j == 11) c3[i] = a[i];
+                    if (j == 15) G[i] = a[i];
+                } else if (j == 15) {
+                    G[i] = slice4x(lds, lb0, lb1, a[i], 0u);
+                } else if ((j & 3) == 3) {
+                    const uint32_t c = slice4x(lds, lb0, lb1, a[i], 0u);
+                    if (j == 3) c1[i] = c;
+                    if (j == 7) c2[i] = c;
+                    if (j == 11) c3[i] = c;
+                    a[i] = c ^ nx;
+                } else {
+                    a[i] = slice4x(lds, lb0, lb1, a[i], nx);
+                }
             }
         }
-        uint32_t a = w[0], c1 = 0, c2 = 0, c3 = 0, G = 0;
+        // Z_{64(63-lane)}(G) of every row (8 nibble lookups in the lane's
+        // table), then the NR wave scans interleaved so each DPP read finds
+        // its source written a few instructions earlier (no s_nop hazards).
+        // Lookup addresses: byte k of ge / go holds nibble 2k / 2k+1 of G
+        // with the nibble's index in its high half, which makes byte 1 of the
+        // address (table q, entry v): one v_perm_b32 per lookup, 3 VALU to
+        // split G (was a shift, an and and an add per lookup)
+        uint32_t P[NR], pre[NR];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-            const uint32_t nx = t < 15 ? w[t < 15 ? t + 1 : 15] : 0u;
-            if (t == 15) {
-                G = slice4x(lds, lb0, lb1, a, 0u);
-            } else if ((t & 3) == 3) {
-                const uint32_t c = slice4x(lds, lb0, lb1, a, 0u);
-                if (t == 3) c1 = c;
-                if (t == 7) c2 = c;
-                if (t == 11) c3 = c;
-                a = c ^ nx;
+        for (int i = 0; i < NR; ++i) {
+            if constexpr ((MODE & 4) == 0) {
+                // (x & m) | q in one v_bitop3_b32 (truth table 0xEA; the two
+                // constants live in registers set up outside the loop)
+                const uint32_t ge = __builtin_amdgcn_bitop3_b32(G[i], 0x0F0F0F0Fu, 0x60402000u, 0xEA);
+                const uint32_t go = __builtin_amdgcn_bitop3_b32(G[i] >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
+                uint32_t t[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    t[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
+                    t[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
+                }
+                P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
             } else {
-                a = slice4x(lds, lb0, lb1, a, nx);
+                P[i] = G[i];
             }
         }
-        // Z_{64(63-lane)}(G) (8 nibble lookups in the lane's table), then the
-        // wave scan.  Lookup addresses: byte k of ge / go holds nibble 2k /
-        // 2k+1 of G with the nibble's index in its high half, which makes byte
-        // 1 of the address (table q, entry v): one v_perm_b32 per lookup; the
-        // split is (x & m) | q in one v_bitop3_b32 (truth table 0xEA)
-        const uint32_t ge = __builtin_amdgcn_bitop3_b32(G, 0x0F0F0F0Fu, 0x60402000u, 0xEA);
-        const uint32_t go = __builtin_amdgcn_bitop3_b32(G >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
-        uint32_t t8[8];
+        if constexpr ((MODE & 4) == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            t8[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
-            t8[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
-        }
-        uint32_t P = xor3(xor3(t8[0], t8[1], t8[2]), xor3(t8[3], t8[4], t8[5]), t8[6] ^ t8[7]);
-        P ^= dpp<0x111, 0xF>(P);  // row_shr:1
-        P ^= dpp<0x112, 0xF>(P);  // row_shr:2
-        P ^= dpp<0x114, 0xF>(P);  // row_shr:4
-        P ^= dpp<0x118, 0xF>(P);  // row_shr:8
-        P ^= dpp<0x142, 0xA>(P);  // row_bcast:15 -> rows 1, 3
-        P ^= dpp<0x143, 0xC>(P);  // row_bcast:31 -> rows 2, 3
-        const uint32_t pre = dpp<0x138, 0xF>(P);  // wave_shr:1 -> exclusive (lane 0: 0)
-        const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
-        // the register at the start of block b, by masks (no branches; a
-        // chain of selects was turned into a lookup in a scratch copy of
-        // c1..c3)
-        auto cap = [&](uint32_t b) {
-            return (c1 & (0u - (uint32_t)(b == 1))) | (c2 & (0u - (uint32_t)(b == 2))) | (c3 & (0u - (uint32_t)(b == 3)));
-        };
-        if (__ballot(m & (m - 1)) == 0) {
-            // common case: at most one record end per slab, its slot is
-            // ra + (lanes with an end before this one)
-            const uint64_t C = __ballot(m != 0);
-            const uint32_t idx =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-            store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre);
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);  // row_shr:1
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);  // row_shr:2
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);  // row_shr:4
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);  // row_shr:8
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);  // row_bcast:15 -> rows 1, 3
+#pragma unroll
+            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);  // row_bcast:31 -> rows 2, 3
+#pragma unroll
+            for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);  // wave_shr:1 -> exclusive (lane 0: 0)
         } else {
-            // a slab with 2..4 record ends (records under 64 B): ids by an
-            // exclusive count over the lanes, four stores per lane
-            const uint32_t n = __builtin_popcount(m);
-            const uint32_t ex = wave_incl_sum(n) - n;
-            uint32_t mm = m;
 #pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre);
-                mm &= mm - 1;
-            }
+            for (int i = 0; i < NR; ++i) pre[i] = 0;
         }
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);  // F(0, row)
-        rend_buf = lane == j ? total : rend_buf;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const uint32_t j = j0 + i;
+            // blocks of this slab holding a record end (the plan is zero past
+            // the last row)
+            const uint32_t m = (nib >> (4 * i)) & 15u;
+            const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
+            // the register at the start of block b (selects, no branches)
+            auto cap = [&](uint32_t b) {
+                uint32_t v = b == 3 ? c3[i] : c2[i];
+                v = b == 1 ? c1[i] : v;
+                return b == 0 ? 0u : v;
+            };
+            if constexpr ((MODE & 16) != 0) {
+                asm volatile("" ::"v"(m), "v"(pre[i]), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
+            } else if (GCK_EPACC) {
+                // the row's ends in slot order (lane, then block), each into
+                // lane acc_n of the accumulator: a uniform loop over the
+                // lanes with ends (about 1.2 per row on C3)
+                (void)ra;
+                // each lane's first end's capture, selected on the vector unit
+                const uint32_t cap0 = cap((uint32_t)__builtin_ctz(m | 16u));
+                auto push = [&](uint32_t cv, uint32_t pv) {
+                    if (acc_n == 64) acc_flush();
+                    acc_c = lane == acc_n ? cv : acc_c;
+                    acc_p = lane == acc_n ? pv : acc_p;
+                    ++acc_n;
+                };
+                uint64_t C = __ballot(m != 0);
+                while (C) {
+                    const int L = __builtin_ctzll(C);
+                    C &= C - 1;
+                    const uint32_t mL = (uint32_t)__builtin_amdgcn_readlane((int)m, L);
+                    const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)pre[i], L);
+                    push((uint32_t)__builtin_amdgcn_readlane((int)cap0, L), pv);
+                    if (mL & (mL - 1)) {  // rare: a slab with 2..4 ends (records under 64 B)
+                        const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)c1[i], L);
+                        const uint32_t v2 = (uint32_t)__builtin_amdgcn_readlane((int)c2[i], L);
+                        const uint32_t v3 = (uint32_t)__builtin_amdgcn_readlane((int)c3[i], L);
+                        for (uint32_t mm = mL & (mL - 1); mm; mm &= mm - 1) {
+                            const uint32_t b = (uint32_t)__builtin_ctz(mm);
+                            push(b == 1 ? v1 : b == 2 ? v2 : v3, pv);
+                        }
+                    }
+                }
+            } else if (__ballot(m & (m - 1)) == 0) {
+                // common case: at most one record end per slab, its slot is
+                // ra + (cut lanes before)
+                const uint64_t C = __ballot(m != 0);
+                const uint32_t idx =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
+                store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
+            } else {
+                // a slab with 2..4 record ends (records under 64 B): ids by
+                // an exclusive count over the lanes, four stores per lane
+                const uint32_t n = __builtin_popcount(m);
+                const uint32_t ex = wave_incl_sum(n) - n;
+                uint32_t mm = m;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
+                    mm &= mm - 1;
+                }
+            }
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P[i], 63);  // F(0, row)
+            rend_buf = lane == j ? total : rend_buf;
+        }
     };
 
-    // prologue: this wave's first two blocks, their plans, the first batch
+    // prologue: this wave's first two blocks, the first plan
     GCK_CLK_BEGIN();
     uint64_t q = grab();
     if (q >= n_blocks) {
@@ -1241,53 +1362,78 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     }
     uint64_t qn = grab();
     Plan pc, pn;
-    Batch bc, bn;
     load_plan(q, pc);
+#if GCK_SPLAN == 2
+    Batch bc, bn;
     load_plan(qn, pn);
     load_batch(pc, bc);
-    // one row in flight ahead of the one processed, in two buffers that
-    // alternate within a quad, so each has fixed registers (two or three rows
-    // ahead measured no faster: 6.71-7.08 / 6.87-6.96 against 6.80-6.81 ms
-    // per C3 step on one box, profiles/r3f/ab_rows_ahead.log)
-    u32x4 buf[2][4];
-    issue(q * kBlockRows, buf[0]);
+#endif
+    // kPrefetch rows in flight per wavefront (row buffers rotate with period
+    // NB, which divides the 4 steps of a quad, so every buffer has fixed
+    // registers)
+    static_assert(kPrefetch == 1 || (NR == 1 && kPrefetch <= 3), "prefetch depth > 1 needs one row per step");
+    constexpr int NB = kPrefetch == 1 ? 2 : 4;
+    RowBuf buf[NB][NR];
+#pragma unroll
+    for (int d = 0; d < kPrefetch; ++d) issue(q * kBlockRows + (uint64_t)d * NR, buf[d]);
     for (;;) {
-        // block q: plan pc and batch bc are resident; pn (block qn) landed
-        // during the previous block: its record ends now, the plan of the
-        // block after it next
+        // block q: plan pc is resident; fetch the next block's plan and claim
+        // the one after it (both land during this block)
+#if GCK_SPLAN == 2
+        // pn (block qn) landed during the previous block: its record ends now,
+        // the plan of the block after it next
         const uint64_t qnn = grab();
         Plan pnn;
         load_batch(pn, bn);
         load_plan(qnn, pnn);
+#else
+        load_plan(qn, pn);
+        const uint64_t qnn = grab();
+#endif
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
+        acc_base = ra0;
+        acc_n = 0;
+#if !GCK_SPLAN
+        const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
+#else
         uint32_t nibs[8];
-        build_nibs(row_b, ra0, pc.re, bc, nibs);
-        // rows in quads: a quad consumes 16 nibble bits per lane
+#if GCK_SPLAN == 2
+        build_nibs(row_b, ra0, pc.re, &bc, nibs);
+#else
+        (void)load_batch;
+        build_nibs(row_b, ra0, pc.re, nullptr, nibs);
+#endif
+#endif
+        // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
+        // lane; the two row buffers alternate, so each has fixed registers
         for (int qd = 0; qd < kSteps / 4; ++qd) {
             // this quad's nibbles (a uniform select: qd is a loop counter)
             uint32_t nib = nibs[0];
 #pragma unroll
             for (int d = 1; d < 8; ++d)
-                if (qd / 2 == d) nib = nibs[d];
-            nib >>= 16 * (qd & 1);
+                if (qd * NR / 2 == d) nib = nibs[d];
+            if constexpr (NR == 1) nib >>= 16 * (qd & 1);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
-                // the next row: this block's, or the next block's first
-                const int ahead = st + 1;
-                const uint64_t nrow = ahead < kSteps ? row_b + (uint64_t)ahead : qn * kBlockRows + (uint64_t)(ahead - kSteps);
-                issue(nrow, buf[(u + 1) & 1]);
+                // the rows kPrefetch steps ahead: this block, or the next block's first
+                const int ahead = st + kPrefetch;
+                const uint64_t nrow =
+                    ahead < kSteps ? row_b + (uint64_t)ahead * NR : qn * kBlockRows + (uint64_t)(ahead - kSteps) * NR;
+                issue(nrow, buf[(u + kPrefetch) % NB]);
                 // keep the next row's loads here, ahead of this row's compute:
                 // left alone, the scheduler sinks them past most of the chain
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process((uint32_t)st, (nib >> (4 * u)) & 15u, pc.ra, buf[u & 1], rend_buf);
+                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u % NB],
+                        rend_buf);
             }
         }
+        if (GCK_EPACC) acc_flush();
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
         *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
@@ -1298,10 +1444,16 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         q = qn;
         qn = qnn;
         pc = pn;
+#if GCK_SPLAN == 2
         pn = pnn;
         bc = bn;
+#endif
     }
 }
+
+#undef GCK_SPLAN
+#undef GCK_EPACC
+#undef GCK_ARENA_AUX
 
 // ---------------------------------------------------------------- finalize ---
 // Per record r = [rs, ve) (core/db.go:311 applied to every record).  Notation
@@ -1997,8 +2149,8 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_crc_rows<<<grid, 1024, 0, s>>>(
-        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
+    k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, nullptr, c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0);
     return GCK_OK;

@@ -141,9 +141,62 @@ def test_c3_file_with_100_header_flips(g, orc):
     for i in rng.choice(len(clean), 100, replace=False):
         f[int(clean[i]["rec_off"]) + int(rng.integers(16))] ^= np.uint8(1 << int(rng.integers(8)))
     want, wst = orc.replay([f], [True])
+    # the records before the first desync are the clean ones (offsets agree);
+    # past it the reference reads whatever the bytes say
+    n = min(len(want), len(clean))
+    diff = np.nonzero(want["rec_off"][:n] != clean["rec_off"][:n])[0]
+    first = int(diff[0]) if len(diff) else n
+    print(f"c3 file 0, 100 header flips: {len(want)} records replayed, {first} before the first desync, "
+          f"{len(clean)} clean; status {wst['status']}")
+    assert 0 < first <= len(want)
     with g.ReplayContext() as ctx:
         ctx.load([f], [True])
         for run in range(2):
             ctx.run()
             got, gst = ctx.fetch()
             _same(got, gst, want, wst, f"c3 file 0 run {run}")
+
+
+@pytest.mark.gpu
+def test_c3_file_1000_crc_and_timestamp_flips(g, orc):
+    """Walk file 0 of C3 with 1,000 random bits flipped inside the CRC and
+    Timestamp words of headers (core/header.go:9-16: bytes 0-7), which never
+    desynchronise the reader: every record is still replayed, the reject set
+    (core/db.go:311: ke.CRC != CalcCRC32(value)) is exactly the records whose
+    CRC word was flipped, the flipped timestamps read back as struct.unpack
+    of the flipped bytes, and everything else equals the oracle field for
+    field."""
+    import struct
+
+    kw = dict(bench.CONFIGS["c3"], n_files=1)
+    files, _ = orc.gen_corpus(**kw)
+    f = files[0]
+    clean, _ = orc.replay([f], [True])
+    assert clean["flags"].min() & 2, "the C3 spec has no corrupt values"
+    rng = np.random.default_rng(4242)
+    picks = rng.choice(len(clean), 1000, replace=False)
+    crc_hit, ts_hit = set(), set()
+    for i in picks:
+        o = int(clean[int(i)]["rec_off"])
+        byte = int(rng.integers(8))  # 0-3 CRC, 4-7 Timestamp
+        f[o + byte] ^= np.uint8(1 << int(rng.integers(8)))
+        (crc_hit if byte < 4 else ts_hit).add(int(i))
+    want, wst = orc.replay([f], [True])
+    assert wst["status"] == 0 and len(want) == len(clean)
+    assert np.array_equal(want["rec_off"], clean["rec_off"])
+    rejects = set(np.nonzero((want["flags"] & 2) == 0)[0].tolist())
+    assert rejects == crc_hit and len(crc_hit) > 400
+    with g.ReplayContext() as ctx:
+        ctx.load([f], [True])
+        for run in range(2):
+            ctx.run()
+            got, gst = ctx.fetch()
+            _same(got, gst, want, wst, f"c3 file 0 crc/ts flips run {run}")
+            assert set(np.nonzero((got["flags"] & 2) == 0)[0].tolist()) == crc_hit
+            fb = f.tobytes() if hasattr(f, "tobytes") else bytes(f)
+            for i in sorted(ts_hit)[:200] + sorted(crc_hit)[:200]:
+                o = int(got[i]["rec_off"])
+                crc, ts = struct.unpack_from("<II", fb, o)
+                assert int(got[i]["ts"]) == ts and int(got[i]["crc"]) == crc, i
+    print(f"c3 file 0: {len(crc_hit)} CRC-word and {len(ts_hit)} timestamp-word flips, "
+          f"{len(want)} records compared, reject set = CRC-flipped set")

@@ -125,10 +125,13 @@ def test_paths_more_files_than_descriptors(g, orc, tmp_path):
     reference's Walk opens one file at a time (internal/fs/disk.go:122-145)."""
     import resource
 
-    wf, reset = _corpus(orc, seed=97, n_files=1)
-    files = [wf[0][: (i % 7) * 900 + 200] for i in range(160)]  # prefixes: some end mid-record
+    wf, _ = _corpus(orc, seed=97, n_files=1, active=0)
+    recs, _ = orc.replay(wf[:1], [True])
+    ends = [int(o) for o in recs["rec_off"][1:40]]  # record boundaries: every file replays whole
+    files = [wf[0][: ends[(i * 7) % len(ends)]] for i in range(160)]
     reset = [True] * 159 + [False]
     want, wst = orc.replay(files, reset)
+    assert wst["status"] == 0 and len(want) > 160
     paths = _write(tmp_path, files)
     soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
     open_now = len(os.listdir("/proc/self/fd"))

@@ -26,11 +26,25 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
-def stats(L, which):
+def stats(L, which, waves_per_wg):
     buf = np.zeros(4 * 16384, dtype=np.uint64)
     assert L.gck_xp_clock_read(which, buf.ctypes.data_as(ctypes.c_void_p)) == 0
     s = buf.reshape(-1, 4).astype(np.float64)
-    s = s[(s[:, 1] > 0) & (s[:, 3] > s[:, 1])]
+    ok = (s[:, 1] > 0) & (s[:, 3] > s[:, 1])
+    wg = np.nonzero(ok)[0] // waves_per_wg
+    s = s[ok]
+    # wave end times from the first wave's start (us); per XCD (workgroups go
+    # round-robin over the 8 XCDs) the median end and the median clock
+    t0 = s[:, 1].min()
+    end = (s[:, 3] - t0) / 100.0
+    beg = (s[:, 1] - t0) / 100.0
+    xcd = wg % 8
+    ghz_all = (s[:, 2] - s[:, 0]) / (s[:, 3] - s[:, 1]) * 0.1
+    extra = dict(end_us_p10=round(float(np.percentile(end, 10)), 1), end_us_p50=round(float(np.median(end)), 1),
+                 end_us_p90=round(float(np.percentile(end, 90)), 1), end_us_p99=round(float(np.percentile(end, 99)), 1),
+                 start_us_p99=round(float(np.percentile(beg, 99)), 1),
+                 xcd_end_us_p50=[round(float(np.median(end[xcd == x])), 1) for x in range(8)],
+                 xcd_ghz=[round(float(np.median(ghz_all[xcd == x])), 3) for x in range(8)])
     dt, dr = s[:, 2] - s[:, 0], s[:, 3] - s[:, 1]
     ghz = dt / dr * 0.1  # real time ticks at 100 MHz
     wave_us = dr / 100.0
@@ -38,7 +52,7 @@ def stats(L, which):
                 clock_ghz_p10=round(float(np.percentile(ghz, 10)), 4),
                 clock_ghz_p90=round(float(np.percentile(ghz, 90)), 4),
                 wave_us_median=round(float(np.median(wave_us)), 1), wave_us_max=round(float(wave_us.max()), 1),
-                span_us=round(float((s[:, 3].max() - s[:, 1].min()) / 100.0), 1))
+                span_us=round(float((s[:, 3].max() - s[:, 1].min()) / 100.0), 1), **extra)
 
 
 def main():
@@ -71,7 +85,7 @@ def main():
     L.gck_xp_clock_reset()
     ctx.run()
     st = ctx.stats()
-    out["crc_rows"] = dict(stats(L, 0), warm_runs=n, kernel_ms=round(st["ms_crc_rows_sum"] - s0["ms_crc_rows_sum"], 4),
+    out["crc_rows"] = dict(stats(L, 0, 16), warm_runs=n, kernel_ms=round(st["ms_crc_rows_sum"] - s0["ms_crc_rows_sum"], 4),
                            step_ms=round(st["ms_total"], 3))
     # the stream read: back-to-back, then one stamped batch
     ms = ctypes.c_double()
@@ -82,7 +96,7 @@ def main():
     L.gck_xp_clock_stream(ctx._h, 1, ctypes.byref(ms))
     one = ms.value
     L.gck_xp_clock_stream(ctx._h, 20, ctypes.byref(ms))
-    out["stream_read"] = dict(stats(L, 1), kernel_ms=round(ms.value, 4), kernel_ms_stamped_launch=round(one, 4),
+    out["stream_read"] = dict(stats(L, 1, 4), kernel_ms=round(ms.value, 4), kernel_ms_stamped_launch=round(one, 4),
                               gbs=round(st["bytes"] / (ms.value * 1e-3) / 1e9, 1))
     print(json.dumps(out), flush=True)
     ctx.close()
