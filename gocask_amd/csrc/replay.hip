@@ -1011,14 +1011,17 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 // without a record end to an out-of-range offset, dropped), so the compiler's
 // vmcnt waits count the same stores on every path and stay a row behind the
 // loads.
-#define GCK_SPLAN 2
-#define GCK_EPACC 0
-#define GCK_ARENA_AUX kArenaAux
-constexpr int kPrefetch = 1;
-constexpr int kRowsPerStep = 1;
-template <int MODE, int NR>
+//
+// Codegen is part of the design here: this text compiles to round 2's
+// instruction stream (register arrays of one row, select-form captures, each
+// row's store before the next row's loads).  Round 3 rewrote it with scalar
+// registers and mask-form captures: the same work, the stores sunk behind the
+// next row's loads, and a tail of late wavefronts (clock stamps: last wave
+// 0.6 ms after the median against 0.13 now): 5.45-5.56 against 5.18-5.20 ms on
+// one box (profiles/r4f/ab_r2_head_port.log, profiles/r4a/bisect_r3_commits.log).
+// Compare the ISA (hipcc --cuda-device-only -S) before and after any edit.
+constexpr int kPrefetch = 1;  // steps between a row's loads and its processing (2, 3 measured slower)
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint4 *__restrict__ plan,
                                                    const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
@@ -1027,10 +1030,10 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    uint32_t *__restrict__ queue,
                                                    const uint64_t *__restrict__ rec_off,
                                                    const uint2 *__restrict__ rec_kv, uint64_t row0) {
-    static_assert(kBlockRows % (4 * NR) == 0, "a block is whole quads of steps");
+    constexpr int NR = 1;                     // rows per step (two measured slower: 5.70 vs 5.64 ms)
     constexpr int kSteps = kBlockRows / NR;  // steps per block
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
-    if constexpr ((MODE & 64) == 0) fill_crc_lds(lds, g_slice, g_nib);
+    fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
     static_assert(kNibBase * 4 == 0x20000, "shift-table addresses: byte 2 of the v_perm base");
     const uint32_t nbase = kNibBase * 4 + lane * 4;  // byte 0: the lane's bank, byte 2: the region
@@ -1063,7 +1066,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     // compute, a fully static split loses to the queue's balance (6.02 vs
     // 5.82 ms), half static / half queue is best (5.77).
     const uint32_t W = gridDim.x * kWaves, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWaves + (threadIdx.x >> 6)));
-    const uint32_t n_static = (MODE & 128) ? (uint32_t)((n_blocks + W - 1) / W) : (uint32_t)(n_blocks / W) * kStaticEighths / 8;
+    const uint32_t n_static = (uint32_t)(n_blocks / W) * kStaticEighths / 8;
     uint32_t st_k = 0;
     uint32_t last = kClaim - 1;
     auto grab = [&]() -> uint32_t {  // next block index
@@ -1078,31 +1081,20 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         return last;
     };
     struct Plan {
-#if !GCK_SPLAN
-        uint4 a, b;  // the lane's 64 row nibbles
-#endif
-        uint32_t ra; // row_first of row lane
-        uint32_t re; // row_first of the block's end (GCK_SPLAN)
+        uint32_t ra;  // row_first of row `lane` of the block
+        uint32_t re;  // row_first of the block's end
     };
     auto load_plan = [&](uint64_t q, Plan &p) {
         const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
-#if !GCK_SPLAN
-        const uint4 *src = plan + qc * (kBlockRows * kPlanLaneBytes / 16) + lane * 2;
-        p.a = src[0];
-        p.b = src[1];
-#else
         p.re = row_first[min(qc * kBlockRows + kBlockRows, n_rows)];
-#endif
         p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
     };
-#if GCK_SPLAN
-    // The block's plan nibbles from its record ends (records [ra0, re) end in
-    // its rows, in offset order), instead of k_row_plan's dense 32 B per row:
-    // a lane per record computes (row, slab, block) of its last byte, then a
-    // uniform loop hands each end to the slab's lane (nibble dword chosen by
-    // a uniform index).
-    // GCK_SPLAN 2: the first 64 record ends of a block are loaded one block
-    // ahead (Batch); later ones (blocks with more than 64 ends) on the spot
+    // The block's nibbles from its record ends (records [ra0, re) end in its
+    // rows, in offset order): a lane per record computes (row, slab, block) of
+    // its last byte, then a uniform loop hands each end to the slab's lane
+    // (nibble dword chosen by a uniform index).  The first 64 record ends of a
+    // block are loaded one block ahead (Batch); later ones (blocks with more
+    // than 64 ends) on the spot.
     struct Batch {
         uint64_t off;
         uint2 kv;
@@ -1144,30 +1136,18 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             }
         }
     };
-#endif
     struct RowBuf {
         u32x4 x[4];
     };
     auto issue = [&](uint64_t row0, RowBuf (&bs)[NR]) {
-        if constexpr ((MODE & 8) != 0) return;
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             // 32-bit row index (rows < 2^32): the clamp stays on the scalar unit
             const uint32_t r = min((uint32_t)(row0 + i), (uint32_t)(n_rows - 1));
             const __amdgpu_buffer_rsrc_t rrow = make_rsrc(arena + (uint64_t)r * kRow, kRow);
-            constexpr int kAux = (MODE & 32) ? 0 : GCK_ARENA_AUX;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kAux);
+            for (int k = 0; k < 4; ++k) bs[i].x[k] = __builtin_amdgcn_raw_buffer_load_b128(rrow, s_rel + 1024 * k, 0, kArenaAux);
         }
-    };
-    // GCK_EPACC: (c, pre) of consecutive record slots gathered in two
-    // registers (lane l = slot acc_base + l) and stored 64 at a time, at the
-    // block end or when full, instead of one 64-lane store per row
-    uint32_t acc_c = 0, acc_p = 0, acc_n = 0, acc_base = 0;
-    auto acc_flush = [&]() {
-        store_ep(lane < acc_n ? (acc_base + lane - ra0) * 8u : kDrop, acc_c, acc_p);
-        acc_base += acc_n;
-        acc_n = 0;
     };
     // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
     // nib holds their plan nibbles from bit 0 up
@@ -1206,10 +1186,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                     w[i][4 * (k + 1) + c] = r[1];
                 }
             }
-            if constexpr ((MODE & 8) != 0) {
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[i][j] = (uint32_t)(row0 + i) * 2654435761u + lane * 97u + j;
-            }
         }
         // NR independent chains interleaved: NR table reads in flight per step
         uint32_t a[NR], c1[NR], c2[NR], c3[NR], G[NR];
@@ -1220,13 +1196,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
                 const uint32_t nx = j < 15 ? w[i][j < 15 ? j + 1 : 15] : 0u;
-                if constexpr ((MODE & 2) != 0) {
-                    a[i] = (__builtin_amdgcn_alignbit(a[i], a[i], 5) + 0x9E3779B9u) ^ nx;
-                    if (j == 3) c1[i] = a[i];
-                    if (j == 7) c2[i] = a[i];
-                    if (j == 11) c3[i] = a[i];
-                    if (j == 15) G[i] = a[i];
-                } else if (j == 15) {
+                if (j == 15) {
                     G[i] = slice4x(lds, lb0, lb1, a[i], 0u);
                 } else if ((j & 3) == 3) {
                     const uint32_t c = slice4x(lds, lb0, lb1, a[i], 0u);
@@ -1249,41 +1219,32 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         uint32_t P[NR], pre[NR];
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
-            if constexpr ((MODE & 4) == 0) {
-                // (x & m) | q in one v_bitop3_b32 (truth table 0xEA; the two
-                // constants live in registers set up outside the loop)
-                const uint32_t ge = __builtin_amdgcn_bitop3_b32(G[i], 0x0F0F0F0Fu, 0x60402000u, 0xEA);
-                const uint32_t go = __builtin_amdgcn_bitop3_b32(G[i] >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
-                uint32_t t[8];
+            // (x & m) | q in one v_bitop3_b32 (truth table 0xEA; the two
+            // constants live in registers set up outside the loop)
+            const uint32_t ge = __builtin_amdgcn_bitop3_b32(G[i], 0x0F0F0F0Fu, 0x60402000u, 0xEA);
+            const uint32_t go = __builtin_amdgcn_bitop3_b32(G[i] >> 4, 0x0F0F0F0Fu, 0x70503010u, 0xEA);
+            uint32_t t[8];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    t[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
-                    t[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
-                }
-                P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
-            } else {
-                P[i] = G[i];
+            for (int k = 0; k < 4; ++k) {
+                t[2 * k] = lds_at(lds, __builtin_amdgcn_perm(ge, nbase, 0x0C020000u | ((4u + k) << 8)));
+                t[2 * k + 1] = lds_at(lds, __builtin_amdgcn_perm(go, nbase, 0x0C020000u | ((4u + k) << 8)));
             }
+            P[i] = xor3(xor3(t[0], t[1], t[2]), xor3(t[3], t[4], t[5]), t[6] ^ t[7]);
         }
-        if constexpr ((MODE & 4) == 0) {
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);  // row_shr:1
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x111, 0xF>(P[i]);  // row_shr:1
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);  // row_shr:2
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x112, 0xF>(P[i]);  // row_shr:2
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);  // row_shr:4
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x114, 0xF>(P[i]);  // row_shr:4
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);  // row_shr:8
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x118, 0xF>(P[i]);  // row_shr:8
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);  // row_bcast:15 -> rows 1, 3
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x142, 0xA>(P[i]);  // row_bcast:15 -> rows 1, 3
 #pragma unroll
-            for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);  // row_bcast:31 -> rows 2, 3
+        for (int i = 0; i < NR; ++i) P[i] ^= dpp<0x143, 0xC>(P[i]);  // row_bcast:31 -> rows 2, 3
 #pragma unroll
-            for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);  // wave_shr:1 -> exclusive (lane 0: 0)
-        } else {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) pre[i] = 0;
-        }
+        for (int i = 0; i < NR; ++i) pre[i] = dpp<0x138, 0xF>(P[i]);  // wave_shr:1 -> exclusive (lane 0: 0)
 #pragma unroll
         for (int i = 0; i < NR; ++i) {
             const uint32_t j = j0 + i;
@@ -1297,39 +1258,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 v = b == 1 ? c1[i] : v;
                 return b == 0 ? 0u : v;
             };
-            if constexpr ((MODE & 16) != 0) {
-                asm volatile("" ::"v"(m), "v"(pre[i]), "v"(c1[i]), "v"(c2[i]), "v"(c3[i]), "v"(ra));
-            } else if (GCK_EPACC) {
-                // the row's ends in slot order (lane, then block), each into
-                // lane acc_n of the accumulator: a uniform loop over the
-                // lanes with ends (about 1.2 per row on C3)
-                (void)ra;
-                // each lane's first end's capture, selected on the vector unit
-                const uint32_t cap0 = cap((uint32_t)__builtin_ctz(m | 16u));
-                auto push = [&](uint32_t cv, uint32_t pv) {
-                    if (acc_n == 64) acc_flush();
-                    acc_c = lane == acc_n ? cv : acc_c;
-                    acc_p = lane == acc_n ? pv : acc_p;
-                    ++acc_n;
-                };
-                uint64_t C = __ballot(m != 0);
-                while (C) {
-                    const int L = __builtin_ctzll(C);
-                    C &= C - 1;
-                    const uint32_t mL = (uint32_t)__builtin_amdgcn_readlane((int)m, L);
-                    const uint32_t pv = (uint32_t)__builtin_amdgcn_readlane((int)pre[i], L);
-                    push((uint32_t)__builtin_amdgcn_readlane((int)cap0, L), pv);
-                    if (mL & (mL - 1)) {  // rare: a slab with 2..4 ends (records under 64 B)
-                        const uint32_t v1 = (uint32_t)__builtin_amdgcn_readlane((int)c1[i], L);
-                        const uint32_t v2 = (uint32_t)__builtin_amdgcn_readlane((int)c2[i], L);
-                        const uint32_t v3 = (uint32_t)__builtin_amdgcn_readlane((int)c3[i], L);
-                        for (uint32_t mm = mL & (mL - 1); mm; mm &= mm - 1) {
-                            const uint32_t b = (uint32_t)__builtin_ctz(mm);
-                            push(b == 1 ? v1 : b == 2 ? v2 : v3, pv);
-                        }
-                    }
-                }
-            } else if (__ballot(m & (m - 1)) == 0) {
+            if (__ballot(m & (m - 1)) == 0) {
                 // common case: at most one record end per slab, its slot is
                 // ra + (cut lanes before)
                 const uint64_t C = __ballot(m != 0);
@@ -1363,11 +1292,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     uint64_t qn = grab();
     Plan pc, pn;
     load_plan(q, pc);
-#if GCK_SPLAN == 2
     Batch bc, bn;
     load_plan(qn, pn);
     load_batch(pc, bc);
-#endif
     // kPrefetch rows in flight per wavefront (row buffers rotate with period
     // NB, which divides the 4 steps of a quad, so every buffer has fixed
     // registers)
@@ -1379,34 +1306,18 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     for (;;) {
         // block q: plan pc is resident; fetch the next block's plan and claim
         // the one after it (both land during this block)
-#if GCK_SPLAN == 2
         // pn (block qn) landed during the previous block: its record ends now,
         // the plan of the block after it next
         const uint64_t qnn = grab();
         Plan pnn;
         load_batch(pn, bn);
         load_plan(qnn, pnn);
-#else
-        load_plan(qn, pn);
-        const uint64_t qnn = grab();
-#endif
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
-        acc_base = ra0;
-        acc_n = 0;
-#if !GCK_SPLAN
-        const uint32_t nibs[8] = {pc.a.x, pc.a.y, pc.a.z, pc.a.w, pc.b.x, pc.b.y, pc.b.z, pc.b.w};
-#else
         uint32_t nibs[8];
-#if GCK_SPLAN == 2
         build_nibs(row_b, ra0, pc.re, &bc, nibs);
-#else
-        (void)load_batch;
-        build_nibs(row_b, ra0, pc.re, nullptr, nibs);
-#endif
-#endif
         // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
         // lane; the two row buffers alternate, so each has fixed registers
         for (int qd = 0; qd < kSteps / 4; ++qd) {
@@ -1433,7 +1344,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                         rend_buf);
             }
         }
-        if (GCK_EPACC) acc_flush();
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
         *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
@@ -1444,16 +1354,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         q = qn;
         qn = qnn;
         pc = pn;
-#if GCK_SPLAN == 2
         pn = pnn;
         bc = bn;
-#endif
     }
 }
 
-#undef GCK_SPLAN
-#undef GCK_EPACC
-#undef GCK_ARENA_AUX
 
 // ---------------------------------------------------------------- finalize ---
 // Per record r = [rs, ve) (core/db.go:311 applied to every record).  Notation
@@ -2149,8 +2054,8 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_crc_rows<0, kRowsPerStep><<<grid, 1024, 0, s>>>(
-        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, nullptr, c->d_row_first.as<uint32_t>() + r0, cap,
+    k_crc_rows<<<grid, 1024, 0, s>>>(
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0);
     return GCK_OK;
