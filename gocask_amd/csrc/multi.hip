@@ -397,7 +397,10 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
     if (!rc) {
         std::unique_lock<std::mutex> lk;
         if (need_rccl) lk = std::unique_lock<std::mutex>(*cset.mu);
-        const Rccl &R = rccl();
+        // RCCL only when a pair crosses devices: loading librccl registers its
+        // kernels, 1.1-4.7 s of a one-device call (GCK_REPLAY_TRACE, round 4)
+        static const Rccl kNone{};
+        const Rccl &R = need_rccl ? rccl() : kNone;
         bool grouped = false;
         ncclResult_t r = ncclSuccess;
         for (uint32_t i = 0; i < nsrc && !rc && r == ncclSuccess; ++i) {
@@ -415,9 +418,14 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
                 ko += nk;
                 if (devs[s] == devs[p] && !rccl_self) {
                     (void)hipSetDevice(devs[p]);
+                    const auto tc = std::chrono::steady_clock::now();
                     if ((ne && hipMemcpyAsync(re, se, ne * sizeof(gck_kd_entry), hipMemcpyDeviceToDevice, sp) != hipSuccess) ||
                         (nk && hipMemcpyAsync(rk, sk, nk, hipMemcpyDeviceToDevice, sp) != hipSuccess))
                         rc = GCK_EDEVICE;
+                    if (trace)
+                        fprintf(stderr, "gck_replay_multi copy src %u -> owner %u: %llu entries, %llu key bytes, %.2f ms\n", i, p,
+                                (unsigned long long)ne, (unsigned long long)nk,
+                                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count());
                     continue;
                 }
                 if (!grouped) {
@@ -443,6 +451,7 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
             set_error(R.err ? R.err(r) : "rccl", hipErrorUnknown, __FILE__, __LINE__);
             rc = GCK_EDEVICE;
         }
+        mark("exch issued");
         // the exchange is complete (and the communicators free for another
         // call) once every owner's stream is
         for (uint32_t p = 0; p < ndev; ++p) {

@@ -39,6 +39,8 @@ try:
              dict(SHIM_PATHS="1", SHIM_MULTI="1")]
     if len(sys.argv) > 2:
         modes = modes[:int(sys.argv[2])]
+    if os.environ.get("SHIM_MODES"):  # e.g. "0 4": by path, single and multi
+        modes = [modes[int(i)] for i in os.environ["SHIM_MODES"].split()]
     # SHIM_THREADS="4 8 16": the by-path / pageable modes at each copy-thread count
     threads = os.environ.get("SHIM_THREADS", "").split()
     if threads:
