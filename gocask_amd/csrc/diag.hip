@@ -137,9 +137,70 @@ __global__ __launch_bounds__(256) void k_chase(const uint8_t *__restrict__ arena
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// Window probe for a walk that reads W = 16 LPC bytes per round trip: 65,536
+// dependent chains (k_walk's concurrency), LPC lanes per chain each loading
+// 16 B of the chain's window; the next address depends on the whole window
+// (an XOR over the chain's lanes).  hops = round trips per chain.
+template <int LPC>
+__global__ __launch_bounds__(256) void k_chase_win(const uint8_t *__restrict__ arena, uint64_t len, uint32_t hops,
+                                                   uint32_t *sink) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x, chain = t / LPC, sub = t % LPC;
+    const uint64_t n16 = (len >> 4) - 64;
+    auto pick = [&](uint64_t v) {
+        v = (v ^ (v >> 31)) * 0xBF58476D1CE4E5B9ull;
+        v ^= v >> 29;
+        return (((v & 0xFFFFFFFFull) * n16) >> 32) << 4;
+    };
+    const uint64_t x = 0x9E3779B97F4A7C15ull * (chain + 1);
+    uint32_t acc = 0;
+    uint64_t o = pick(x);
+    for (uint32_t h = 0; h < hops; ++h) {
+        const uint4 a = *reinterpret_cast<const uint4 *>(arena + o + 16 * sub);
+        uint32_t v = a.x ^ a.y ^ a.z ^ a.w;
+#pragma unroll
+        for (int m = 1; m < LPC; m <<= 1) v ^= (uint32_t)__shfl_xor((int)v, m);
+        acc += v;
+        o = pick(x + acc + h);
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
 }  // namespace gck
 
 using namespace gck;
+
+// Window probes: k_chase_win<lpc> with `hops` round trips per chain.
+extern "C" int gck_diag_chase_win(gck_ctx *ctx, int lpc, uint32_t hops, int iters, double *ms_per_iter) {
+    if (!ctx || iters <= 0 || !(lpc == 1 || lpc == 4 || lpc == 8 || lpc == 16 || lpc == 32)) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    if (!c->n_rows) return GCK_EINVAL;
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    const uint32_t threads = 65536u * (uint32_t)lpc, grid = threads / 256;
+    auto launch = [&]() {
+        uint8_t *a = c->arena.as<uint8_t>();
+        const uint64_t n = c->arena_len;
+        if (lpc == 1) k_chase_win<1><<<grid, 256, 0, c->stream>>>(a, n, hops, sink);
+        else if (lpc == 4) k_chase_win<4><<<grid, 256, 0, c->stream>>>(a, n, hops, sink);
+        else if (lpc == 8) k_chase_win<8><<<grid, 256, 0, c->stream>>>(a, n, hops, sink);
+        else if (lpc == 16) k_chase_win<16><<<grid, 256, 0, c->stream>>>(a, n, hops, sink);
+        else k_chase_win<32><<<grid, 256, 0, c->stream>>>(a, n, hops, sink);
+    };
+    hipEvent_t e0, e1;
+    GCK_HIP(hipEventCreate(&e0));
+    GCK_HIP(hipEventCreate(&e1));
+    launch();
+    GCK_HIP(hipEventRecord(e0, c->stream));
+    for (int i = 0; i < iters; ++i) launch();
+    GCK_HIP(hipEventRecord(e1, c->stream));
+    GCK_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    *ms_per_iter = ms / iters;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return GCK_OK;
+}
 
 // pattern 0: k_stream_read; 15: the same with non-temporal loads; 1: k_stream_rows<SLAB>; 2: k_stream_rows<coalesced>;
 // 16: k_stream_rows_nt, rows strided over the wavefronts; 17: the same in 64-row blocks;

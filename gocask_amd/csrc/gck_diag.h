@@ -20,6 +20,9 @@ int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *g
  * coalesced, 16 / 17 = k_crc_rows' row geometry without compute, 3..14 =
  * random-access probes. */
 int gck_diag_stream_pattern(gck_ctx *ctx, int pattern, int iters, double *ms_per_iter, double *gbs);
+/* 65,536 dependent chains reading 16 x lpc bytes per round trip (lpc lanes per
+ * chain), hops round trips each: the cost of a windowed header walk. */
+int gck_diag_chase_win(gck_ctx *ctx, int lpc, uint32_t hops, int iters, double *ms_per_iter);
 /* Per-chunk chain length (records k_walk staged) and final entry of the last
  * run; count / entry NULL: *n = chunks only. */
 int gck_diag_chunks(gck_ctx *ctx, uint32_t *count, uint64_t *entry, uint64_t cap, uint64_t *n);
