@@ -429,7 +429,11 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
                                                   const uint32_t *__restrict__ ch_term,
                                                   const uint32_t *__restrict__ f_first_chunk,
                                                   uint32_t *__restrict__ ch_bad, uint32_t *counter,
-                                                  uint32_t c_begin, uint32_t c_end) {
+                                                  uint32_t c_begin, uint32_t c_end,
+                                                  const uint32_t *__restrict__ prev_counter) {
+    // a round after one that found every chunk consistent (so its fixup
+    // changed nothing) finds the same: its counter stays at the run's zero
+    if (prev_counter && *prev_counter == 0) return;
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
@@ -463,7 +467,8 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                                                uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
                                                uint64_t *ch_tpos, uint64_t *ch_wend, uint2 *s_kv,
                                                uint32_t cap, uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end,
-                                               uint32_t *counter) {
+                                               uint32_t *counter, const uint32_t *__restrict__ bad_counter) {
+    if (bad_counter && *bad_counter == 0) return;  // nothing to fix (the common case)
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end || !ch_bad[c]) return;
     const uint32_t f = ch_file[c], fc = f_first_chunk[f];
@@ -1972,14 +1977,14 @@ static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + p
 enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
 constexpr int kRounds = 2;             // device validation/fixup rounds
 
-static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1) {
+static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, const uint32_t *bad_cnt = nullptr) {
     k_fixup<<<nblk(c1 - c0, 256), 256, 0, s>>>(
         c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
         c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
         c->d_ch_entry.as<uint64_t>(), c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(),
         c->d_stage.as<uint2>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
-        c->d_counters.as<uint32_t>() + CNT_FIXUP);
+        c->d_counters.as<uint32_t>() + CNT_FIXUP, bad_cnt);
 }
 
 // Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
@@ -2001,9 +2006,10 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
                                                 c->d_ch_term.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
-                                                c->d_ch_bad.as<uint32_t>(), val_cnt + r, c0, c1);
+                                                c->d_ch_bad.as<uint32_t>(), val_cnt + r, c0, c1,
+                                                r ? val_cnt + r - 1 : nullptr);
         if (r == kRounds) break;
-        launch_fixup(c, s, c0, c1);
+        launch_fixup(c, s, c0, c1, val_cnt + r);
     }
 }
 
@@ -2167,7 +2173,7 @@ static int ctx_run_host(Ctx *c) {
         k_validate<<<nblk(nc, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                  c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
                                                  c->d_ch_term.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
-                                                 c->d_ch_bad.as<uint32_t>(), cnt + CNT_HOSTVAL, 0u, nc);
+                                                 c->d_ch_bad.as<uint32_t>(), cnt + CNT_HOSTVAL, 0u, nc, nullptr);
         uint32_t v = 0;
         GCK_HIP(hipMemcpyAsync(&v, cnt + CNT_HOSTVAL, 4, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipStreamSynchronize(s));

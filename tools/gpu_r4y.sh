@@ -1,7 +1,7 @@
 set -o pipefail
 out=gpurun_out/r4y
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_encode_batch.py tests/test_gpu_fuzz.py tests/test_gpu_parity.py tests/test_gpu_ring.py -m gpu -x -q --timeout 400 --timeout-method thread > $out/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?
 tail -3 $out/pytest.log
 [ $rc -ne 0 ] && exit $rc
