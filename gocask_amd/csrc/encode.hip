@@ -388,6 +388,18 @@ __device__ __forceinline__ uint4 load16u(const uint8_t *src) {
                       __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
 }
 
+// 16 bytes to any byte address: one dwordx4 store (gfx9 global stores need no
+// alignment; the amdhsa target compiles a 1-byte-aligned vector access to it).
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void store16u(uint8_t *dst, uint4 v) {
+    u32x4_a1 x;
+    x.x = v.x;
+    x.y = v.y;
+    x.z = v.z;
+    x.w = v.w;
+    *reinterpret_cast<u32x4_a1 *>(dst) = x;
+}
+
 __device__ __forceinline__ CrcTabs &enc_tabs() {
     __shared__ CrcTabs t;
     return t;
@@ -411,7 +423,6 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0 = 0, lb1 = 0, kl_shift = 0;
     CrcTabs *T = &enc_tabs();
-    const uint64_t key_total = key_off[n], val_total = val_off[n];  // blob sizes (readable + 4 bytes)
     // the slicing tables, built here (no context): T0..T3 into Zs, expanded
     // into the conflict-free image, then Zs itself
     {
@@ -473,7 +484,18 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
             if ((todo >> lane) & 1) crc = c;
         }
         const uint32_t h1 = t, h2 = del ? 0u : (uint32_t)kl, h3 = (uint32_t)(del ? kl : vl);
-        // 3. the group's output, 1 KiB rows of 16 B chunks
+        // 3. the group's output.  (a) The 16 B chunks of the output that lie
+        // wholly inside one record's value, 1 KiB rows of them: aligned 16 B
+        // stores.  (b) A lane per record: its header, its key and the value
+        // bytes (a) leaves out, as whole 16 B pieces at any alignment, each
+        // inside the record.  A piece that ends at the end of a region and
+        // starts before the region (a key or value shorter than 16 B) carries
+        // wrong bytes in front; the lane writes the pieces from the record's
+        // end back to its header, so its later stores overwrite them (one
+        // thread's stores to one address land in program order).  Bytes
+        // written by both (a) and (b) are the same value bytes.
+        const uint64_t vsx = oo + 16 + kl, vex = vsx + vl;  // the value's output range
+        const uint64_t vsrc = vo - vsx;                      // value byte of output X: vals + vsrc + X
         uint32_t rr = 0;  // first record overlapping the row (wave-uniform)
         for (uint64_t R = O0 & ~15ull; R < O1; R += 1024) {
             const uint64_t X = R + 16ull * lane;
@@ -486,98 +508,43 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
                 if (X >= sk) r = k;
             }
             rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
-            // (uniform) the whole row inside one record's value: most rows
-            // of large records; its fields by readlane, no permutes
-            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr && R + 1024 <= O1) {
-                const int src = (int)rr;
-                const uint64_t s0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oo >> 32), src) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oo, src);
-                const uint64_t kl0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(kl >> 32), src) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kl, src);
-                const uint64_t vl0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(vl >> 32), src) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vl, src);
-                const uint64_t vs0 = s0 + 16 + kl0;  // the value's first output byte
-                if (R >= vs0 && R + 1024 <= vs0 + vl0) {
-                    const uint64_t vo0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(vo >> 32), src) << 32) |
-                                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)vo, src);
-                    const uint4 v = load16u(vals + vo0 + (X - vs0));
-                    *reinterpret_cast<uint4 *>(out + X) = v;
+            uint64_t a, b, d;  // the chunk's record: value range [a, b), source offset d
+            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr) {  // (uniform) one record: readlane
+                a = lane_u64(vsx, (int)rr);
+                b = lane_u64(vex, (int)rr);
+                d = lane_u64(vsrc, (int)rr);
+                if (R >= a && R + 1024 <= b) {  // the whole row inside the value: most rows of large records
+                    *reinterpret_cast<uint4 *>(out + X) = load16u(vals + d + X);
                     continue;
                 }
+            } else {
+                a = __shfl(vsx, (int)r);
+                b = __shfl(vex, (int)r);
+                d = __shfl(vsrc, (int)r);
             }
-            // at most two records meet in a chunk: r, and r + 1 from its end on
-            uint32_t w[4] = {0u, 0u, 0u, 0u};
-            uint32_t mask = 0;  // bytes of the chunk written from this group's records
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int src = (int)min<uint32_t>(r + j, cnt - 1);
-                const uint64_t s = __shfl(oo, src), k_o = __shfl(ko, src), k_l = __shfl(kl, src);
-                const uint64_t v_o = __shfl(vo, src), v_l = __shfl(vl, src);
-                const uint32_t hv[4] = {(uint32_t)__shfl((int)crc, src), (uint32_t)__shfl((int)h1, src),
-                                        (uint32_t)__shfl((int)h2, src), (uint32_t)__shfl((int)h3, src)};
-                const bool use = r + j < cnt && X < O1;
-                const uint64_t e = s + 16 + k_l + v_l;
-                const uint64_t b0 = max(X, s), b1 = min(X + 16, e);
-                if (!use || b0 >= b1) continue;
-                const uint8_t *kp = keys + k_o, *vp = vals + v_o;
-                const uint64_t q0 = b0 - s;
-                if (b0 == X && b1 == X + 16 && q0 >= 16 && (q0 + 16 <= 16 + k_l || q0 >= 16 + k_l)) {
-                    // the whole chunk inside the key or inside the value
-                    const uint4 v = load16u(q0 >= 16 + k_l ? vp + (q0 - 16 - k_l) : kp + (q0 - 16));
-                    w[0] = v.x;
-                    w[1] = v.y;
-                    w[2] = v.z;
-                    w[3] = v.w;
-                    mask = 0xFFFFu;
+            if (X >= a && X + 16 <= b) *reinterpret_cast<uint4 *>(out + X) = load16u(vals + d + X);
+        }
+        if (have) {
+            // (b), from the record's end back: the value's last and first 16
+            // bytes (the chunks between them are (a)'s), the key, the header
+            if (vl >= 16) {
+                store16u(out + vex - 16, load16u(vals + vo + vl - 16));
+                store16u(out + vsx, load16u(vals + vo));
+            } else if (vl && vo + vl >= 16) {  // reaches back into the key / header
+                store16u(out + vex - 16, load16u(vals + vo + vl - 16));
+            } else {
+                for (uint32_t i = 0; i < (uint32_t)vl; ++i) out[vsx + i] = vals[vo + i];  // (the blob's first bytes)
+            }
+            const uint64_t ks = oo + 16;
+            if (kl & 15) {
+                if (ko + kl >= 16) {
+                    store16u(out + ks + kl - 16, load16u(keys + ko + kl - 16));
                 } else {
-                    // byte by byte.  The key / value bytes come from 16 B
-                    // windows aligned to the chunk (chunk byte i = key byte
-                    // kst + i, value byte vst + i: one unaligned load each
-                    // instead of 16 byte loads); where a window would leave
-                    // its blob (the batch's first and last records), from byte
-                    // loads clamped into the key / value
-                    uint32_t by[16];
-                    const int64_t kst = (int64_t)(X - s) - 16, vst = kst - (int64_t)k_l;
-                    const bool need_k = k_l && b0 < s + 16 + k_l && b1 > s + 16;
-                    const bool need_v = v_l && b1 > s + 16 + k_l;
-                    const bool win = (!need_k || ((int64_t)k_o + kst >= 0 && k_o + kst + 16 <= key_total)) &&
-                                     (!need_v || ((int64_t)v_o + vst >= 0 && v_o + vst + 16 <= val_total));
-                    if (win) {
-                        const uint4 kw = need_k ? load16u(kp + kst) : make_uint4(0, 0, 0, 0);
-                        const uint4 vw = need_v ? load16u(vp + vst) : make_uint4(0, 0, 0, 0);
-                        const uint32_t kd[4] = {kw.x, kw.y, kw.z, kw.w}, vd[4] = {vw.x, vw.y, vw.z, vw.w};
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const uint64_t q = X + i - s;
-                            by[i] = ((q < 16 + k_l || v_l == 0) ? kd[i >> 2] : vd[i >> 2]) >> (8 * (i & 3)) & 0xFFu;
-                        }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 16; ++i) {
-                            const uint64_t q = X + i - s;  // may be past the record: clamped, unused
-                            const bool in_key = q < 16 + k_l || v_l == 0;
-                            const uint64_t kq = q < 16 ? 0 : min(q - 16, k_l - 1);
-                            const uint64_t vq = q < 16 + k_l ? 0 : min(q - 16 - k_l, v_l - 1);
-                            by[i] = in_key ? kp[kq] : vp[vq];
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const uint64_t b = X + i;
-                        if (b < b0 || b >= b1) continue;
-                        const uint64_t q = b - s;
-                        const uint32_t v = q < 16 ? (hv[q >> 2] >> (8 * (q & 3))) & 0xFFu : by[i];
-                        w[i >> 2] |= v << (8 * (i & 3));
-                        mask |= 1u << i;
-                    }
+                    for (uint32_t i = 0; i < (uint32_t)kl; ++i) out[ks + i] = keys[ko + i];
                 }
             }
-            if (mask == 0xFFFFu) {
-                *reinterpret_cast<uint4 *>(out + X) = make_uint4(w[0], w[1], w[2], w[3]);
-            } else if (mask) {  // the group's first or last chunk: its bytes only
-                for (uint32_t i = 0; i < 16; ++i)
-                    if ((mask >> i) & 1) out[X + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-            }
+            for (uint64_t i = 0; i + 16 <= kl; i += 16) store16u(out + ks + i, load16u(keys + ko + i));
+            store16u(out + oo, make_uint4(crc, h1, h2, h3));
         }
     }
     }

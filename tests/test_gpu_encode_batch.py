@@ -121,3 +121,26 @@ def test_encode_batch_exact_size_and_alignment():
     assert rc == _lib.GCK_EINVAL
     rc, _ = _raw_encode(dev(keys), d_koff, dev(vals, 3), d_voff, ts, tomb, out, out_off)
     assert rc == _lib.GCK_EINVAL
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_encode_batch_piece_edges(seed):
+    """Key and value lengths around the 16 B pieces and 1 KiB rows of the
+    copy (a region shorter than a piece, exactly one or two pieces, one byte
+    over), tombstones with long keys, and the batch's first records, whose
+    short keys and values are copied byte by byte (no 16 B before them in the
+    blob)."""
+    from gocask_amd import core
+
+    rng = random.Random(seed)
+    klens = [1, 2, 15, 16, 17, 31, 32, 33, 48, 100]
+    vlens = [0, 1, 2, 15, 16, 17, 31, 32, 33, 1007, 1008, 1023, 1024, 1025, 2048]
+    ops = [(1, b"a", b"b"), (2, b"cd", b""), (3, b"e" * 15, b"f" * 3)]
+    for i in range(3000):
+        k = rng.randbytes(rng.choice(klens))
+        if rng.random() < 0.1:
+            ops.append((100 + i, k, None))
+        else:
+            ops.append((100 + i, k, rng.randbytes(rng.choice(vlens + [rng.randint(0, 5000)]))))
+    out, off = core.encode_batch(ops)
+    assert bytes(out.cpu().numpy()) == _expected(ops)
