@@ -405,12 +405,12 @@ __device__ __forceinline__ CrcTabs &enc_tabs() {
     return t;
 }
 // Per group of 64 records: the payload CRCs (the LDS tables, 1024-thread
-// workgroups), then the group's output bytes, the headers taking the CRCs
-// from registers and the copy re-reading the payload bytes from L2 right
-// after the CRC pass read them from HBM (the stripe loads keep the default
-// cache policy here).  Two kernels -- CRCs into a table, then a copy pass
-// with more wavefronts per CU and no LDS -- took 0.48 + 0.87 ms for 1 GB
-// against 1.23 ms (kernel trace, profiles/r3q).
+// workgroups), a payload larger than kLaneMax copied to the output from the
+// stripe registers of its CRC (gck_crc_wave.h fold_stripe<true>: no second
+// read), then a lane per record writes its header (the CRC from a register),
+// key and the rest of a small payload as 16 B pieces.  Round 3's copy pass
+// over 1 KiB output rows re-read the payloads from L2 and assembled the rows
+// holding record boundaries byte by byte: 1.22 ms per GB against 0.77.
 __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict__ keys,
                                                        const uint64_t *__restrict__ key_off,
                                                        const uint8_t *__restrict__ vals,
@@ -464,7 +464,6 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         const uint64_t vo = have ? val_off[mine] : 0, vl = have && !del ? val_off[mine + 1] - vo : 0;
         const uint32_t t = have ? ts[mine] : 0u;
         const uint64_t oo = have ? out_off[mine] : 0;
-        const uint64_t O0 = __shfl(oo, 0), O1 = out_off[g0 + cnt];  // the group's output range
         // 2. CRCs: a lane per small payload (and per payload at its blob's
         // first 16 bytes: the stripe reads may reach 15 bytes before it),
         // the wavefront for the rest
@@ -478,57 +477,31 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         }
         const uint64_t todo = __ballot(have && !small);
         if (todo) {
-            const uint32_t c = wave_crcs<false>(
+            // the payload's copy from the stripe registers: out + ps
+            const uint64_t ps = oo + 16 + (del ? 0 : kl);
+            const uint32_t c = wave_crcs<false, true>(
                 todo, [&](int it) { return (lane_u32(del, it) ? keys : vals) + lane_u64(po, it); }, L, *T, lb0,
-                lb1, [&](uint32_t A) { return lanes_combine_gmul(kl_shift, A); });
+                lb1, [&](uint32_t A) { return lanes_combine_gmul(kl_shift, A); },
+                [&](int it) { return out + lane_u64(ps, it); });
             if ((todo >> lane) & 1) crc = c;
         }
         const uint32_t h1 = t, h2 = del ? 0u : (uint32_t)kl, h3 = (uint32_t)(del ? kl : vl);
-        // 3. the group's output.  (a) The 16 B chunks of the output that lie
-        // wholly inside one record's value, 1 KiB rows of them: aligned 16 B
-        // stores.  (b) A lane per record: its header, its key and the value
-        // bytes (a) leaves out, as whole 16 B pieces at any alignment, each
-        // inside the record.  A piece that ends at the end of a region and
-        // starts before the region (a key or value shorter than 16 B) carries
-        // wrong bytes in front; the lane writes the pieces from the record's
-        // end back to its header, so its later stores overwrite them (one
-        // thread's stores to one address land in program order).  Bytes
-        // written by both (a) and (b) are the same value bytes.
-        const uint64_t vsx = oo + 16 + kl, vex = vsx + vl;  // the value's output range
-        const uint64_t vsrc = vo - vsx;                      // value byte of output X: vals + vsrc + X
-        uint32_t rr = 0;  // first record overlapping the row (wave-uniform)
-        for (uint64_t R = O0 & ~15ull; R < O1; R += 1024) {
-            const uint64_t X = R + 16ull * lane;
-            // the record holding X (the group's first for chunks before O0)
-            uint32_t r = rr;
-            for (uint32_t k = rr + 1; k < cnt; ++k) {  // k wave-uniform: readlane, not a permute
-                const uint64_t sk = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oo >> 32), (int)k) << 32) |
-                                    (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oo, (int)k);
-                if (sk >= R + 1024) break;
-                if (X >= sk) r = k;
-            }
-            rr = (uint32_t)__builtin_amdgcn_readlane((int)r, 63);
-            uint64_t a, b, d;  // the chunk's record: value range [a, b), source offset d
-            if ((uint32_t)__builtin_amdgcn_readlane((int)r, 0) == rr) {  // (uniform) one record: readlane
-                a = lane_u64(vsx, (int)rr);
-                b = lane_u64(vex, (int)rr);
-                d = lane_u64(vsrc, (int)rr);
-                if (R >= a && R + 1024 <= b) {  // the whole row inside the value: most rows of large records
-                    *reinterpret_cast<uint4 *>(out + X) = load16u(vals + d + X);
-                    continue;
-                }
-            } else {
-                a = __shfl(vsx, (int)r);
-                b = __shfl(vex, (int)r);
-                d = __shfl(vsrc, (int)r);
-            }
-            if (X >= a && X + 16 <= b) *reinterpret_cast<uint4 *>(out + X) = load16u(vals + d + X);
-        }
+        // 3. the rest of the group's output, a lane per record, as 16 B
+        // pieces at any alignment inside the record: a payload the wave path
+        // copied (above) needs only its first 16 bytes; a small one is copied
+        // here whole.  A piece that ends at the end of a region and starts
+        // before it (a key or value shorter than 16 B) carries wrong bytes in
+        // front; the lane writes its pieces from the record's end back to its
+        // header, so its later stores overwrite them (one thread's stores to
+        // one address land in program order).  Bytes written twice are the
+        // same bytes.
         if (have) {
-            // (b), from the record's end back: the value's last and first 16
-            // bytes (the chunks between them are (a)'s), the key, the header
+            const uint64_t vsx = oo + 16 + kl, vex = vsx + vl;  // the value's output range
             if (vl >= 16) {
-                store16u(out + vex - 16, load16u(vals + vo + vl - 16));
+                if (small) {
+                    store16u(out + vex - 16, load16u(vals + vo + vl - 16));
+                    for (uint64_t i = 16; i + 16 <= vl; i += 16) store16u(out + vsx + i, load16u(vals + vo + i));
+                }
                 store16u(out + vsx, load16u(vals + vo));
             } else if (vl && vo + vl >= 16) {  // reaches back into the key / header
                 store16u(out + vex - 16, load16u(vals + vo + vl - 16));

@@ -136,8 +136,8 @@ struct CrcJob {
         b = p - pad - sh;
     }
 };
-// NT: non-temporal stripe loads (bytes read once); without, the lines stay in
-// L2 for a second read of the same bytes (the fused encoder's copy).
+// NT: non-temporal stripe loads (bytes read once; the scrub).  The encoder's
+// fused copy measured faster with the default policy (0.77 vs 0.83 ms per GB).
 template <bool NT = true>
 __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint32_t j, uint32_t d[5]) {
     const uint32_t lane = threadIdx.x & 63;
@@ -172,14 +172,29 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint32_t j, uint32
 // part is finally shifted past the 16 (63-l) bytes after it and the lanes
 // XOR-reduced (lanes_combine): F(~0, V); crc = ~that.
 //
-// One stripe of the value at virtual stripe j into A:
+// One stripe of the value at virtual stripe j into A.  Store: the value's
+// bytes also go to ob (the value's copy, any alignment) -- every lane whose 16
+// bytes lie inside the value writes them (the value's first < 16 bytes are the
+// caller's); one buffer store per stripe on every path (lanes in the padding
+// at an offset past the stripe's 1 KiB window: dropped by the bounds check),
+// so the vmcnt counts stay exact.
+typedef uint32_t u32x4_st __attribute__((ext_vector_type(4)));
+template <bool Store = false>
 __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint32_t j, const uint32_t d[5], uint32_t A,
-                                                const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
+                                                const CrcTabs &t, uint32_t lb0, uint32_t lb1,
+                                                uint8_t *ob = nullptr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t v = (j << 10) + 16u * lane;  // virtual position of this lane's chunk
     uint32_t w[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], jb.sh);
+    if constexpr (Store) {
+        // the stripe's window in the copy: ob + (j KiB - pad), never read or
+        // written outside [ob, ob + L) (the padding lanes are dropped)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ob + (j << 10) - jb.pad, 0, 1024, 0x00020000);
+        const u32x4_st x = {w[0], w[1], w[2], w[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(v >= jb.pad ? 16u * lane : 0x800u), 0, 0);
+    }
     // (uniform) the stripes that hold the value's first 4 bytes; then per lane:
     // bytes before the value are zero, its first 4 complemented
     if (j < jb.head4) {  // (a scalar branch, then the lanes)
@@ -208,9 +223,12 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint32_t j, co
 // every load is issued unconditionally (a dummy reload past the last stripe),
 // so the compiler's vmcnt counts stay exact.  Item t's CRC lands in lane t.
 constexpr int kRing = 4;  // ring depths 2, 4 and 8 measured the same (again in round 3)
-template <bool NT = true, class PtrOf, class Combine>
+struct NoCopy {
+    __device__ uint8_t *operator()(int) const { return nullptr; }
+};
+template <bool NT = true, bool Store = false, class PtrOf, class Combine, class OutOf = NoCopy>
 __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const CrcTabs &t, uint32_t lb0,
-                              uint32_t lb1, Combine combine) {
+                              uint32_t lb1, Combine combine, OutOf out_of = OutOf()) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t out = 0;
     auto job = [&](int it) { return CrcJob(ptr_of(it), lane_u32(len, it)); };
@@ -239,6 +257,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
     uint64_t crem = todo;
     int ct = __builtin_ctzll(todo);
     CrcJob cj = job(ct);
+    uint8_t *ob = out_of(ct);
     uint32_t cs = 0;
     uint32_t A = 0;
     while (crem) {
@@ -250,7 +269,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
             // exact (a load inside the branch made the merge at the loop head
             // wait for every load in flight: the ring drained once per round)
             if (crem) {
-                A = fold_stripe(cj, cs, ring[k], A, t, lb0, lb1);
+                A = fold_stripe<Store>(cj, cs, ring[k], A, t, lb0, lb1, ob);
                 if (++cs == cj.J) {  // value done
                     const uint32_t f = combine(A);
                     if (lane == (uint32_t)ct) out = f;
@@ -260,6 +279,7 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
                     if (crem) {
                         ct = __builtin_ctzll(crem);
                         cj = job(ct);
+                        ob = out_of(ct);
                     }
                 }
             }
