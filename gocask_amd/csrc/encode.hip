@@ -472,7 +472,9 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         const bool small = have && (L <= kLaneMax || po < 16);
         uint32_t crc = 0;
         if (__ballot(small)) {
-            const uint32_t c = lane_crc((del ? keys : vals) + po, L, small, *T, lb0, lb1);
+            // (its whole 16 B pieces copied to the output from the same registers)
+            const uint32_t c = lane_crc<false, true>((del ? keys : vals) + po, L, small, *T, lb0, lb1,
+                                                     out + oo + 16 + (del ? 0 : kl));
             if (small) crc = c;
         }
         const uint64_t todo = __ballot(have && !small);
@@ -488,8 +490,8 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         const uint32_t h1 = t, h2 = del ? 0u : (uint32_t)kl, h3 = (uint32_t)(del ? kl : vl);
         // 3. the rest of the group's output, a lane per record, as 16 B
         // pieces at any alignment inside the record: a payload the wave path
-        // copied (above) needs only its first 16 bytes; a small one is copied
-        // here whole.  A piece that ends at the end of a region and starts
+        // copied (above) needs only its first 16 bytes, a small one (whose
+        // whole pieces lane_crc stored) its last L % 16.  A piece that ends at the end of a region and starts
         // before it (a key or value shorter than 16 B) carries wrong bytes in
         // front; the lane writes its pieces from the record's end back to its
         // header, so its later stores overwrite them (one thread's stores to
@@ -498,11 +500,10 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         if (have) {
             const uint64_t vsx = oo + 16 + kl, vex = vsx + vl;  // the value's output range
             if (vl >= 16) {
-                if (small) {
+                if (!small)
+                    store16u(out + vsx, load16u(vals + vo));
+                else if (vl & 15)
                     store16u(out + vex - 16, load16u(vals + vo + vl - 16));
-                    for (uint64_t i = 16; i + 16 <= vl; i += 16) store16u(out + vsx + i, load16u(vals + vo + i));
-                }
-                store16u(out + vsx, load16u(vals + vo));
             } else if (vl && vo + vl >= 16) {  // reaches back into the key / header
                 store16u(out + vex - 16, load16u(vals + vo + vl - 16));
             } else {

@@ -297,8 +297,11 @@ constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
 // four 16 B loads (each lane's address is its own line, so one instruction
 // per 16 B instead of per 4 B); reads up to 12 bytes past the value's last
 // dword, so only for buffers padded past their end (the replay arena).
-template <bool Wide = false>
-__device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1) {
+// Store: the value's whole 16 B pieces also go to op (any alignment), from
+// the same registers; the last L % 16 bytes are the caller's.
+template <bool Wide = false, bool Store = false>
+__device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1,
+                                    uint8_t *op = nullptr) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
     const uint32_t nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
@@ -319,6 +322,20 @@ __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, cons
         } else {
 #pragma unroll
             for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
+        }
+        if constexpr (Store) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (act && 4 * b + 16 * q + 16 <= L) {
+                    typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+                    u32x4_a1 x;
+                    x.x = __builtin_amdgcn_alignbyte(d[4 * q + 1], d[4 * q], sh);
+                    x.y = __builtin_amdgcn_alignbyte(d[4 * q + 2], d[4 * q + 1], sh);
+                    x.z = __builtin_amdgcn_alignbyte(d[4 * q + 3], d[4 * q + 2], sh);
+                    x.w = __builtin_amdgcn_alignbyte(d[4 * q + 4], d[4 * q + 3], sh);
+                    *reinterpret_cast<u32x4_a1 *>(op + 4 * b + 16 * q) = x;
+                }
+            }
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
