@@ -117,6 +117,11 @@ def test_encode_batch_exact_size_and_alignment():
     rc, total = _raw_encode(dev(keys), d_koff, dev(vals), d_voff, ts, tomb, out, out_off)
     assert rc == _lib.GCK_OK and total == need
     assert bytes(out.cpu().numpy()) == _expected(ops)
+    # too small an output: refused, the size needed reported, nothing written
+    small = torch.zeros(need - 1, dtype=torch.uint8, device="cuda")
+    rc, total = _raw_encode(dev(keys), d_koff, dev(vals), d_voff, ts, tomb, small, out_off)
+    assert rc == _lib.GCK_EINVAL and total == need
+    assert int(small.sum()) == 0
     rc, _ = _raw_encode(dev(keys, 1), d_koff, dev(vals), d_voff, ts, tomb, out, out_off)
     assert rc == _lib.GCK_EINVAL
     rc, _ = _raw_encode(dev(keys), d_koff, dev(vals, 3), d_voff, ts, tomb, out, out_off)
