@@ -435,6 +435,7 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0 = 0, lb1 = 0, kl_shift = 0;
     CrcTabs *T = &enc_tabs();
+    const uint64_t key_total = key_off[n], val_total = val_off[n];  // the blobs' sizes
     // the slicing tables, built here (no context): T0..T3 into Zs, expanded
     // into the conflict-free image, then Zs itself
     {
@@ -483,11 +484,20 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         const uint32_t L = (uint32_t)(del ? kl : vl);
         const bool small = have && (L <= kLaneMax || po < 16);
         uint32_t crc = 0;
-        if (__ballot(small)) {
-            // (its whole 16 B pieces copied to the output from the same registers)
-            const uint32_t c = lane_crc<false, true>((del ? keys : vals) + po, L, small, *T, lb0, lb1,
+        // (its whole 16 B pieces copied to the output from the same
+        // registers).  16 B loads where the blob holds 16 bytes past the
+        // payload (wide: the loads may reach 15 bytes past its last byte),
+        // dword loads for the rest (the blob's last payloads)
+        const bool wide = small && po + L + 16 <= (del ? key_total : val_total);
+        if (__ballot(wide)) {
+            const uint32_t c = lane_crc<true, true>((del ? keys : vals) + po, L, wide, *T, lb0, lb1,
+                                                    out + oo + 16 + (del ? 0 : kl));
+            if (wide) crc = c;
+        }
+        if (__ballot(small && !wide)) {
+            const uint32_t c = lane_crc<false, true>((del ? keys : vals) + po, L, small && !wide, *T, lb0, lb1,
                                                      out + oo + 16 + (del ? 0 : kl));
-            if (small) crc = c;
+            if (small && !wide) crc = c;
         }
         const uint64_t todo = __ballot(have && !small);
         if (todo) {
