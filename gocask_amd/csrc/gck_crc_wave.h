@@ -193,7 +193,8 @@ __device__ __forceinline__ uint32_t fold_stripe(const CrcJob &jb, uint32_t j, co
         // written outside [ob, ob + L) (the padding lanes are dropped)
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(ob + (j << 10) - jb.pad, 0, 1024, 0x00020000);
         const u32x4_st x = {w[0], w[1], w[2], w[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(v >= jb.pad ? 16u * lane : 0x800u), 0, 0);
+        // (non-temporal: written once; 0.717-0.719 against 0.732-0.737 ms per GB)
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, (int)(v >= jb.pad ? 16u * lane : 0x800u), 0, 2);
     }
     // (uniform) the stripes that hold the value's first 4 bytes; then per lane:
     // bytes before the value are zero, its first 4 complemented
