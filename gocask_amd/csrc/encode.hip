@@ -490,7 +490,7 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
         // dword loads for the rest (the blob's last payloads)
         const bool wide = small && po + L + 16 <= (del ? key_total : val_total);
         if (__ballot(wide)) {
-            const uint32_t c = lane_crc<true, true>((del ? keys : vals) + po, L, wide, *T, lb0, lb1,
+            const uint32_t c = lane_crc<true, true, 32>((del ? keys : vals) + po, L, wide, *T, lb0, lb1,
                                                     out + oo + 16 + (del ? 0 : kl));
             if (wide) crc = c;
         }

@@ -293,25 +293,27 @@ __device__ uint32_t wave_crcs(uint64_t todo, PtrOf ptr_of, uint32_t len, const C
 constexpr uint32_t kLaneMax = 256;  // values up to this size: one lane each
 
 // crc32.ChecksumIEEE of a small value by one lane (lanes run different
-// values): aligned dwords, 64 bytes of loads in flight per round, slicing-by-4
+// values): aligned dwords, 4 R bytes of loads in flight per round (R = 32:
+// a 256 B value in two round trips; scrub and encoder about 1 % faster than
+// R = 16, profiles/r4zs), slicing-by-4
 // per word, the last 0..3 bytes one at a time.  Wide: the round's dwords as
 // four 16 B loads (each lane's address is its own line, so one instruction
 // per 16 B instead of per 4 B); reads up to 12 bytes past the value's last
 // dword, so only for buffers padded past their end (the replay arena).
 // Store: the value's whole 16 B pieces also go to op (any alignment), from
 // the same registers; the last L % 16 bytes are the caller's.
-template <bool Wide = false, bool Store = false>
+template <bool Wide = false, bool Store = false, int R = 16>
 __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, const CrcTabs &t, uint32_t lb0, uint32_t lb1,
                                     uint8_t *op = nullptr) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
     const uint32_t nw = act ? (sh + L + 3) >> 2 : 0u;  // dwords covering the value
     uint32_t c = 0xFFFFFFFFu, pos = 0;
-    for (uint32_t b = 0; __ballot(b < nw); b += 16) {
-        uint32_t d[17];
+    for (uint32_t b = 0; __ballot(b < nw); b += R) {
+        uint32_t d[R + 1];
         if constexpr (Wide) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < R / 4; ++k) {
                 u32x4_a4 x = {0u, 0u, 0u, 0u};
                 if (b + 4 * k < nw) x = *reinterpret_cast<const u32x4_a4 *>(a + b + 4 * k);
                 d[4 * k] = x.x;
@@ -319,14 +321,14 @@ __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, cons
                 d[4 * k + 2] = x.z;
                 d[4 * k + 3] = x.w;
             }
-            d[16] = b + 16 < nw ? a[b + 16] : 0u;
+            d[R] = b + R < nw ? a[b + R] : 0u;
         } else {
 #pragma unroll
-            for (int i = 0; i < 17; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
+            for (int i = 0; i < R + 1; ++i) d[i] = b + i < nw ? a[b + i] : 0u;
         }
         if constexpr (Store) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < R / 4; ++q) {
                 if (act && 4 * b + 16 * q + 16 <= L) {
                     typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
                     u32x4_a1 x;
@@ -339,7 +341,7 @@ __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, cons
             }
         }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
+        for (int i = 0; i < R; ++i) {
             const uint32_t w = __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh);
             if (pos + 4 <= L) {
                 c = slice4x(t.S, lb0, lb1, c ^ w, 0u);

@@ -120,7 +120,7 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
         const bool small = ok && len <= kLaneMax;
         const uint64_t todo = __ballot(ok && !small);
         if (__ballot(small)) {  // small values: a lane each, all at once
-            const uint32_t c = lane_crc<true>(arena + off, len, small, T, lb0, lb1);  // the arena is padded
+            const uint32_t c = lane_crc<true, false, 32>(arena + off, len, small, T, lb0, lb1);  // the arena is padded
             if (small) crc = c;
         }
         if (todo) {
