@@ -364,15 +364,18 @@ __global__ void k_enc_add(uint64_t *__restrict__ out_off, const uint64_t *__rest
 // by bytes: groups of 64 records differ by orders of magnitude.
 constexpr uint64_t kEncUnit = 64 << 10;
 // The unit count from the scan's results on the device (res[0] = the batch's
-// bytes, res[1] = refusals): none when the batch is refused or does not fit
-// out_cap, so the host launches every kernel before it reads anything back.
-__device__ __forceinline__ uint64_t enc_units(const uint64_t *res, uint64_t out_cap) {
+// bytes, res[1] = refusals): none when the batch is refused, does not fit
+// out_cap, or needs more units than the host allotted (units_max: the host
+// then runs the call again with enough), so the host launches every kernel
+// before it reads anything back.
+__device__ __forceinline__ uint64_t enc_units(const uint64_t *res, uint64_t out_cap, uint64_t units_max) {
     const uint64_t total = res[0];
-    return ((uint32_t)res[1] || total == 0 || total > out_cap) ? 0 : (total - 1) / kEncUnit + 1;
+    const uint64_t u = total ? (total - 1) / kEncUnit + 1 : 0;
+    return ((uint32_t)res[1] || total > out_cap || u > units_max) ? 0 : u;
 }
 __global__ void k_enc_units(const uint64_t *__restrict__ out_off, uint64_t n, const uint64_t *__restrict__ res,
-                            uint64_t out_cap, uint32_t *__restrict__ ufirst) {
-    const uint64_t n_units = enc_units(res, out_cap);
+                            uint64_t out_cap, uint64_t units_max, uint32_t *__restrict__ ufirst) {
+    const uint64_t n_units = enc_units(res, out_cap, units_max);
     if (n_units == 0) return;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= n; r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t s = r < n ? out_off[r] : ~0ull;
@@ -429,8 +432,8 @@ __global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict
                                                        const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
                                                        const uint32_t *__restrict__ ufirst,
                                                        const uint64_t *__restrict__ res, uint64_t out_cap,
-                                                       uint32_t *__restrict__ queue) {
-    const uint64_t n_units = enc_units(res, out_cap);
+                                                       uint64_t units_max, uint32_t *__restrict__ queue) {
+    const uint64_t n_units = enc_units(res, out_cap, units_max);
     if (n_units == 0) return;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0 = 0, lb1 = 0, kl_shift = 0;
@@ -565,40 +568,45 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
     // queue, ufirst for as many units as out_cap holds.  Every kernel is
     // launched before the one readback (the sizes' verdict is applied on the
     // device, enc_units): one host round trip per call instead of two.
-    const uint64_t nb = (n + kEncScanBlock - 1) / kEncScanBlock;
-    size_t dev_mem = 0;  // (an output larger than the device's memory is not one kernel's)
+    size_t dev_mem = 0;  // (an output larger than the device's memory: a second pass, below)
     GCK_HIP(hipDeviceTotalMem(&dev_mem, dev));
-    const uint64_t cap = std::min<uint64_t>(out_cap, dev_mem);
-    const uint64_t units_max = cap ? (cap - 1) / kEncUnit + 1 : 1;
-    void *tmp = nullptr;
-    GCK_HIP(hipMallocAsync(&tmp, (nb + 1) * 8 + 24 + (units_max + 1) * 4, s));
-    uint64_t *bsum = static_cast<uint64_t *>(tmp), *res = bsum + nb + 1;
-    uint32_t *queue = reinterpret_cast<uint32_t *>(res + 2), *ufirst = queue + 2;
-    GCK_HIP(hipMemsetAsync(res, 0, 24, s));
-    // 1. sizes and offsets on the device
-    if (n) k_enc_sizes<<<(uint32_t)nb, kEncScanBlock, 0, s>>>(key_off, val_off, tomb, n, out_off, bsum,
-                                                              reinterpret_cast<uint32_t *>(res + 1));
-    k_enc_top<<<1, 64, 0, s>>>(bsum, nb, n, out_off, res);
-    if (n) {
-        k_enc_add<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(out_off, bsum, n);
-        // units of 64 KiB of output: the last record starts before the total
-        // (units past its start stay empty, k_enc_units)
-        k_enc_units<<<(uint32_t)std::min<uint64_t>((n + 256) / 256, 4096), 256, 0, s>>>(out_off, n, res, out_cap,
-                                                                                       ufirst);
-        // one 1024-thread workgroup per CU (the CRC tables take 152 KiB of LDS)
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((units_max + 15) / 16, (uint64_t)n_cu);
-        k_encode_batch<<<grid, 1024, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst, res,
-                                              out_cap, queue);
-        GCK_HIP(hipGetLastError());
+    const uint64_t nb = (n + kEncScanBlock - 1) / kEncScanBlock;
+    uint64_t units_max = (std::min<uint64_t>(out_cap, dev_mem) + kEncUnit - 1) / kEncUnit;
+    for (;;) {
+        units_max = std::max<uint64_t>(units_max, 1);
+        void *tmp = nullptr;
+        GCK_HIP(hipMallocAsync(&tmp, (nb + 1) * 8 + 24 + (units_max + 1) * 4, s));
+        uint64_t *bsum = static_cast<uint64_t *>(tmp), *res = bsum + nb + 1;
+        uint32_t *queue = reinterpret_cast<uint32_t *>(res + 2), *ufirst = queue + 2;
+        GCK_HIP(hipMemsetAsync(res, 0, 24, s));
+        // 1. sizes and offsets on the device
+        if (n) k_enc_sizes<<<(uint32_t)nb, kEncScanBlock, 0, s>>>(key_off, val_off, tomb, n, out_off, bsum,
+                                                                  reinterpret_cast<uint32_t *>(res + 1));
+        k_enc_top<<<1, 64, 0, s>>>(bsum, nb, n, out_off, res);
+        if (n) {
+            k_enc_add<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(out_off, bsum, n);
+            // units of 64 KiB of output: the last record starts before the total
+            // (units past its start stay empty, k_enc_units)
+            k_enc_units<<<(uint32_t)std::min<uint64_t>((n + 256) / 256, 4096), 256, 0, s>>>(out_off, n, res, out_cap,
+                                                                                           units_max, ufirst);
+            // one 1024-thread workgroup per CU (the CRC tables take 152 KiB of LDS)
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((units_max + 15) / 16, (uint64_t)n_cu);
+            k_encode_batch<<<grid, 1024, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst,
+                                                  res, out_cap, units_max, queue);
+            GCK_HIP(hipGetLastError());
+        }
+        uint64_t h[2] = {0, 0};
+        GCK_HIP(hipMemcpyAsync(h, res, 16, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        (void)hipFreeAsync(tmp, s);
+        const uint32_t err = (uint32_t)h[1];
+        if (err & 1u) return GCK_EINVALID_KEY;  // Put / Delete of an empty key (core/db.go:186, :294)
+        if (err & 2u) return GCK_EINVAL;        // decreasing offsets, or u32 header fields overflow
+        *total = h[0];
+        if (*total > out_cap) return GCK_EINVAL;  // *total says how much is needed (nothing was written)
+        const uint64_t need = *total ? (*total - 1) / kEncUnit + 1 : 0;
+        if (need <= units_max) break;
+        units_max = need;  // an output past the device's memory (mapped host memory): again, with room
     }
-    uint64_t h[2] = {0, 0};
-    GCK_HIP(hipMemcpyAsync(h, res, 16, hipMemcpyDeviceToHost, s));
-    GCK_HIP(hipStreamSynchronize(s));
-    (void)hipFreeAsync(tmp, s);
-    const uint32_t err = (uint32_t)h[1];
-    if (err & 1u) return GCK_EINVALID_KEY;  // Put / Delete of an empty key (core/db.go:186, :294)
-    if (err & 2u) return GCK_EINVAL;        // decreasing offsets, or u32 header fields overflow
-    *total = h[0];
-    if (*total > out_cap) return GCK_EINVAL;  // *total says how much is needed (nothing was written)
     return GCK_OK;
 }
