@@ -363,6 +363,7 @@ __global__ void k_enc_add(uint64_t *__restrict__ out_off, const uint64_t *__rest
 // (start_{r-1} / W, start_r / W]); ufirst[U] = n.  Units balance the kernel
 // by bytes: groups of 64 records differ by orders of magnitude.
 constexpr uint64_t kEncUnit = 64 << 10;
+constexpr uint32_t kEncThreads = 512;  // k_encode_batch's workgroup (see its launch)
 // The unit count from the scan's results on the device (res[0] = the batch's
 // bytes, res[1] = refusals): none when the batch is refused, does not fit
 // out_cap, or needs more units than the host allotted (units_max: the host
@@ -423,7 +424,7 @@ __device__ __forceinline__ CrcTabs &enc_tabs() {
 // key and the rest of a small payload as 16 B pieces.  Round 3's copy pass
 // over 1 KiB output rows re-read the payloads from L2 and assembled the rows
 // holding record boundaries byte by byte: 1.22 ms per GB against 0.77.
-__global__ __launch_bounds__(1024) void k_encode_batch(const uint8_t *__restrict__ keys,
+__global__ __launch_bounds__(kEncThreads) void k_encode_batch(const uint8_t *__restrict__ keys,
                                                        const uint64_t *__restrict__ key_off,
                                                        const uint8_t *__restrict__ vals,
                                                        const uint64_t *__restrict__ val_off,
@@ -589,9 +590,12 @@ extern "C" int gck_encode_batch(const uint8_t *keys, const uint64_t *key_off, co
             // (units past its start stay empty, k_enc_units)
             k_enc_units<<<(uint32_t)std::min<uint64_t>((n + 256) / 256, 4096), 256, 0, s>>>(out_off, n, res, out_cap,
                                                                                            units_max, ufirst);
-            // one 1024-thread workgroup per CU (the CRC tables take 152 KiB of LDS)
-            const uint32_t grid = (uint32_t)std::min<uint64_t>((units_max + 15) / 16, (uint64_t)n_cu);
-            k_encode_batch<<<grid, 1024, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst,
+            // one workgroup per CU (the CRC tables take 152 KiB of LDS) of 8
+            // wavefronts: 0.68-0.69 ms per GB against 0.71-0.72 with 16 (the
+            // memory system, not latency, is what more wavefronts add to), 0.69
+            // with 12, 0.76 with 6, 0.95 with 4 (profiles/r4zu, r4zv)
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((units_max + 7) / 8, (uint64_t)n_cu);
+            k_encode_batch<<<grid, kEncThreads, 0, s>>>(keys, key_off, vals, val_off, ts, tomb, n, out_off, out, ufirst,
                                                   res, out_cap, units_max, queue);
             GCK_HIP(hipGetLastError());
         }
