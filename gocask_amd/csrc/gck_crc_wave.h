@@ -136,8 +136,11 @@ struct CrcJob {
         b = p - pad - sh;
     }
 };
-// NT: non-temporal stripe loads (bytes read once; the scrub).  The encoder's
-// fused copy measured faster with the default policy (0.77 vs 0.83 ms per GB).
+// NT: non-temporal stripe loads.  Both callers now keep the default policy:
+// a stripe's 1 KiB starts anywhere, so its first and last lines are shared
+// with the neighbouring stripes (and the fifth dword load reads the next
+// lane's line again) -- non-temporal loads re-fetch them: C3 scrub 2.83-2.92
+// against 3.21-3.27 ms (profiles/r4zy), the encoder 0.77 against 0.83 ms.
 template <bool NT = true>
 __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint32_t j, uint32_t d[5]) {
     const uint32_t lane = threadIdx.x & 63;
@@ -147,7 +150,7 @@ __device__ __forceinline__ void stripe_load(const CrcJob &jb, uint32_t j, uint32
         const uint8_t *p0 = jb.p - (reinterpret_cast<uintptr_t>(jb.p) & 3);
         a = v + 16 <= jb.pad ? p0 : a;
     }
-    // non-temporal stripe loads (scrub 4.92 -> 4.76-4.90 ms)
+    // (NT: round 2 measured 4.92 -> 4.76-4.90 ms for the scrub of then; round 4 reversed it, above)
     u32x4_a4 x;
     if constexpr (NT)
         x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_a4 *>(a));

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
             if (small) crc = c;
         }
         if (todo) {
-            const uint32_t c = wave_crcs(todo, [&](int it) { return arena + lane_u64(off, it); }, len, T, lb0, lb1,
+            const uint32_t c = wave_crcs<false>(todo, [&](int it) { return arena + lane_u64(off, it); }, len, T, lb0, lb1,
                                          [&](uint32_t A) { return lanes_combine(T, lb0, A); });
             if ((todo >> lane) & 1) crc = c;
         }
