@@ -149,3 +149,36 @@ def test_encode_batch_piece_edges(seed):
             ops.append((100 + i, k, rng.randbytes(rng.choice(vlens + [rng.randint(0, 5000)]))))
     out, off = core.encode_batch(ops)
     assert bytes(out.cpu().numpy()) == _expected(ops)
+
+
+@pytest.mark.parametrize("seed", [31, 32])
+def test_encode_batch_random_large(seed):
+    """100 K records of every size class at once -- many per 16 B piece, per
+    1 KiB stripe and per 64 KiB unit, values past a unit -- so the wave path's
+    stripe stores, the lane path's pieces and the per-record pieces of
+    neighbouring records (often in one wavefront, sometimes in two) all meet;
+    byte-exact against the oracle's serializeEntry."""
+    from gocask_amd import core
+
+    rng = np.random.default_rng(seed)
+    n = 100_000
+    kl = rng.integers(1, 65, n)
+    cls = rng.random(n)
+    vl = np.where(cls < 0.6, rng.integers(0, 300, n),
+                  np.where(cls < 0.95, rng.integers(300, 4096, n), rng.integers(4096, 70_000, n)))
+    tomb = rng.random(n) < 0.05
+    blob = rng.integers(0, 256, int(kl.sum() + vl.sum()), dtype=np.uint8).tobytes()
+    ops, o = [], 0
+    for i in range(n):
+        k = blob[o:o + int(kl[i])]
+        o += int(kl[i])
+        v = None if tomb[i] else blob[o:o + int(vl[i])]
+        o += int(vl[i])
+        ops.append((int(rng.integers(0, 2**32)), k, v))
+    out, off = core.encode_batch(ops)
+    exp = _expected(ops)
+    got = bytes(out.cpu().numpy())
+    assert len(got) == len(exp)
+    if got != exp:
+        a = np.frombuffer(got, np.uint8) != np.frombuffer(exp, np.uint8)
+        raise AssertionError(f"first differing byte {int(np.argmax(a))} of {len(exp)}")
