@@ -550,6 +550,7 @@ class ReplayContext:
         if not values:
             check(self._L.gck_ctx_get_batch(self._h, blob.ctypes.data, off.ctypes.data, n, st.ctypes.data,
                                             vs.ctypes.data, cc.ctypes.data, None, 0, None, ctypes.byref(ms)))
+            self.last_get_ms = ms.value
             return st, vs, cc, None
         vo = np.zeros(n, dtype=np.uint64)
         cap = 1 << 20
@@ -565,6 +566,7 @@ class ReplayContext:
             check(rc)
             break
         vals = [bytes(buf[int(vo[i]):int(vo[i]) + int(vs[i])]) if st[i] == GCK_OK else None for i in range(n)]
+        self.last_get_ms = ms.value  # device time of the lookup, CRCs and value copy (events)
         return st, vs, cc, vals
 
     def scrub_keydir(self):

@@ -93,6 +93,23 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
 // the caller), claimed one group ahead: value sizes are heavy-tailed, so a
 // fixed stride left the kernel waiting for the wavefronts that drew the
 // largest values.
+// 16 bytes to any byte address (gfx9 global stores need no alignment).
+__device__ __forceinline__ void store16_any(uint8_t *dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+    u32x4_a1 x;
+    x.x = a;
+    x.y = b;
+    x.z = c;
+    x.w = d;
+    *reinterpret_cast<u32x4_a1 *>(dst) = x;
+}
+
+// Copy (Get with values): every found value is also copied to dst + dst_off
+// from the registers its CRC is computed in -- a large one by the stripe
+// stores of wave_crcs, a small one's whole 16 B pieces by lane_crc, the rest
+// (a large value's first 16 bytes, a small one's last L % 16) by its lane.
+// A value whose CRC fails is copied too; the caller reports no value for it.
+template <bool Copy>
 __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ arena, const uint32_t *__restrict__ g_slice,
                                                  uint64_t n,
                                                 const uint64_t *__restrict__ item,
@@ -120,21 +137,25 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
         const bool small = ok && len <= kLaneMax;
         const uint64_t todo = __ballot(ok && !small);
         if (__ballot(small)) {  // small values: a lane each, all at once
-            const uint32_t c = lane_crc<true, false, 32>(arena + off, len, small, T, lb0, lb1);  // the arena is padded
+            const uint32_t c = lane_crc<true, Copy, 32>(arena + off, len, small, T, lb0, lb1, dst + doff);  // (the arena is padded)
             if (small) crc = c;
         }
         if (todo) {
-            const uint32_t c = wave_crcs<false>(todo, [&](int it) { return arena + lane_u64(off, it); }, len, T, lb0, lb1,
-                                         [&](uint32_t A) { return lanes_combine(T, lb0, A); });
+            const uint32_t c = wave_crcs<false, Copy>(todo, [&](int it) { return arena + lane_u64(off, it); }, len, T,
+                                                      lb0, lb1, [&](uint32_t A) { return lanes_combine(T, lb0, A); },
+                                                      [&](int it) { return dst + lane_u64(doff, it); });
             if ((todo >> lane) & 1) crc = c;
         }
-        if (dst) {  // the values that passed, copied by the whole wave
-            for (uint64_t cp = __ballot(ok && crc == want); cp; cp &= cp - 1) {
-                const int t = __builtin_ctzll(cp);
-                uint8_t *d = dst + lane_u64(doff, t);  // (t wave-uniform: scalars)
-                const uint8_t *src = arena + lane_u64(off, t);
-                const uint32_t L = lane_u32(len, t);
-                for (uint64_t j = lane; j < L; j += 64) d[j] = src[j];
+        if constexpr (Copy) {
+            if (ok && len >= 16 && (!small || (len & 15))) {  // a large value's first 16 bytes, a small one's last
+                const uint32_t at = small ? len - 16 : 0u;
+                const uint8_t *p = arena + off + at;
+                const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+                const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
+                store16_any(dst + doff + at, __builtin_amdgcn_alignbyte(a[1], a[0], sh), __builtin_amdgcn_alignbyte(a[2], a[1], sh),
+                            __builtin_amdgcn_alignbyte(a[3], a[2], sh), __builtin_amdgcn_alignbyte(a[4], a[3], sh));
+            } else if (ok && len < 16) {
+                for (uint32_t j = 0; j < len; ++j) dst[doff + j] = arena[off + j];
             }
         }
         if (have) {
@@ -207,7 +228,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     const uint32_t grid = std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueVerify;
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_verify<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
+    (dvals ? k_verify<true> : k_verify<false>)<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
                                   c->d_gvoff.as<uint64_t>(), dvals, queue);
     GCK_HIP(hipEventRecord(b, s));
@@ -257,7 +278,7 @@ int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint
                                                        c->d_gexp.as<uint32_t>());
     uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueVerify;
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_verify<<<(uint32_t)c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(),
+    k_verify<false><<<(uint32_t)c->n_cu, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(),
                                                     c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>(),
                                                     c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(), nullptr,
                                                     nullptr, queue);
