@@ -133,7 +133,7 @@ struct Ctx {
     bool kd_valid = false;   // d_ktab / d_khash / d_kdout describe the last run
     uint64_t kd_slots = 0;   // table slots (power of two; 0: no records)
     // batched Get / scrub (get.hip): query keys, per-item state, values
-    DBuf d_gkeys, d_gkoff, d_gstat, d_gitem, d_gvsize, d_gexp, d_gcrc, d_gvoff, d_gvals;
+    DBuf d_gkeys, d_gkoff, d_gstat, d_gitem, d_gvsize, d_gexp, d_gcrc, d_gvoff, d_gvals, d_gscan;
     // the key blob of gck_replay with GCK_OPT_KEYS: look-back words, offsets, bytes
     DBuf d_klb, d_koff, d_keyblob;
 

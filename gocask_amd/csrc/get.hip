@@ -69,6 +69,62 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
     }
 }
 
+// The values' offsets in the caller's buffer, on the device: an exclusive
+// scan of ValueSize over the keys the lookup found (UINT64_MAX for the
+// others), blocks of 1024, then the block sums by one wavefront, then the
+// add; res[0] = the bytes of all found values.  (The host had read back
+// status and sizes, summed them and sent the offsets down: a round trip of
+// 16 B per key in the middle of the call.)
+constexpr uint32_t kVoffBlock = 1024;
+__global__ __launch_bounds__(kVoffBlock) void k_voff_block(const int32_t *__restrict__ status,
+                                                           const uint32_t *__restrict__ vsize, uint32_t n,
+                                                           uint64_t *__restrict__ voff, uint64_t *__restrict__ bsum) {
+    __shared__ uint64_t ws[kVoffBlock / 64];
+    const uint32_t i = blockIdx.x * kVoffBlock + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t v = i < n && status[i] == GCK_OK ? vsize[i] : 0;
+    uint64_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(inc, d, 64);
+        if (lane >= (uint32_t)d) inc += y;
+    }
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (uint32_t k = 0; k < kVoffBlock / 64; ++k) {
+            const uint64_t t = ws[k];
+            ws[k] = run;
+            run += t;
+        }
+        bsum[blockIdx.x] = run;
+    }
+    __syncthreads();
+    if (i < n) voff[i] = ws[wid] + inc - v;
+}
+__global__ void k_voff_top(uint64_t *__restrict__ bsum, uint32_t nb, uint64_t *__restrict__ res) {
+    const uint32_t lane = threadIdx.x;
+    uint64_t run = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+        const uint32_t b = b0 + lane;
+        const uint64_t v = b < nb ? bsum[b] : 0;
+        uint64_t inc = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(inc, d, 64);
+            if (lane >= (uint32_t)d) inc += y;
+        }
+        if (b < nb) bsum[b] = run + inc - v;
+        run += __shfl(inc, 63, 64);
+    }
+    if (lane == 0) res[0] = run;
+}
+__global__ __launch_bounds__(256) void k_voff_add(const int32_t *__restrict__ status, uint32_t n,
+                                                  uint64_t *__restrict__ voff, const uint64_t *__restrict__ bsum) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) voff[i] = status[i] == GCK_OK ? voff[i] + bsum[i / kVoffBlock] : ~0ull;
+}
+
 // k_scrub_items: the live keydir entries as verify items (Get of every key).
 __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__ live, uint64_t n,
                                                      const uint64_t *__restrict__ fbase,
@@ -189,7 +245,8 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     if ((rc = c->d_gkeys.ensure(kb + 16)) || (rc = c->d_gkoff.ensure((n + 1) * 8ull)) ||
         (rc = c->d_gstat.ensure(n * 4ull)) || (rc = c->d_gitem.ensure(n * 8ull)) ||
         (rc = c->d_gvsize.ensure(n * 4ull)) || (rc = c->d_gexp.ensure(n * 4ull)) ||
-        (rc = c->d_gcrc.ensure(n * 4ull)) || (rc = c->d_gvoff.ensure(n * 8ull)))
+        (rc = c->d_gcrc.ensure(n * 4ull)) || (rc = c->d_gvoff.ensure(n * 8ull)) ||
+        (rc = c->d_gscan.ensure(((n + kVoffBlock - 1) / kVoffBlock + 1) * 8ull + 8)))
         return rc;
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -206,22 +263,25 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
         c->d_out.as<gck_rec>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
         c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>());
     uint8_t *dvals = nullptr;
-    if (values) {  // value offsets of the found keys, back to back
-        GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipStreamSynchronize(s));
+    if (values) {  // value offsets of the found keys, back to back (on the device; 8 B come back)
+        const uint32_t nb = (n + kVoffBlock - 1) / kVoffBlock;
+        uint64_t *bsum = c->d_gscan.as<uint64_t>(), *res = bsum + nb + 1;
+        k_voff_block<<<nb, kVoffBlock, 0, s>>>(c->d_gstat.as<int32_t>(), c->d_gvsize.as<uint32_t>(), n,
+                                               c->d_gvoff.as<uint64_t>(), bsum);
+        k_voff_top<<<1, 64, 0, s>>>(bsum, nb, res);
+        k_voff_add<<<(n + 255) / 256, 256, 0, s>>>(c->d_gstat.as<int32_t>(), n, c->d_gvoff.as<uint64_t>(), bsum);
         uint64_t tot = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-            val_off[i] = status[i] == GCK_OK ? tot : ~0ull;
-            if (status[i] == GCK_OK) tot += value_size[i];
-        }
-        if (tot > values_cap) {
+        GCK_HIP(hipMemcpyAsync(&tot, res, 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        if (tot > values_cap) {  // status / value_size of the lookup, for a retry
+            GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
+            GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
+            GCK_HIP(hipStreamSynchronize(s));
             (void)hipEventDestroy(a);
             (void)hipEventDestroy(b);
             return GCK_EINVAL;
         }
         if ((rc = c->d_gvals.ensure(tot))) return rc;
-        GCK_HIP(hipMemcpyAsync(c->d_gvoff.p, val_off, n * 8ull, hipMemcpyHostToDevice, s));
         dvals = c->d_gvals.as<uint8_t>();
     }
     // one 1024-thread workgroup per CU (the tables take 132 KiB of LDS)
@@ -235,6 +295,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     GCK_HIP(hipMemcpyAsync(status, c->d_gstat.p, n * 4ull, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipMemcpyAsync(value_size, c->d_gvsize.p, n * 4ull, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipMemcpyAsync(crc_calc, c->d_gcrc.p, n * 4ull, hipMemcpyDeviceToHost, s));
+    if (values) GCK_HIP(hipMemcpyAsync(val_off, c->d_gvoff.p, n * 8ull, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
     if (values) {
         uint64_t tot = 0;

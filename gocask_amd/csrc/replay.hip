@@ -1842,7 +1842,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
-                   &c->d_gvoff, &c->d_gvals, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
+                   &c->d_gvoff, &c->d_gvals, &c->d_gscan, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
                    &c->d_cdata, &c->d_chint, &c->d_cjmp, &c->d_con, &c->d_klb, &c->d_koff, &c->d_keyblob};
     for (DBuf *b : all) b->release();
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
