@@ -401,17 +401,6 @@ __device__ __forceinline__ uint4 load16u(const uint8_t *src) {
                       __builtin_amdgcn_alignbyte(x.w, x.z, sh), __builtin_amdgcn_alignbyte(y, x.w, sh));
 }
 
-// 16 bytes to any byte address: one dwordx4 store (gfx9 global stores need no
-// alignment; the amdhsa target compiles a 1-byte-aligned vector access to it).
-typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
-__device__ __forceinline__ void store16u(uint8_t *dst, uint4 v) {
-    u32x4_a1 x;
-    x.x = v.x;
-    x.y = v.y;
-    x.z = v.z;
-    x.w = v.w;
-    *reinterpret_cast<u32x4_a1 *>(dst) = x;
-}
 
 __device__ __forceinline__ CrcTabs &enc_tabs() {
     __shared__ CrcTabs t;

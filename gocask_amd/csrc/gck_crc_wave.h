@@ -114,6 +114,20 @@ __device__ __forceinline__ uint64_t lane_u64(uint64_t x, int it) {
 // bytes); a lane straddling the value start reads up to 15 bytes before it
 // (the record's header and key: inside the arena).
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+// 16 bytes to any byte address: one dwordx4 store (gfx9 global stores need no
+// alignment; the amdhsa target compiles a 1-byte-aligned vector access to it).
+// The copies built on it (the encoder's records, Get's values) rely on one
+// thread's overlapping stores landing in program order.
+typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+__device__ __forceinline__ void store16u(uint8_t *dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    u32x4_a1 x;
+    x.x = a;
+    x.y = b;
+    x.z = c;
+    x.w = d;
+    *reinterpret_cast<u32x4_a1 *>(dst) = x;
+}
+__device__ __forceinline__ void store16u(uint8_t *dst, uint4 v) { store16u(dst, v.x, v.y, v.z, v.w); }
 // (Pointer arithmetic only, never an integer cast back to a pointer: that
 // would make the loads flat, and flat loads also count on lgkmcnt, so every
 // LDS table wait would wait for HBM too.)
@@ -332,15 +346,11 @@ __device__ inline uint32_t lane_crc(const uint8_t *p, uint32_t L, bool act, cons
         if constexpr (Store) {
 #pragma unroll
             for (int q = 0; q < R / 4; ++q) {
-                if (act && 4 * b + 16 * q + 16 <= L) {
-                    typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
-                    u32x4_a1 x;
-                    x.x = __builtin_amdgcn_alignbyte(d[4 * q + 1], d[4 * q], sh);
-                    x.y = __builtin_amdgcn_alignbyte(d[4 * q + 2], d[4 * q + 1], sh);
-                    x.z = __builtin_amdgcn_alignbyte(d[4 * q + 3], d[4 * q + 2], sh);
-                    x.w = __builtin_amdgcn_alignbyte(d[4 * q + 4], d[4 * q + 3], sh);
-                    *reinterpret_cast<u32x4_a1 *>(op + 4 * b + 16 * q) = x;
-                }
+                if (act && 4 * b + 16 * q + 16 <= L)
+                    store16u(op + 4 * b + 16 * q, __builtin_amdgcn_alignbyte(d[4 * q + 1], d[4 * q], sh),
+                             __builtin_amdgcn_alignbyte(d[4 * q + 2], d[4 * q + 1], sh),
+                             __builtin_amdgcn_alignbyte(d[4 * q + 3], d[4 * q + 2], sh),
+                             __builtin_amdgcn_alignbyte(d[4 * q + 4], d[4 * q + 3], sh));
             }
         }
 #pragma unroll

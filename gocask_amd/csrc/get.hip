@@ -149,17 +149,6 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
 // the caller), claimed one group ahead: value sizes are heavy-tailed, so a
 // fixed stride left the kernel waiting for the wavefronts that drew the
 // largest values.
-// 16 bytes to any byte address (gfx9 global stores need no alignment).
-__device__ __forceinline__ void store16_any(uint8_t *dst, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-    typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
-    u32x4_a1 x;
-    x.x = a;
-    x.y = b;
-    x.z = c;
-    x.w = d;
-    *reinterpret_cast<u32x4_a1 *>(dst) = x;
-}
-
 // Copy (Get with values): every found value is also copied to dst + dst_off
 // from the registers its CRC is computed in -- a large one by the stripe
 // stores of wave_crcs, a small one's whole 16 B pieces by lane_crc, the rest
@@ -208,7 +197,7 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
                 const uint8_t *p = arena + off + at;
                 const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
                 const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
-                store16_any(dst + doff + at, __builtin_amdgcn_alignbyte(a[1], a[0], sh), __builtin_amdgcn_alignbyte(a[2], a[1], sh),
+                store16u(dst + doff + at, __builtin_amdgcn_alignbyte(a[1], a[0], sh), __builtin_amdgcn_alignbyte(a[2], a[1], sh),
                             __builtin_amdgcn_alignbyte(a[3], a[2], sh), __builtin_amdgcn_alignbyte(a[4], a[3], sh));
             } else if (ok && len < 16) {
                 for (uint32_t j = 0; j < len; ++j) dst[doff + j] = arena[off + j];
