@@ -406,13 +406,14 @@ __device__ __forceinline__ CrcTabs &enc_tabs() {
     __shared__ CrcTabs t;
     return t;
 }
-// Per group of 64 records: the payload CRCs (the LDS tables, 1024-thread
-// workgroups), a payload larger than kLaneMax copied to the output from the
+// Per group of 64 records: the payload CRCs (the LDS tables; one workgroup
+// of kEncThreads per CU), a payload larger than kLaneMax copied to the output from the
 // stripe registers of its CRC (gck_crc_wave.h fold_stripe<true>: no second
 // read), then a lane per record writes its header (the CRC from a register),
 // key and the rest of a small payload as 16 B pieces.  Round 3's copy pass
 // over 1 KiB output rows re-read the payloads from L2 and assembled the rows
-// holding record boundaries byte by byte: 1.22 ms per GB against 0.77.
+// holding record boundaries byte by byte: 1.22 ms per GB against 0.68 now
+// (DESIGN.md §10e).
 __global__ __launch_bounds__(kEncThreads) void k_encode_batch(const uint8_t *__restrict__ keys,
                                                        const uint64_t *__restrict__ key_off,
                                                        const uint8_t *__restrict__ vals,
