@@ -154,7 +154,9 @@ __global__ __launch_bounds__(256) void k_scrub_items(const gck_rec *__restrict__
 // stores of wave_crcs, a small one's whole 16 B pieces by lane_crc, the rest
 // (a large value's first 16 bytes, a small one's last L % 16) by its lane.
 // A value whose CRC fails is copied too; the caller reports no value for it.
-template <bool Copy>
+// GS: items per wavefront group (64: a lane each; fewer when a batch is too
+// small to give every wavefront of the chip a group of 64).
+template <bool Copy, int GS = 64>
 __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ arena, const uint32_t *__restrict__ g_slice,
                                                  uint64_t n,
                                                 const uint64_t *__restrict__ item,
@@ -167,13 +169,13 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ are
     const uint32_t lane = threadIdx.x & 63;
     uint32_t lb0, lb1;
     slice_bases(lane, lb0, lb1);
-    const uint64_t groups = (n + 63) >> 6, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t groups = (n + GS - 1) / GS, waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t gi = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     uint32_t claim = 0;
     if (gi < groups && lane == 0) claim = atomicAdd(queue, 1u);
     while (gi < groups) {
-        const uint64_t mine = (gi << 6) + lane;
-        const bool have = mine < n;
+        const uint64_t mine = gi * GS + lane;
+        const bool have = lane < (uint32_t)GS && mine < n;
         const bool ok = have && status[mine] == GCK_OK;
         const uint64_t off = ok ? item[mine] : 0;
         const uint32_t len = ok ? vsize[mine] : 0u, want = ok ? expect[mine] : 0u;
@@ -274,10 +276,13 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
         dvals = c->d_gvals.as<uint8_t>();
     }
     // one 1024-thread workgroup per CU (the tables take 132 KiB of LDS)
-    const uint32_t grid = std::min<uint32_t>((n + 1023) / 1024, (uint32_t)c->n_cu);
+    // groups of 16 when 64 would leave wavefronts idle (65,536 keys: 1,024
+    // groups of 64 for 4,096 wavefronts; k_verify 383 us, profiles/r4zzb)
+    const bool g16 = n < 64ull * 16 * c->n_cu;
+    const uint32_t grid = std::min<uint32_t>(g16 ? (n + 255) / 256 : (n + 1023) / 1024, (uint32_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueVerify;
     GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    (dvals ? k_verify<true> : k_verify<false>)<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
+    (dvals ? (g16 ? k_verify<true, 16> : k_verify<true, 64>) : (g16 ? k_verify<false, 16> : k_verify<false, 64>))<<<grid, 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_slice.as<uint32_t>(), n, c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(),
                                   c->d_gexp.as<uint32_t>(), c->d_gstat.as<int32_t>(), c->d_gcrc.as<uint32_t>(),
                                   c->d_gvoff.as<uint64_t>(), dvals, queue);
     GCK_HIP(hipEventRecord(b, s));
