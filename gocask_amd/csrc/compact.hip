@@ -240,6 +240,17 @@ __global__ __launch_bounds__(kCmpBlock) void k_cmp_fscatter(const uint32_t *__re
 }
 
 // The 16 bytes at p (any alignment): two dword-aligned loads and a byte shift.
+// 16 bytes to any byte address: one dwordx4 store (gfx9 global stores need no
+// alignment; as gck_crc_wave.h store16u).
+__device__ __forceinline__ void st16u(uint8_t *dst, uint4 v) {
+    typedef uint32_t u32x4_a1 __attribute__((ext_vector_type(4), aligned(1)));
+    u32x4_a1 x;
+    x.x = v.x;
+    x.y = v.y;
+    x.z = v.z;
+    x.w = v.w;
+    *reinterpret_cast<u32x4_a1 *>(dst) = x;
+}
 __device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint8_t *a = p - sh;
@@ -340,7 +351,7 @@ __global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ ar
     }
 }
 
-// Hint entries: a lane per record, byte stores (16 + KeySize bytes each).
+// Hint entries: a lane per record (16 + KeySize bytes each).
 __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
                             const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
                             const uint64_t *__restrict__ hpos, const uint32_t *__restrict__ fstart, uint32_t nf,
@@ -355,12 +366,17 @@ __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *_
         if (fstart[mid] <= i) lo = mid; else hi = mid - 1;
     }
     const uint64_t fo = pos[i] - pos[fstart[lo]];  // the record's offset in its merged file
-    const uint32_t h[4] = {r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)};
     uint8_t *d = hints + hpos[i];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) d[k] = (uint8_t)(h[k >> 2] >> (8 * (k & 3)));
     const uint8_t *key = arena + fbase[r.file] + r.rec_off + 16;
-    for (uint32_t k = 0; k < r.key_len; ++k) d[16 + k] = key[k];
+    // 16 B pieces at any alignment: the key's last 16 bytes first (a key
+    // under 16 B reaches back into the entry's header, from the record's
+    // header in the arena: written over below), then its whole pieces, then
+    // the header -- one thread's stores land in program order.  (Byte stores:
+    // 370 us for C3's 138 MB of hints, pieces 215 us, profiles/r4zzf.)
+    const uint32_t kl = r.key_len;
+    if (kl & 15) st16u(d + kl, ld16u(key + kl - 16));
+    for (uint32_t k = 0; k + 16 <= kl; k += 16) st16u(d + 16 + k, ld16u(key + k));
+    st16u(d, make_uint4(r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)));
 }
 
 }  // namespace gck
@@ -441,7 +457,9 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
     if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16))) return rc;
     if (n) {
         const uint64_t groups = (n + 63) / 64;
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((groups + 3) / 4, (uint64_t)c->n_cu * 8);
+        // 16 wavefronts per CU: 6.90-6.93 ms on C3 against 7.22-7.26 with 32;
+        // 12, 20 and 24 slower, 8 much slower (profiles/r4zzg, r4zzh)
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((groups + 3) / 4, (uint64_t)c->n_cu * 4);
         k_cmp_copy<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_kdout.as<gck_rec>(), pos, n,
                                         c->d_cdata.as<uint8_t>());
         k_cmp_hints<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
