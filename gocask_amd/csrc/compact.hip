@@ -271,10 +271,11 @@ __device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
 __global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ fbase,
                                                   const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
-                                                  uint64_t n, uint8_t *__restrict__ out) {
+                                                  uint64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ queue) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t groups = (n + 63) / 64, waves = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); g < groups; g += waves) {
+    // groups: the first per wavefront static, the rest from an atomic queue
+    for (uint64_t g = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); g < groups;) {
         const uint64_t g0 = g * 64, mine = g0 + lane;
         const uint32_t cnt = (uint32_t)min<uint64_t>(64, n - g0);
         const bool have = lane < cnt;
@@ -348,6 +349,9 @@ __global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ ar
                     if ((mask >> i) & 1) out[X + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
             }
         }
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(queue, 1u);
+        g = waves + (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
     }
 }
 
@@ -457,11 +461,15 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
     if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16))) return rc;
     if (n) {
         const uint64_t groups = (n + 63) / 64;
-        // 16 wavefronts per CU: 6.90-6.93 ms on C3 against 7.22-7.26 with 32;
-        // 12, 20 and 24 slower, 8 much slower (profiles/r4zzg, r4zzh)
+        // 16 wavefronts per CU, groups from an atomic queue: 6.41-6.43 ms on
+        // C3 against 6.88-6.94 with a static stride (which itself had been
+        // 7.22-7.26 at 32 wavefronts); 32 or 8 with the queue slower
+        // (profiles/r4zzg, r4zzh, r4zzi)
         const uint32_t grid = (uint32_t)std::min<uint64_t>((groups + 3) / 4, (uint64_t)c->n_cu * 4);
+        uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueCompact;
+        GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
         k_cmp_copy<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_kdout.as<gck_rec>(), pos, n,
-                                        c->d_cdata.as<uint8_t>());
+                                        c->d_cdata.as<uint8_t>(), queue);
         k_cmp_hints<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
                                                                c->d_kdout.as<gck_rec>(), pos, hpos,
                                                                c->d_cfstart.as<uint32_t>(), nf, n,

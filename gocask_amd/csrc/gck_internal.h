@@ -62,7 +62,7 @@ enum Phase {
 constexpr uint32_t kGbSlots = 2, kGbWords = kGbSlots + 4;
 // d_queue: atomic work queues, zeroed before each use: k_crc_rows' row
 // blocks, k_verify's item groups.
-constexpr uint32_t kQueueCrc = 0, kQueueVerify = 1, kQueueSlots = 2;
+constexpr uint32_t kQueueCrc = 0, kQueueVerify = 1, kQueueCompact = 2, kQueueSlots = 3;
 
 
 struct Ctx {
