@@ -72,22 +72,41 @@ __global__ __launch_bounds__(kCmpBlock) void k_cmp_sizes(const gck_rec *__restri
 }
 
 // One wavefront: exclusive scan of the block totals (in place), totals at [nb].
-__global__ __launch_bounds__(64) void k_cmp_top(uint64_t *__restrict__ bsum, uint64_t *__restrict__ hbsum, uint64_t nb) {
-    uint64_t ra = 0, rb = 0;
-    for (uint64_t i0 = 0; i0 < nb; i0 += 64) {
+// The block totals' exclusive scan by one 1024-thread workgroup, 1024 totals
+// per step (C3: 4,211 blocks; one wavefront took 43 us for it).
+__global__ __launch_bounds__(1024) void k_cmp_top(uint64_t *__restrict__ bsum, uint64_t *__restrict__ hbsum, uint64_t nb) {
+    __shared__ uint64_t wt[2][16], run[2];
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) run[0] = run[1] = 0;
+    __syncthreads();
+    for (uint64_t i0 = 0; i0 < nb; i0 += 1024) {
         const uint64_t i = i0 + threadIdx.x;
         const uint64_t va = i < nb ? bsum[i] : 0, vb = i < nb ? hbsum[i] : 0;
         const uint64_t a = wave_incl_sum64(va), b = wave_incl_sum64(vb);
-        if (i < nb) {
-            bsum[i] = ra + a - va;
-            hbsum[i] = rb + b - vb;
+        if (lane == 63) {
+            wt[0][wid] = a;
+            wt[1][wid] = b;
         }
-        ra += __shfl(a, 63);
-        rb += __shfl(b, 63);
+        __syncthreads();
+        uint64_t pa = run[0], pb = run[1];
+        for (uint32_t k = 0; k < wid; ++k) {
+            pa += wt[0][k];
+            pb += wt[1][k];
+        }
+        if (i < nb) {
+            bsum[i] = pa + a - va;
+            hbsum[i] = pb + b - vb;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) {
+            run[0] = pa + a;
+            run[1] = pb + b;
+        }
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
-        bsum[nb] = ra;
-        hbsum[nb] = rb;
+        bsum[nb] = run[0];
+        hbsum[nb] = run[1];
     }
 }
 
@@ -426,7 +445,7 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
     uint64_t *pos = c->d_cpos.as<uint64_t>(), *hpos = c->d_chpos.as<uint64_t>();
     uint64_t *bsum = c->d_cbsum.as<uint64_t>(), *hbsum = bsum + nb + 1;
     if (nb) k_cmp_sizes<<<(uint32_t)nb, kCmpBlock, 0, s>>>(c->d_kdout.as<gck_rec>(), n, pos, hpos, bsum, hbsum);
-    k_cmp_top<<<1, 64, 0, s>>>(bsum, hbsum, nb);
+    k_cmp_top<<<1, 1024, 0, s>>>(bsum, hbsum, nb);
     k_cmp_add<<<(uint32_t)((n + 1 + 255) / 256), 256, 0, s>>>(pos, hpos, bsum, hbsum, n, nb);
     uint64_t tot[3] = {0, 0, 0};  // data bytes, hint bytes, pos[1]
     uint32_t nf = 0;
