@@ -1,0 +1,14 @@
+"""Device keydir build (gck_ctx_keydir) on C3: device ms of three builds."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+import gocask_amd as g  # noqa: E402
+
+ctx = g.ReplayContext()
+ctx.encode(**bench.CONFIGS["c3"])
+ctx.run()
+for _ in range(3):
+    n, ms = ctx.keydir(fetch=False)
+    print("keydir_ms", round(ms, 3), "live", n, flush=True)
