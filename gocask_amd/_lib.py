@@ -269,6 +269,11 @@ def load_diag():
     D.gck_diag_stream_read.argtypes = [vp, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
     D.gck_diag_stream_pattern.restype = ctypes.c_int
     D.gck_diag_stream_pattern.argtypes = [vp, ctypes.c_int, ctypes.c_int, P(ctypes.c_double), P(ctypes.c_double)]
+    D.gck_diag_stream_blocks.restype = ctypes.c_int
+    D.gck_diag_stream_blocks.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, P(ctypes.c_double),
+                                         P(ctypes.c_double)]
+    D.gck_diag_clock_read.restype = ctypes.c_int
+    D.gck_diag_clock_read.argtypes = [vp, vp, ctypes.c_uint32]
     D.gck_diag_chunks.restype = ctypes.c_int
     D.gck_diag_chunks.argtypes = [vp, vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]
     D.gck_diag_multi_resolve.restype = ctypes.c_int

@@ -640,6 +640,28 @@ class ReplayContext:
         check(_lib.load_diag().gck_diag_stream_read(self._h, iters, ctypes.byref(ms), ctypes.byref(gbs)))
         return ms.value, gbs.value
 
+    def stream_blocks_ceiling(self, iters=10, static_eighths=4, stamp=False):
+        """The XCD-balanced stream ceiling (measurement helper,
+        libgocask_diag.so): k_crc_rows' geometry and work assignment -- 64-row
+        blocks, half static, half from an atomic queue -- without its compute.
+        (ms per pass, GB/s); stamp: the last pass leaves per-wavefront clock
+        stamps for clock_stamps()."""
+        ms = ctypes.c_double()
+        gbs = ctypes.c_double()
+        check(_lib.load_diag().gck_diag_stream_blocks(self._h, iters, static_eighths, int(bool(stamp)),
+                                                      ctypes.byref(ms), ctypes.byref(gbs)))
+        return ms.value, gbs.value
+
+    @staticmethod
+    def clock_stamps():
+        """(stamps u64[W, 4] = clock, real time at start; clock, real time at
+        end; xcc u32[W]) of the last stamped stream_blocks_ceiling pass."""
+        w = 16384
+        st = np.zeros(4 * w, dtype=np.uint64)
+        xcc = np.zeros(w, dtype=np.uint32)
+        check(_lib.load_diag().gck_diag_clock_read(st.ctypes.data, xcc.ctypes.data, w))
+        return st.reshape(w, 4), xcc
+
     def read_file(self, file, off=0, length=None, out=None):
         n = length
         buf = np.zeros(n, dtype=np.uint8) if out is None else out

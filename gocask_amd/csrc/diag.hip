@@ -102,6 +102,97 @@ __global__ __launch_bounds__(1024) void k_stream_rows_nt(const uint8_t *__restri
     if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// The XCD-balanced stream ceiling: k_crc_rows' geometry and work assignment
+// with its compute removed -- 1024-thread workgroups, one per CU (the 160 KiB
+// of LDS declared, as k_crc_rows' tables, so occupancy matches), 64-row blocks,
+// the first static_eighths / 8 of the full rounds static (wavefront w of W
+// takes blocks k W + w), the rest claimed from an atomic queue two blocks at a
+// time, one row's four 16 B non-temporal buffer loads (whole KiB per
+// instruction) issued before the previous row is consumed.  A static grid
+// stride (k_stream_read) leaves XCDs that finish early idle while others still
+// read (in-kernel stamps); the queue keeps every XCD busy to
+// the end, as in k_crc_rows.  STAMP: each wavefront stamps (shader clock,
+// 100 MHz real time) at start and end plus its XCC id into g_dclk.
+constexpr uint32_t kDclkWaves = 16384;
+__device__ uint64_t g_dclk[4 * kDclkWaves];
+__device__ uint32_t g_dxcc[kDclkWaves];
+
+template <bool STAMP>
+__global__ __launch_bounds__(1024) void k_stream_blocks(const uint8_t *__restrict__ arena, uint64_t n_rows,
+                                                        uint32_t *__restrict__ queue, uint32_t *sink,
+                                                        uint32_t static_eighths) {
+    __shared__ uint32_t lds[40960];
+    uint64_t t0 = 0, r0 = 0;
+    if constexpr (STAMP) {
+        t0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    constexpr uint32_t kRowsPerBlock = 64, kClaimBlocks = 2;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t s_rel = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint64_t n_blocks = (n_rows + kRowsPerBlock - 1) / kRowsPerBlock;
+    const uint32_t W = gridDim.x * 16;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * 16 + (threadIdx.x >> 6)));
+    const uint32_t n_static = (uint32_t)(n_blocks / W) * static_eighths / 8;
+    uint32_t st_k = 0, last = kClaimBlocks - 1;
+    auto grab = [&]() -> uint64_t {
+        if (st_k < n_static) return (uint64_t)(st_k++) * W + w;
+        if (last % kClaimBlocks == kClaimBlocks - 1) {
+            uint32_t v = 0;
+            if (lane == 0) v = atomicAdd(queue, 1u);
+            last = n_static * W + kClaimBlocks * (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        } else {
+            ++last;
+        }
+        return last;
+    };
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    auto issue = [&](uint64_t row, v4u (&v)[4]) {
+        const uint32_t r = min((uint32_t)row, (uint32_t)(n_rows - 1));
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena + (uint64_t)r * 4096), 0, 4096, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, s_rel + 1024 * k, 0, 2);
+    };
+    uint32_t acc = 0;
+    uint64_t q = grab();
+    if (q < n_blocks) {
+        v4u A[4], B[4];
+        issue(q * kRowsPerBlock, A);
+        for (;;) {
+            const uint64_t qn = grab();
+            const uint64_t rb = q * kRowsPerBlock;
+            for (uint32_t j = 0; j < kRowsPerBlock; j += 2) {
+                issue(rb + j + 1, B);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc ^= A[k].x ^ A[k].y ^ A[k].z ^ A[k].w;
+                issue(j + 2 < kRowsPerBlock ? rb + j + 2 : qn * kRowsPerBlock, A);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc ^= B[k].x ^ B[k].y ^ B[k].z ^ B[k].w;
+            }
+            if (qn >= n_blocks) break;
+            q = qn;
+        }
+    }
+    if (acc == 0x9E3779B9u) {
+        lds[threadIdx.x] = acc;
+        sink[0] = lds[(threadIdx.x + 1) & 1023];
+    }
+    if constexpr (STAMP) {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t wi = blockIdx.x * 16 + (threadIdx.x >> 6);
+        if (lane == 0 && wi < kDclkWaves) {
+            g_dclk[4 * wi] = t0;
+            g_dclk[4 * wi + 1] = r0;
+            g_dclk[4 * wi + 2] = t1;
+            g_dclk[4 * wi + 3] = r1;
+            g_dxcc[wi] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID[3:0]
+        }
+    }
+}
+
 // Random-access probes with k_walk's access shape (a 16 B load per hop):
 // DEP = each lane's next address depends on the bytes it just loaded (a chain
 // walk); otherwise the lane's hops are independent (8 loads in flight).
@@ -276,6 +367,52 @@ extern "C" int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter
     const double per = ms / iters;
     if (ms_per_iter) *ms_per_iter = per;
     if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
+    return GCK_OK;
+}
+
+extern "C" int gck_diag_stream_blocks(gck_ctx *ctx, int iters, uint32_t static_eighths, int stamp,
+                                      double *ms_per_iter, double *gbs) {
+    if (!ctx || iters <= 0 || static_eighths > 8) return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    if (!c->n_rows) return GCK_EINVAL;
+    if (int rc = c->d_queue.ensure(kQueueSlots * 4 + 64)) return rc;
+    uint32_t *queue = c->d_queue.as<uint32_t>() + kQueueSlots;  // a slot of its own past the product's queues
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    auto launch = [&](bool st) {
+        (void)hipMemsetAsync(queue, 0, 4, c->stream);
+        if (st)
+            k_stream_blocks<true><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, queue, sink,
+                                                                   static_eighths);
+        else
+            k_stream_blocks<false><<<c->n_cu, 1024, 0, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, queue, sink,
+                                                                    static_eighths);
+    };
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    launch(false);  // warm-up
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) launch(stamp && i == iters - 1);
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    const double per = ms / iters;
+    if (ms_per_iter) *ms_per_iter = per;
+    if (gbs) *gbs = (double)c->arena_len / (per * 1e-3) / 1e9;
+    return GCK_OK;
+}
+
+// The stamps of the last stamped k_stream_blocks launch: 4 u64 per wavefront
+// (clock, real time at start; clock, real time at end) and its XCC id.
+extern "C" int gck_diag_clock_read(uint64_t *stamps, uint32_t *xcc, uint32_t cap_waves) {
+    if (!stamps || !xcc || cap_waves < kDclkWaves) return GCK_EINVAL;
+    GCK_HIP(hipMemcpyFromSymbol(stamps, HIP_SYMBOL(g_dclk), sizeof(uint64_t) * 4 * kDclkWaves, 0,
+                                hipMemcpyDeviceToHost));
+    GCK_HIP(hipMemcpyFromSymbol(xcc, HIP_SYMBOL(g_dxcc), sizeof(uint32_t) * kDclkWaves, 0, hipMemcpyDeviceToHost));
     return GCK_OK;
 }
 

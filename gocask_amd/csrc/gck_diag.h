@@ -14,6 +14,16 @@ extern "C" {
 /* A plain streaming read of the context's resident arena (16 B per lane,
  * non-temporal loads): ms per pass and GB/s. */
 int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *gbs);
+/* The XCD-balanced stream ceiling: k_crc_rows' geometry and work assignment
+ * (64-row blocks, static_eighths / 8 of the full rounds static, the rest from
+ * an atomic queue) without its compute.  stamp: the last pass records
+ * per-wavefront clock stamps (gck_diag_clock_read). */
+int gck_diag_stream_blocks(gck_ctx *ctx, int iters, uint32_t static_eighths, int stamp, double *ms_per_iter,
+                           double *gbs);
+/* Stamps of the last stamped gck_diag_stream_blocks pass: per wavefront 4 u64
+ * (shader clock, 100 MHz real time at start; the same at end) and its XCC id;
+ * cap_waves >= 16384. */
+int gck_diag_clock_read(uint64_t *stamps, uint32_t *xcc, uint32_t cap_waves);
 /* Read probes over the arena: 0 = the streaming read with the default cache
  * policy, 15 = with non-temporal loads (gck_diag_stream_read's kernel), 1 = a
  * lane-contiguous 64 B slab layout (lane stride 64 B), 2 = same geometry

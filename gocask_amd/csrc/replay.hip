@@ -916,8 +916,16 @@ __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *_
 constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
 constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
 constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue claim
-constexpr uint32_t kStaticEighths = 4;     // eighths of k_crc_rows' full rounds assigned statically
+#ifndef GCK_STATIC_EIGHTHS
+#define GCK_STATIC_EIGHTHS 4
+#endif
+constexpr uint32_t kStaticEighths = GCK_STATIC_EIGHTHS;     // eighths of k_crc_rows' full rounds assigned statically
 constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the records (k_crc_rows)
+#ifdef GCK_XP_EBLK
+constexpr uint64_t kEpBytes = 24;  // (c, pre) + the end block
+#else
+constexpr uint64_t kEpBytes = 8;
+#endif
 
 // Diagnostic build only (make EXTRA=-DGCK_CLOCK_STAMPS OUT=../var/...): every
 // wavefront of k_crc_rows and of k_clk_stream stamps the shader clock and the
@@ -928,9 +936,11 @@ constexpr uint64_t kEpScratch = 256 * 64;  // (c, pre) scratch slots past the re
 #ifdef GCK_CLOCK_STAMPS
 constexpr uint32_t kClkWaves = 16384;
 __device__ uint64_t g_clk[2][4 * kClkWaves];
+__device__ uint32_t g_clk_xcc[2][kClkWaves];
 __device__ __forceinline__ void clk_put(int which, uint32_t wi, uint64_t t0, uint64_t r0) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0 && wi < kClkWaves) {
+        g_clk_xcc[which][wi] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID[3:0]
         u32x4 a, b;
         a.x = (uint32_t)t0, a.y = (uint32_t)(t0 >> 32), a.z = (uint32_t)r0, a.w = (uint32_t)(r0 >> 32);
         b.x = (uint32_t)t1, b.y = (uint32_t)(t1 >> 32), b.z = (uint32_t)r1, b.w = (uint32_t)(r1 >> 32);
@@ -1034,7 +1044,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    uint32_t *__restrict__ rend_scratch,
                                                    uint32_t *__restrict__ queue,
                                                    const uint64_t *__restrict__ rec_off,
-                                                   const uint2 *__restrict__ rec_kv, uint64_t row0) {
+                                                   const uint2 *__restrict__ rec_kv, uint64_t row0
+#ifdef GCK_XP_EBLK
+                                                   , uint8_t *__restrict__ out_blk
+#endif
+                                                   ) {
     constexpr int NR = 1;                     // rows per step (two measured slower: 5.70 vs 5.64 ms)
     constexpr int kSteps = kBlockRows / NR;  // steps per block
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
@@ -1062,6 +1076,21 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         v.y = pv;
         __builtin_amdgcn_raw_buffer_store_b64(v, ep_rsrc, (int)off, 0, 0);
     };
+#ifdef GCK_XP_EBLK
+    // experiment: each record end's 16 B block beside its (c, pre)
+    __amdgpu_buffer_rsrc_t blk_rsrc = make_rsrc(out_blk, 0x7FFFFFF0);
+    auto store_blk = [&](uint32_t off8, const u32x4 &v) {
+        __builtin_amdgcn_raw_buffer_store_b128(v, blk_rsrc, (int)(off8 == kDrop ? kDrop : off8 * 2u), 0, 0);
+    };
+    auto pick_blk = [&](const uint32_t *wv, uint32_t b) {
+        u32x4 v;
+        v.x = b == 0 ? wv[0] : b == 1 ? wv[4] : b == 2 ? wv[8] : wv[12];
+        v.y = b == 0 ? wv[1] : b == 1 ? wv[5] : b == 2 ? wv[9] : wv[13];
+        v.z = b == 0 ? wv[2] : b == 1 ? wv[6] : b == 2 ? wv[10] : wv[14];
+        v.w = b == 0 ? wv[3] : b == 1 ? wv[7] : b == 2 ? wv[11] : wv[15];
+        return v;
+    };
+#endif
 
     // Work assignment: the first rounds are static (wavefront w of W takes
     // blocks k W + w, k < n_static: every wavefront streams its share with no
@@ -1270,6 +1299,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 const uint32_t idx =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
                 store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
+#ifdef GCK_XP_EBLK
+                store_blk(m ? (ra + idx - ra0) * 8u : kDrop, pick_blk(w[i], (uint32_t)__builtin_ctz(m | 16u) & 3u));
+#endif
             } else {
                 // a slab with 2..4 record ends (records under 64 B): ids by
                 // an exclusive count over the lanes, four stores per lane
@@ -1279,6 +1311,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
                     store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
+#ifdef GCK_XP_EBLK
+                    store_blk(q < n ? (ra + ex + q - ra0) * 8u : kDrop, pick_blk(w[i], (uint32_t)__builtin_ctz(mm | 16u) & 3u));
+#endif
                     mm &= mm - 1;
                 }
             }
@@ -1321,6 +1356,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
+#ifdef GCK_XP_EBLK
+        blk_rsrc = make_rsrc(out_blk + (uint64_t)ra0 * 16, 0x7FFFFFF0);
+#endif
         uint32_t nibs[8];
         build_nibs(row_b, ra0, pc.re, &bc, nibs);
         // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
@@ -2063,7 +2101,11 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     k_crc_rows<<<grid, 1024, 0, s>>>(
         c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
-        c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0);
+        c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0
+#ifdef GCK_XP_EBLK
+        , c->d_ep.as<uint8_t>() + (cap + kEpScratch) * 8
+#endif
+        );
     return GCK_OK;
 }
 
@@ -2086,7 +2128,7 @@ static int ensure_records(Ctx *c, uint64_t nr) {
     nr = nr ? nr : 1;
     int rc;
     if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_kv.ensure(nr * 8)) ||
-        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_ep.ensure((nr + kEpScratch) * 8)) ||
+        (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_ep.ensure((nr + kEpScratch) * kEpBytes)) ||
         (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
         return rc;
     return GCK_OK;
@@ -3063,6 +3105,14 @@ int gck_xp_clock_read(int which, uint64_t *out) {
     GCK_HIP(hipDeviceSynchronize());
     GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(uint64_t) * 4 * kClkWaves,
                                 sizeof(uint64_t) * 4 * kClkWaves * which));
+    return GCK_OK;
+}
+// the XCC id of each stamped wavefront (kClkWaves entries)
+int gck_xp_clock_xcc(int which, uint32_t *out) {
+    if (which < 0 || which > 1 || !out) return GCK_EINVAL;
+    GCK_HIP(hipDeviceSynchronize());
+    GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_xcc), sizeof(uint32_t) * kClkWaves,
+                                sizeof(uint32_t) * kClkWaves * which));
     return GCK_OK;
 }
 // iters back-to-back stamped stream reads of the context's arena; *ms = per launch
