@@ -61,6 +61,7 @@ EXPORTED = [
 
 
 OPT_KEYS = 1  # gck_opts.flags GCK_OPT_KEYS
+OPT_LIVE = 2  # gck_opts.flags GCK_OPT_LIVE
 
 
 class GckFile(ctypes.Structure):

@@ -79,13 +79,13 @@ def NewInMemory(data: bytes = b""):
     return InMemory(data)
 
 
-def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0, max_resident=0, keys=False):
+def _opts(device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0, max_resident=0, keys=False, live=False):
     o = GckOpts()
     o.device = device
     o.chunk_bytes = chunk_bytes
     o.max_key = max_key
     o.chunk_cap = chunk_cap
-    o.flags = _lib.OPT_KEYS if keys else 0
+    o.flags = (_lib.OPT_KEYS if keys else 0) | (_lib.OPT_LIVE if live else 0)
     o.spec_window = spec_window
     o.max_resident = max_resident
     return o
@@ -240,15 +240,16 @@ def host_unregister(arr):
 
 
 def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_cap=0, spec_window=0,
-           max_resident=0, keys=False):
-    """Host-in/host-out replay through gck_replay.  Returns (records, status)."""
+           max_resident=0, keys=False, live=False):
+    """Host-in/host-out replay through gck_replay.  Returns (records, status);
+    live=True (GCK_OPT_LIVE): the live keydir records instead of every record."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(files)
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
     rc = L.gck_replay(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_key, chunk_cap, spec_window,
-                                                        max_resident, keys)), ctypes.byref(res))
+                                                        max_resident, keys, live)), ctypes.byref(res))
     try:  # (an error return may still hand back memory: freed either way)
         check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
         return _result(res)
@@ -256,10 +257,10 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False):
+def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False, live=False):
     """gck_replay_paths: the same replay of files named by path (read by the
     library with pread into page-locked staging buffers).  Returns (records,
-    status)."""
+    status); live=True (GCK_OPT_LIVE): the live keydir records."""
     L = _lib.load()
     if reset_after is None:
         reset_after = [True] * len(paths)
@@ -269,7 +270,7 @@ def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=
         pa[i].path = p
         pa[i].reset_after = 1 if reset_after[i] else 0
     res = GckResult()
-    rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident, keys)),
+    rc = L.gck_replay_paths(pa, len(enc), ctypes.byref(_opts(device, chunk_bytes, 0, 0, 0, max_resident, keys, live)),
                             ctypes.byref(res))
     try:  # (an error return may still hand back memory: freed either way)
         check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
@@ -278,7 +279,7 @@ def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=
         L.gck_result_free(ctypes.byref(res))
 
 
-def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False):
+def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False, live=False):
     """gck_replay_into: host-in/host-out replay (pipelined over file groups)
     with the tuples written into recs (a REC_DTYPE array; register it with
     host_register for DMA rate).  Returns the status dict; recs[:n] hold the
@@ -289,7 +290,7 @@ def replay_into(files, recs, reset_after=None, device=0, chunk_bytes=0, max_resi
     fa, arrs = _files_struct(files, reset_after)
     res = GckResult()
     rc = L.gck_replay_into(fa, len(arrs), ctypes.byref(_opts(device, chunk_bytes, max_resident=max_resident,
-                                                             keys=keys)),
+                                                             keys=keys, live=live)),
                            recs.ctypes.data if recs.size else None, recs.size, ctypes.byref(res))
     try:
         check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))

@@ -44,10 +44,43 @@ constexpr int kHops = 4;          // extra headers a speculative start must chai
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 constexpr uint32_t kNibBase = 32768;
 
-// ---------------------------------------------------------------- helpers ---
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// Diagnostic build only (make EXTRA=-DGCK_CLOCK_STAMPS OUT=../var/...): every
+// wavefront of k_crc_rows, k_clk_stream, k_spec_entry, k_walk, k_compact and
+// k_finalize stamps the shader clock and the
+// 100 MHz real-time counter when its loop starts and when it leaves, into
+// buffers of their own that nothing else reads; the in-kernel clock is
+// d(shader clock) / d(real time) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
+// gck_xp_clock() reads them back.  The product build has no stamp.
+#ifdef GCK_CLOCK_STAMPS
+constexpr uint32_t kClkWaves = 16384;
+constexpr int kClkKinds = 6;  // 0 k_crc_rows, 1 k_clk_stream, 2 k_spec_entry, 3 k_walk, 4 k_compact, 5 k_finalize
+__device__ uint64_t g_clk[kClkKinds][4 * kClkWaves];
+__device__ uint32_t g_clk_xcc[kClkKinds][kClkWaves];
+__device__ __forceinline__ void clk_put(int which, uint32_t wi, uint64_t t0, uint64_t r0) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0 && wi < kClkWaves) {
+        g_clk_xcc[which][wi] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID[3:0]
+        u32x4 a, b;
+        a.x = (uint32_t)t0, a.y = (uint32_t)(t0 >> 32), a.z = (uint32_t)r0, a.w = (uint32_t)(r0 >> 32);
+        b.x = (uint32_t)t1, b.y = (uint32_t)(t1 >> 32), b.z = (uint32_t)r1, b.w = (uint32_t)(r1 >> 32);
+        u32x4 *d = reinterpret_cast<u32x4 *>(&g_clk[which][4 * wi]);
+        d[0] = a;
+        d[1] = b;
+    }
+}
+#define GCK_CLK_BEGIN() const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime()
+#define GCK_CLK_END(which, wi) clk_put(which, wi, clk_t0, clk_r0)
+#else
+#define GCK_CLK_BEGIN() ((void)0)
+#define GCK_CLK_END(which, wi) ((void)0)
+#endif
+
+
+// ---------------------------------------------------------------- helpers ---
 
 // Raw buffer resource over [p, p + bytes) (gfx9 dword3: untyped, bounds-checked).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *p, uint32_t bytes) {
@@ -173,6 +206,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
     if (c >= n_chunks) return;
+    GCK_CLK_BEGIN();
     const uint32_t f = ch_file[c];
     const uint64_t cs = ch_start[c], ce = ch_end[c], base = fbase[f], len = flen[f];
     const uint32_t mk = min(max_key, 65535u);
@@ -327,6 +361,7 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         }
     }
     if (lane == 0) ch_entry[c] = found;
+    GCK_CLK_END(2, c);
 }
 
 // The stage: per chunk, cap record slots + 1 scratch slot (records past cap
@@ -407,6 +442,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
                                               uint64_t *ch_wend, uint2 *s_kv, uint32_t cap,
                                               uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end) {
+    GCK_CLK_BEGIN();
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end) return;
     const uint32_t f = ch_file[c];
@@ -414,6 +450,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
     const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
     walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
                     ch_wend);
+    GCK_CLK_END(3, (c - c_begin) >> 6);
 }
 
 // Consistency of chunk c against j, the nearest earlier chunk of its file with
@@ -822,6 +859,7 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
     if (c >= n_chunks) return;
+    GCK_CLK_BEGIN();
     // everything a chunk needs in one round trip: its entry, count, record
     // base and file, and the first kPreBatches batches of its stage (slots
     // past the count or the capacity read the chunk's scratch slot, which
@@ -873,6 +911,7 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
         uint64_t exit, tpos;
         walk_chain(arena, base, flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
     }
+    GCK_CLK_END(4, c);
 }
 
 __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uint2 *rec_kv, uint64_t r) {
@@ -927,30 +966,7 @@ constexpr uint64_t kEpBytes = 24;  // (c, pre) + the end block
 constexpr uint64_t kEpBytes = 8;
 #endif
 
-// Diagnostic build only (make EXTRA=-DGCK_CLOCK_STAMPS OUT=../var/...): every
-// wavefront of k_crc_rows and of k_clk_stream stamps the shader clock and the
-// 100 MHz real-time counter when its loop starts and when it leaves, into
-// buffers of their own that nothing else reads; the in-kernel clock is
-// d(shader clock) / d(real time) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
-// gck_xp_clock() reads them back.  The product build has no stamp.
 #ifdef GCK_CLOCK_STAMPS
-constexpr uint32_t kClkWaves = 16384;
-__device__ uint64_t g_clk[2][4 * kClkWaves];
-__device__ uint32_t g_clk_xcc[2][kClkWaves];
-__device__ __forceinline__ void clk_put(int which, uint32_t wi, uint64_t t0, uint64_t r0) {
-    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
-    if ((threadIdx.x & 63) == 0 && wi < kClkWaves) {
-        g_clk_xcc[which][wi] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID[3:0]
-        u32x4 a, b;
-        a.x = (uint32_t)t0, a.y = (uint32_t)(t0 >> 32), a.z = (uint32_t)r0, a.w = (uint32_t)(r0 >> 32);
-        b.x = (uint32_t)t1, b.y = (uint32_t)(t1 >> 32), b.z = (uint32_t)r1, b.w = (uint32_t)(r1 >> 32);
-        u32x4 *d = reinterpret_cast<u32x4 *>(&g_clk[which][4 * wi]);
-        d[0] = a;
-        d[1] = b;
-    }
-}
-#define GCK_CLK_BEGIN() const uint64_t clk_t0 = __builtin_amdgcn_s_memtime(), clk_r0 = __builtin_amdgcn_s_memrealtime()
-#define GCK_CLK_END(which, wi) clk_put(which, wi, clk_t0, clk_r0)
 // the plain non-temporal stream read (diag.hip's k_stream_read<true>), stamped
 __global__ __launch_bounds__(256) void k_clk_stream(const uint4 *__restrict__ p, uint64_t n16, uint32_t *sink) {
     GCK_CLK_BEGIN();
@@ -969,9 +985,6 @@ __global__ __launch_bounds__(256) void k_clk_stream(const uint4 *__restrict__ p,
     if (acc == 0x9E3779B9u) sink[0] = acc;
     GCK_CLK_END(1, blockIdx.x * 4 + (threadIdx.x >> 6));
 }
-#else
-#define GCK_CLK_BEGIN() ((void)0)
-#define GCK_CLK_END(which, wi) ((void)0)
 #endif
 
 template <int CTRL, int ROWMASK>
@@ -1729,6 +1742,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // issued together and waited for, then the compute.  (Loading the table
     // two iterations ahead and the dependent loads one ahead measured slower:
     // 0.517-0.520 vs 0.496-0.498 ms)
+    GCK_CLK_BEGIN();
     uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
     Rec cur, nxt;
     if (base < re) load_rec(base, cur);
@@ -1740,6 +1754,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         compute(cur, g, dc, base);
         cur = nxt;
     }
+    GCK_CLK_END(5, blockIdx.x * 4 + (threadIdx.x >> 6));
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
     __shared__ uint32_t blk_rej;
@@ -3019,11 +3034,21 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     return out->status;
 }
 
+// GCK_OPT_LIVE: the live keydir instead of every record -- each file group's
+// device keydir (tombstones kept) packed as it finishes, then merged in walk
+// order on the device: gck_replay_multi's path with the one device of the
+// options (no RCCL: every pair is a device copy).
+static bool want_live(const gck_opts *o) { return o && (o->flags & GCK_OPT_LIVE); }
+static int replay_live(const Src *v, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
+    return replay_multi(v, nfiles, std::vector<int>{opts->device}, opts, out, false);
+}
+
 int gck_replay(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out) {
     if (!out) return GCK_EINVAL;
     memset(out, 0, sizeof(*out));
     if (nfiles && !files) return GCK_EINVAL;
     const std::vector<Src> v = mem_srcs(files, nfiles);
+    if (want_live(opts)) return replay_live(v.data(), nfiles, opts, out);
     return replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
 }
 
@@ -3031,6 +3056,23 @@ int gck_replay_into(const gck_file *files, uint32_t nfiles, const gck_opts *opts
                     gck_result *out) {
     if (!out || (cap && !dst) || (nfiles && !files)) return GCK_EINVAL;
     const std::vector<Src> v = mem_srcs(files, nfiles);
+    if (want_live(opts)) {
+        memset(out, 0, sizeof(*out));
+        const int rc = replay_live(v.data(), nfiles, opts, out);
+        if (rc != GCK_OK && rc != GCK_EUNEXPECTED_EOF) return rc;
+        gck_rec *h = out->recs;
+        out->recs = nullptr;
+        if (out->n > cap) {
+            res_free(h);
+            res_free(out->keys);
+            out->keys = nullptr;
+            out->keys_len = 0;
+            return GCK_EINVAL;
+        }
+        if (out->n) memcpy(dst, h, out->n * sizeof(gck_rec));
+        res_free(h);
+        return rc;
+    }
     return replay_grouped(v.data(), nfiles, opts, true, dst, cap, out);
 }
 
@@ -3041,7 +3083,8 @@ int gck_replay_paths(const gck_path *files, uint32_t nfiles, const gck_opts *opt
     std::vector<Src> v;
     int rc = open_srcs(files, nfiles, v);
     if (rc) return rc;
-    rc = replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
+    rc = want_live(opts) ? replay_live(v.data(), nfiles, opts, out)
+                         : replay_grouped(v.data(), nfiles, opts, false, nullptr, 0, out);
     close_srcs(v);
     return rc;
 }
@@ -3096,12 +3139,12 @@ extern "C" {
 // k_clk_stream's; out receives 4 u64 per wavefront (clock, real time at the
 // loop start, then at the end), kClkWaves entries; zeroed by reset.
 int gck_xp_clock_reset(void) {
-    static const uint64_t zero[2][4 * kClkWaves] = {};
+    static const uint64_t zero[kClkKinds][4 * kClkWaves] = {};
     GCK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_clk), zero, sizeof zero));
     return GCK_OK;
 }
 int gck_xp_clock_read(int which, uint64_t *out) {
-    if (which < 0 || which > 1 || !out) return GCK_EINVAL;
+    if (which < 0 || which >= kClkKinds || !out) return GCK_EINVAL;
     GCK_HIP(hipDeviceSynchronize());
     GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(uint64_t) * 4 * kClkWaves,
                                 sizeof(uint64_t) * 4 * kClkWaves * which));
@@ -3109,7 +3152,7 @@ int gck_xp_clock_read(int which, uint64_t *out) {
 }
 // the XCC id of each stamped wavefront (kClkWaves entries)
 int gck_xp_clock_xcc(int which, uint32_t *out) {
-    if (which < 0 || which > 1 || !out) return GCK_EINVAL;
+    if (which < 0 || which >= kClkKinds || !out) return GCK_EINVAL;
     GCK_HIP(hipDeviceSynchronize());
     GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk_xcc), sizeof(uint32_t) * kClkWaves,
                                 sizeof(uint32_t) * kClkWaves * which));

@@ -79,6 +79,19 @@ typedef struct gck_rec {
  * the records' key bytes (gck_result.keys), so a caller that never maps the
  * files (gck_replay_paths) can fill its keydir map. */
 #define GCK_OPT_KEYS 1u
+/* gck_opts.flags: gck_replay / gck_replay_into / gck_replay_paths return the
+ * live keydir instead of every record (SURVEY.md §8f f1 on the one-GPU drop-in
+ * path; replaces applying every record with keyDir.set / unset,
+ * core/keydir.go:22-49): one gck_rec per live key -- its last record in walk
+ * order, a Put (a key whose last record is a Delete is absent) -- with
+ * rec.file the walk index; with GCK_OPT_KEYS the live keys' bytes in the
+ * order of the records.  Each file group's keydir is built on the device as
+ * the group replays and the groups are merged there in walk order (the
+ * one-device form of gck_replay_multi, no RCCL), so only live entries cross
+ * PCIe and the caller's map takes one insert per live key.  status, err_*,
+ * files_walked, final_last_offset and n_crc_fail (rejects among all replayed
+ * records) as without the flag. */
+#define GCK_OPT_LIVE 2u
 
 /* Tuning knobs; zero fields take the defaults.  Results never depend on them
  * (GCK_OPT_KEYS adds an output). */

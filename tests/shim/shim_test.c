@@ -29,6 +29,12 @@
  * SHIM_PATHS=1: gck_replay_paths (with SHIM_MULTI=1 gck_replay_multi_paths)
  * -- the library opens and reads the files itself (the shim maps them only
  * to print keys, never when timing).
+ * SHIM_LIVE=1: GCK_OPT_LIVE -- the single-GPU call returns the live keydir
+ * (the device keydir, merged over the file groups) instead of every record.
+ * Timing mode also fills the keydir map as the Go shim does after the call
+ * (map_fill.cpp: a std::unordered_map<std::string, entry>, the Go map's
+ * proxy; every record set / unset in walk order, or one insert per live
+ * key), with the key bytes from GCK_OPT_KEYS, and includes it in open_ms.
  */
 #define _GNU_SOURCE
 #include <dirent.h>
@@ -42,6 +48,8 @@
 #include <unistd.h>
 
 #include "gocask_hip.h"
+
+double shim_map_fill(const gck_rec *recs, uint64_t n, const uint8_t *keys, int live, uint64_t *n_live);
 
 typedef struct {
     char name[256]; /* DiskFile.Name(): base name without the extension */
@@ -154,6 +162,7 @@ int main(int argc, char **argv) {
     const int timing = getenv("SHIM_TIME") && atoi(getenv("SHIM_TIME"));
     const int multi = getenv("SHIM_MULTI") && atoi(getenv("SHIM_MULTI"));
     const int by_path = getenv("SHIM_PATHS") && atoi(getenv("SHIM_PATHS"));
+    const int live_mode = getenv("SHIM_LIVE") && atoi(getenv("SHIM_LIVE"));
     if (getenv("SHIM_PIN")) g_pin = atoi(getenv("SHIM_PIN"));
     if (by_path) g_pin = 0;
     if (by_path && timing) g_map = 0;
@@ -185,6 +194,9 @@ int main(int argc, char **argv) {
     int rc = GCK_OK;
     gck_result res;
     memset(&res, 0, sizeof res);
+    gck_opts opts;
+    memset(&opts, 0, sizeof opts);
+    opts.flags = (live_mode ? GCK_OPT_LIVE : 0u) | (timing ? GCK_OPT_KEYS : 0u);
     if (g_n) { /* zero files: no replay, no files[0] */
         gck_file *gf = calloc(g_n, sizeof(gck_file));
         for (size_t i = 0; i < g_n; ++i) {
@@ -200,16 +212,16 @@ int main(int argc, char **argv) {
             }
             if (multi) {
                 const int32_t dev0 = 0;
-                rc = gck_replay_multi_paths(gp, (uint32_t)g_n, &dev0, 1, NULL, &res);
+                rc = gck_replay_multi_paths(gp, (uint32_t)g_n, &dev0, 1, &opts, &res);
             } else {
-                rc = gck_replay_paths(gp, (uint32_t)g_n, NULL, &res);
+                rc = gck_replay_paths(gp, (uint32_t)g_n, &opts, &res);
             }
             free(gp);
         } else if (multi) {
             const int32_t dev0 = 0;
-            rc = gck_replay_multi(gf, (uint32_t)g_n, &dev0, 1, NULL, &res);
+            rc = gck_replay_multi(gf, (uint32_t)g_n, &dev0, 1, &opts, &res);
         } else {
-            rc = gck_replay(gf, (uint32_t)g_n, NULL, &res);
+            rc = gck_replay(gf, (uint32_t)g_n, &opts, &res);
         }
         free(gf);
         if (rc != GCK_OK && rc != GCK_EUNEXPECTED_EOF) {
@@ -223,17 +235,24 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < g_n; ++i) bytes += g_files[i].len;
         const uint64_t n = res.n, fail = res.n_crc_fail;
         const uint32_t last = res.final_last_offset, groups = res.n_groups, resident = res.n_resident;
+        /* the Go shim's keydir fill (records set / unset in walk order, or
+         * one insert per live entry), keys from GCK_OPT_KEYS */
+        uint64_t n_map = 0;
+        const double fill_ms = n ? shim_map_fill(res.recs, n, res.keys, live_mode || multi, &n_map) : 0.0;
+        const double t2b = now_ms();
         if (g_n) gck_result_free(&res);
         const double t3 = now_ms();
         release_files();
         const double t4 = now_ms();
         printf("{\"files\": %zu, \"bytes\": %llu, \"status\": %d, \"records\": %llu, \"crc_rejects\": %llu, "
                "\"last_offset\": %u, \"groups\": %u, \"resident\": %u, \"walk_mmap_register_ms\": %.2f, "
-               "\"replay_ms\": %.2f, \"free_ms\": %.2f, \"unregister_unmap_ms\": %.2f, \"open_ms\": %.2f, "
-               "\"open_gib_s\": %.3f, \"multi\": %d, \"mode\": \"%s\"}\n",
+               "\"replay_ms\": %.2f, \"map_fill_ms\": %.2f, \"map_entries\": %llu, \"free_ms\": %.2f, "
+               "\"unregister_unmap_ms\": %.2f, \"open_ms\": %.2f, "
+               "\"open_gib_s\": %.3f, \"multi\": %d, \"live\": %d, \"mode\": \"%s\"}\n",
                g_n, (unsigned long long)bytes, rc, (unsigned long long)n, (unsigned long long)fail, last, groups,
-               resident, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t4 - t0, bytes / ((t4 - t0) * 1e-3) / (1 << 30), multi,
-               by_path ? "paths" : g_pin ? "pinned" : "pageable");
+               resident, t1 - t0, t2 - t1, fill_ms, (unsigned long long)n_map, t3 - t2b, t4 - t3, t4 - t0,
+               bytes / ((t4 - t0) * 1e-3) / (1 << 30), multi, live_mode, by_path ? "paths" : g_pin ? "pinned" : "pageable");
+        (void)fill_ms;
         free(g_files);
         return 0;
     }

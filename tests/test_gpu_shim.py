@@ -26,9 +26,9 @@ def shim():
     return SHIM
 
 
-def run(shim, d, active=None, multi=False, mode="pinned"):
+def run(shim, d, active=None, multi=False, mode="pinned", live=False):
     env = dict(os.environ, SHIM_MULTI="1" if multi else "0", SHIM_PIN="1" if mode == "pinned" else "0",
-               SHIM_PATHS="1" if mode == "paths" else "0")
+               SHIM_PATHS="1" if mode == "paths" else "0", SHIM_LIVE="1" if live else "0")
     p = subprocess.run([shim, str(d)] + ([active] if active else []), capture_output=True, text=True, timeout=120,
                        env=env)
     assert p.returncode == 0, p.stderr
@@ -135,3 +135,41 @@ def test_shim_pageable_and_by_path_same_keydir(shim, orc, tmp_path, name):
     assert run(shim, tmp_path, meta["active"], mode="pageable") == pinned
     assert run(shim, tmp_path, meta["active"], mode="paths") == pinned
     assert run(shim, tmp_path, meta["active"], mode="paths", multi=True) == pinned
+
+
+@pytest.mark.parametrize("name", ["existing_after_startup", "keys_in_order", "updated_values_across_files",
+                                  "deleted_after_startup", "removed_keys", "datatxt_1000_puts", "crc_fail",
+                                  "partial_write_desync"])
+def test_shim_live_keydir_same_keydir(shim, orc, tmp_path, name):
+    """GCK_OPT_LIVE on the single-GPU drop-in call (SHIM_LIVE=1): the live
+    keydir comes back instead of every record, pinned and by path, and the
+    shim's map equals the records mode's."""
+    meta, files, reset = load_case(name)
+    for w, f in zip(meta["walk"], files):
+        (tmp_path / (w + ".csk")).write_bytes(f.tobytes())
+    pinned = run(shim, tmp_path, meta["active"])
+    assert run(shim, tmp_path, meta["active"], live=True) == pinned
+    assert run(shim, tmp_path, meta["active"], mode="paths", live=True) == pinned
+
+
+def test_shim_timing_mode_fills_the_map(shim, orc, tmp_path):
+    """SHIM_TIME=1 (tools/shim_c3.py): the Open as the shim pays it, map fill
+    included, in both modes; the map holds the oracle keydir's size."""
+    import json
+
+    files, names = orc.gen_corpus(seed=41, val_fixed=0, key_min=8, key_max=16, key_universe=500, tomb_permille=80,
+                                  max_file_size=1 << 18, n_files=4)
+    for f, n in zip(files, names):
+        (tmp_path / (n + ".csk")).write_bytes(f.tobytes())
+    walk = sorted(names)
+    wf = [files[names.index(n)] for n in walk]
+    reset = [i + 1 < len(wf) for i in range(len(wf))]
+    want, _ = orc.replay(wf, reset)
+    n_live = len(orc.keydir(wf, want, reset))
+    for live in ("0", "1"):
+        env = dict(os.environ, SHIM_TIME="1", SHIM_PATHS="1", SHIM_LIVE=live)
+        p = subprocess.run([shim, str(tmp_path)], capture_output=True, text=True, timeout=120, env=env)
+        assert p.returncode == 0, p.stderr
+        d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+        assert d["map_entries"] == n_live and d["live"] == int(live)
+        assert d["records"] == (n_live if live == "1" else len(want))

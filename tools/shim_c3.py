@@ -6,7 +6,10 @@ Walk callback, calls gck_replay (or gck_replay_multi on device 0), frees the
 tuples, unregisters and unmaps.  One JSON line per run; the directory is
 removed at the end.  Modes: by path (gck_replay_paths: the library preads the
 files into its staging buffers), pageable mappings (staged by the library),
-pinned mappings (the shim registers each mmap), pinned + gck_replay_multi.
+pinned mappings (the shim registers each mmap), pinned + gck_replay_multi,
+by path + gck_replay_multi, by path with GCK_OPT_LIVE (mode 5: the live
+keydir instead of every record).  Every mode includes the shim's keydir map
+fill (map_fill.cpp, a C++ unordered_map as the Go map's proxy).
 python tools/shim_c3.py [reps] [number of modes]"""
 import json
 import os
@@ -36,7 +39,7 @@ try:
     shim = os.path.join(ROOT, "tests", "shim", "build", "shim_test")
     out = []
     modes = [dict(SHIM_PATHS="1"), dict(SHIM_PIN="0"), dict(SHIM_PIN="1"), dict(SHIM_PIN="1", SHIM_MULTI="1"),
-             dict(SHIM_PATHS="1", SHIM_MULTI="1")]
+             dict(SHIM_PATHS="1", SHIM_MULTI="1"), dict(SHIM_PATHS="1", SHIM_LIVE="1")]
     if len(sys.argv) > 2:
         modes = modes[:int(sys.argv[2])]
     if os.environ.get("SHIM_MODES"):  # e.g. "0 4": by path, single and multi
