@@ -19,6 +19,16 @@ independent).
 After the timed replays, N>1 runs also time the keydir merge across ranks (the
 path's one exchange step, RCCL all-to-all; reported as "keydir_merge", not
 part of value).  Rank 0 prints one JSON line.
+
+  python bench.py --gpus N --lib-multi   the drop-in multi-GPU path instead:
+       ONE process, a ReplayContext per device holding rank r's C4 shard,
+       the replays from one host thread each, then the library's own keydir
+       exchange + merge (gck_ctx_multi_keydir: RCCL across devices, as
+       gck_replay_multi), reported as "keydir_merge_lib".  More ranks than
+       visible GPUs share them (a loopback rehearsal: device copies instead of
+       RCCL).  The default N>1 run ends with this mode as a child process of
+       rank 0 (after every rank has released its GPU) and reports its
+       keydir_merge_lib beside the torch path's keydir_merge.
 """
 import argparse
 import json
@@ -270,26 +280,118 @@ def encode_workload(ctx, cfg_name, world, rank, files_per_rank=C4_FILES_PER_GPU,
     return ctx.encode(**shard_config(cfg_name, rank))
 
 
-def launcher_cmd(n, port, argv, script=None):
+def launcher_cmd(n, argv, script=None):
     """The torch.distributed.run command that starts n rank processes of this
-    script with the same arguments (one node, rendezvous on 127.0.0.1)."""
-    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__)] + list(argv)
+    script with the same arguments (one node; --standalone: the launcher's
+    own c10d store picks a free port as it binds, on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--standalone", "--nnodes=1", f"--nproc-per-node={n}",
+            "--local-addr=127.0.0.1", script or os.path.abspath(__file__)] + list(argv)
 
 
 def relaunch(n, argv):
     """--gpus N > 1 with no launcher around this process: run the N ranks as a
     child torch.distributed.run (nothing here has touched a GPU yet: only the
     argument parser ran), pass its output through (rank 0 prints the JSON
-    line) and return its exit code."""
-    import socket
+    line) and return its exit code.  A process that was itself started this
+    way and still sees no WORLD_SIZE refuses to start another launcher."""
     import subprocess
 
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
+    if os.environ.get("GCK_BENCH_LAUNCHED"):
+        sys.exit("bench.py: started by bench.py's own launcher but no WORLD_SIZE: refusing a nested relaunch")
     env = dict(os.environ, GCK_BENCH_LAUNCHED="1")
-    return subprocess.run(launcher_cmd(n, port, argv), env=env).returncode
+    return subprocess.run(launcher_cmd(n, argv), env=env).returncode
+
+
+def lib_multi(args):
+    """--lib-multi (see the module docstring): one process, one context per
+    device, the library's own exchange + merge timed.  Prints one JSON line."""
+    import threading
+
+    import torch
+
+    import gocask_amd as g
+
+    n = args.gpus
+    nvis = max(torch.cuda.device_count(), 1)
+    devs = [d % nvis for d in range(n)]
+    ctxs = [g.ReplayContext(device=dv, chunk_bytes=args.chunk_kib << 10) for dv in devs]
+    infos, errs = [None] * n, []
+
+    def each(fn):
+        def wrap(i):
+            try:
+                fn(i)
+            except Exception as e:  # noqa: BLE001  (re-raised below)
+                errs.append(e)
+        th = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+
+    def enc(i):
+        infos[i] = encode_workload(ctxs[i], "c4", n, i, args.c4_files_per_gpu, args.c4_file_mib << 20)
+
+    each(enc)
+    for _ in range(max(1, args.warmup)):
+        each(lambda i: ctxs[i].run())
+    for dv in sorted(set(devs)):
+        torch.cuda.synchronize(dv)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        each(lambda i: ctxs[i].run())
+    elapsed = time.perf_counter() - t0
+    nbytes = sum(c.stats()["bytes"] for c in ctxs)
+    merges = []
+    for _ in range(2):
+        t1 = time.perf_counter()
+        _, st = g.multi_keydir(ctxs, fetch=False)
+        merges.append((time.perf_counter() - t1, st))
+    wall, st = merges[-1]
+    out = {
+        "metric": "device-resident data-file GiB/s CRC-verified+header-decoded, 1 GPU (+2/4/8)",
+        "value": round(nbytes * args.steps / elapsed / GiB, 2),
+        "unit": "GiB/s",
+        "n_gpus": n,
+        "steps": args.steps,
+        "mode": "lib-multi: one process, a context per device, replays from one host thread each",
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "devices": devs,
+        "keydir_merge_lib": dict(ms=round(wall * 1e3, 3), **{k + "_ms": round(v, 3) for k, v in st["ms"].items()},
+                                 live_entries=st["n_live"], global_status=st["status"],
+                                 transport="device copies (loopback)" if len(set(devs)) < n else "RCCL over xGMI",
+                                 note="gck_ctx_multi_keydir: per device the keydir with tombstones packed over the "
+                                      "owners, partitions exchanged in one RCCL group, per-owner merge (the library's "
+                                      "own path behind gck_replay_multi); last of 2 runs; not part of value"),
+    }
+    print(json.dumps(out), flush=True)
+    for c in ctxs:
+        c.close()
+    return 0
+
+
+def lib_multi_child(args):
+    """Rank 0 of an N>1 run, after every rank has released its GPU: the
+    --lib-multi measurement as a child process (its own RCCL communicators
+    over all N devices).  Returns its keydir_merge_lib (or the failure)."""
+    import subprocess
+
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", str(args.gpus), "--lib-multi", "--steps", "2",
+           "--warmup", "1", "--c4-files-per-gpu", str(args.c4_files_per_gpu), "--c4-file-mib", str(args.c4_file_mib),
+           "--chunk-kib", str(args.chunk_kib)]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+                                                          "GROUP_RANK", "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    except subprocess.TimeoutExpired:
+        return dict(error="timeout after 240 s")
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    if p.returncode or not lines:
+        return dict(error=f"rc {p.returncode}: {p.stderr[-400:]}")
+    d = json.loads(lines[-1])
+    return dict(d["keydir_merge_lib"], replay_gibs=d["value"], replay_ms_per_step=d["ms_per_step"])
 
 
 def reduce_over_ranks(dist, elapsed, nbytes, device):
@@ -329,7 +431,12 @@ def main():
                     help="C4: files per rank (16: BASELINE's C4; fewer only for rehearsals)")
     ap.add_argument("--c4-file-mib", type=int, default=2048,
                     help="C4: file size in MiB (2048: BASELINE's C4; smaller only for rehearsals)")
+    ap.add_argument("--lib-multi", action="store_true",
+                    help="one process, a context per device, the library's own keydir exchange (see above)")
+    ap.add_argument("--no-lib-multi", action="store_true", help="N>1: skip the --lib-multi child at the end")
     args = ap.parse_args()
+    if args.lib_multi:
+        sys.exit(lib_multi(args))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch(args.gpus, sys.argv[1:]))
@@ -505,14 +612,19 @@ def main():
             out["host_inclusive"] = host_inclusive(g, ctx, info, args.host_inclusive)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.config, int(args.cpu_sample_gib * GiB))
+        lib_multi_pending = world > 1 and not args.no_lib_multi
         if args.verbose:
             out["setup_s"] = round(setup_s, 2)
             out["fixups"] = st["n_fixups"]
             out["overflow_chunks"] = st["n_overflow"]
-        print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:
+        dist.barrier()  # every rank's context freed before the child takes the GPUs
         dist.destroy_process_group()
+    if rank == 0:
+        if lib_multi_pending:
+            out["keydir_merge_lib"] = lib_multi_child(args)
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,7 @@ from .core import (GB, KB, MB, TB, Config, DB, DefaultConfig, ErrCRCFailed, ErrI
                    NewInMemory, Open, ReplayContext, StartupError, WithDataDir, WithMaxDataFileSize, device_count,
                    host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into, replay_paths,
                    replay_multi, replay_multi_paths, zipf_table, multi_resolve, multi_recv_offsets,
-                   replay_multi_loopback)
+                   replay_multi_loopback, multi_keydir)
 from ._lib import F_CRC_OK, F_TOMBSTONE, REC_DTYPE
 
 __all__ = [
@@ -17,6 +17,6 @@ __all__ = [
     "ErrKeyNotFound", "ErrPartialWrite", "ErrUnexpectedEOF", "GoCaskError", "InMemoryDB", "NewDB", "NewDisk",
     "NewInMemory", "Open", "ReplayContext", "StartupError", "WithDataDir", "WithMaxDataFileSize", "device_count",
     "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into", "replay_paths",
-    "replay_multi", "replay_multi_paths", "zipf_table", "multi_resolve", "multi_recv_offsets", "replay_multi_loopback",
+    "replay_multi", "replay_multi_paths", "zipf_table", "multi_resolve", "multi_recv_offsets", "replay_multi_loopback", "multi_keydir",
     "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
 ]

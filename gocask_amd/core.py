@@ -343,6 +343,33 @@ def replay_multi_paths(paths, reset_after=None, devices=(0,), chunk_bytes=0, key
         L.gck_result_free(ctypes.byref(res))
 
 
+def multi_keydir(ctxs, fetch=True, keys=False):
+    """gck_ctx_multi_keydir: the keydir merge of gck_replay_multi over shards
+    already resident and replayed in ReplayContexts (ctxs[s] = shard s, walk
+    order; one device each, or several on one device: device copies).
+    Returns (live records or None, status dict with "n_live" and "ms" =
+    keydir + pack, exchange, merge, fetch wall milliseconds; "keys" with
+    keys=True)."""
+    L = _lib.load()
+    hs = (ctypes.c_void_p * max(1, len(ctxs)))(*[c._h.value for c in ctxs])
+    res = GckResult()
+    ms = (ctypes.c_double * 4)()
+    flags = (_lib.MULTI_FETCH if fetch else 0) | (_lib.MULTI_KEYS if keys else 0)
+    rc = L.gck_ctx_multi_keydir(hs, len(ctxs), flags, ctypes.byref(res), ms)
+    try:
+        check(rc, (GCK_OK, GCK_EUNEXPECTED_EOF))
+        n = res.n
+        if not fetch:
+            res.n = 0
+        recs, st = _result(res)
+        st["n_live"] = n
+        st["ms"] = dict(keydir_pack=ms[0], exchange=ms[1], merge=ms[2], fetch=ms[3])
+        return (recs if fetch else None), st
+    finally:
+        res.n = 0
+        L.gck_result_free(ctypes.byref(res))
+
+
 OUTCOME_DTYPE = np.dtype([("status", "<i4"), ("nfiles", "<u4"), ("err_file", "<u4"), ("files_walked", "<u4"),
                           ("final_last_offset", "<u4"), ("_pad", "<u4"), ("err_off", "<u8"), ("n_crc_fail", "<u8")])
 

@@ -239,6 +239,173 @@ void multi_recv_offsets(const uint64_t *counts, uint32_t nsrc, uint32_t nown, ui
     }
 }
 
+// Steps 3-5 of a sharded replay, shared by gck_replay_multi and
+// gck_ctx_multi_keydir: the packed sources (walk order) exchanged so that
+// owner p holds partition p of every source in source order -- a device copy
+// where source and owner share a device, RCCL send / receive pairs in one
+// group across devices (every count is known here: no size exchange) -- then
+// per owner the merge (the last writer wins, a winning tombstone drops the
+// key) and the owners' live entries gathered on the host (*h, *tot; with
+// want_keys their key bytes in out->keys).  h == nullptr: counted only.
+// ph_ms (optional): [exchange, merge, fetch] wall milliseconds.
+struct SrcRef {
+    uint32_t shard;
+    const Part *part;
+};
+static int exchange_merge(const std::vector<SrcRef> &srcs, const std::vector<int> &devs,
+                          const std::vector<gck_ctx *> &mctx, bool need_rccl, bool rccl_self, CommSet &cset,
+                          bool want_keys, bool trace, gck_rec **h_out, uint64_t *tot_out, gck_result *out,
+                          double *ph_ms) {
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    const uint32_t ndev = (uint32_t)devs.size();
+    int rc = GCK_OK;
+    const uint32_t nsrc = (uint32_t)srcs.size();
+    if (nsrc > 65536) return GCK_EINVAL;
+    std::vector<void *> r_ents(ndev, nullptr), r_keys(ndev, nullptr);
+    auto free_recv = [&]() {
+        for (uint32_t p = 0; p < ndev; ++p) {
+            (void)hipSetDevice(devs[p]);
+            for (void *q : {r_ents[p], r_keys[p]})
+                if (q) (void)hipFree(q);
+        }
+    };
+    std::vector<uint64_t> cnt((uint64_t)nsrc * ndev), kb((uint64_t)nsrc * ndev);
+    for (uint32_t i = 0; i < nsrc; ++i)
+        for (uint32_t p = 0; p < ndev; ++p) {
+            cnt[(uint64_t)i * ndev + p] = srcs[i].part->counts[p];
+            kb[(uint64_t)i * ndev + p] = srcs[i].part->kbytes[p];
+        }
+    std::vector<uint64_t> e_off((uint64_t)ndev * (nsrc + 1)), k_off((uint64_t)ndev * (nsrc + 1));
+    multi_recv_offsets(cnt.data(), nsrc, ndev, e_off.data());
+    multi_recv_offsets(kb.data(), nsrc, ndev, k_off.data());
+    auto EO = [&](uint32_t p, uint32_t i) { return e_off[(uint64_t)p * (nsrc + 1) + i]; };
+    auto KO = [&](uint32_t p, uint32_t i) { return k_off[(uint64_t)p * (nsrc + 1) + i]; };
+    for (uint32_t p = 0; p < ndev && !rc; ++p) {
+        if (hipSetDevice(devs[p]) != hipSuccess ||
+            hipMalloc(&r_ents[p], EO(p, nsrc) * sizeof(gck_kd_entry) + 64) != hipSuccess ||
+            hipMalloc(&r_keys[p], KO(p, nsrc) + 64) != hipSuccess) {
+            (void)hipGetLastError();
+            rc = GCK_ENOMEM;
+        }
+    }
+    const auto t_ex = clk::now();
+    if (!rc) {
+        std::unique_lock<std::mutex> lk;
+        if (need_rccl) lk = std::unique_lock<std::mutex>(*cset.mu);
+        // RCCL only when a pair crosses devices: loading librccl registers its
+        // kernels, 1.1-4.7 s of a one-device call (GCK_REPLAY_TRACE, round 4)
+        static const Rccl kNone{};
+        const Rccl &R = need_rccl ? rccl() : kNone;
+        bool grouped = false;
+        ncclResult_t r = ncclSuccess;
+        for (uint32_t i = 0; i < nsrc && !rc && r == ncclSuccess; ++i) {
+            const uint32_t s = srcs[i].shard;
+            const Part &pt = *srcs[i].part;
+            uint64_t eo = 0, ko = 0;  // the part's offsets of partition p
+            for (uint32_t p = 0; p < ndev && !rc && r == ncclSuccess; ++p) {
+                const uint64_t ne = pt.counts[p], nk = pt.kbytes[p];
+                const uint8_t *se = static_cast<const uint8_t *>(pt.d_ents) + eo * sizeof(gck_kd_entry);
+                const uint8_t *sk = static_cast<const uint8_t *>(pt.d_keys) + ko;
+                uint8_t *re = static_cast<uint8_t *>(r_ents[p]) + EO(p, i) * sizeof(gck_kd_entry);
+                uint8_t *rk = static_cast<uint8_t *>(r_keys[p]) + KO(p, i);
+                hipStream_t sp = mctx[p]->c.stream, ss = mctx[s]->c.stream;
+                eo += ne;
+                ko += nk;
+                if (devs[s] == devs[p] && !rccl_self) {
+                    (void)hipSetDevice(devs[p]);
+                    const auto tc = clk::now();
+                    if ((ne && hipMemcpyAsync(re, se, ne * sizeof(gck_kd_entry), hipMemcpyDeviceToDevice, sp) != hipSuccess) ||
+                        (nk && hipMemcpyAsync(rk, sk, nk, hipMemcpyDeviceToDevice, sp) != hipSuccess))
+                        rc = GCK_EDEVICE;
+                    if (trace)
+                        fprintf(stderr, "gck_replay_multi copy src %u -> owner %u: %llu entries, %llu key bytes, %.2f ms\n", i, p,
+                                (unsigned long long)ne, (unsigned long long)nk, ms_since(tc));
+                    continue;
+                }
+                if (!grouped) {
+                    r = R.group_start();
+                    grouped = true;
+                    if (r != ncclSuccess) break;
+                }
+                if (ne) {
+                    r = R.send(se, ne * sizeof(gck_kd_entry), ncclUint8, (int)p, cset.comms[s], ss);
+                    if (r == ncclSuccess) r = R.recv(re, ne * sizeof(gck_kd_entry), ncclUint8, (int)s, cset.comms[p], sp);
+                }
+                if (nk && r == ncclSuccess) {
+                    r = R.send(sk, nk, ncclUint8, (int)p, cset.comms[s], ss);
+                    if (r == ncclSuccess) r = R.recv(rk, nk, ncclUint8, (int)s, cset.comms[p], sp);
+                }
+            }
+        }
+        if (grouped) {
+            const ncclResult_t r2 = R.group_end();
+            if (r == ncclSuccess) r = r2;
+        }
+        if (r != ncclSuccess) {
+            set_error(R.err ? R.err(r) : "rccl", hipErrorUnknown, __FILE__, __LINE__);
+            rc = GCK_EDEVICE;
+        }
+        // the exchange is complete (and the communicators free for another
+        // call) once every owner's stream is
+        for (uint32_t p = 0; p < ndev; ++p) {
+            (void)hipSetDevice(devs[p]);
+            if (hipStreamSynchronize(mctx[p]->c.stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
+        }
+    }
+    if (ph_ms) ph_ms[0] = ms_since(t_ex);
+    // per owner, the merge (sources in walk order: the last writer wins, a
+    // winning tombstone drops the key); the live entries gathered in owner order
+    const auto t_mg = clk::now();
+    std::vector<uint64_t> n_live(ndev, 0);
+    for (uint32_t p = 0; p < ndev && !rc; ++p) {
+        std::vector<uint64_t> sc(nsrc ? nsrc : 1, 0), sk(nsrc ? nsrc : 1, 0);
+        for (uint32_t i = 0; i < nsrc; ++i) {
+            sc[i] = cnt[(uint64_t)i * ndev + p];
+            sk[i] = kb[(uint64_t)i * ndev + p];
+        }
+        rc = gck_kd_merge(mctx[p], static_cast<const gck_kd_entry *>(r_ents[p]), static_cast<const uint8_t *>(r_keys[p]),
+                          sc.data(), sk.data(), nsrc ? nsrc : 1, &n_live[p], nullptr);
+    }
+    if (ph_ms) ph_ms[1] = ms_since(t_mg);
+    const auto t_fe = clk::now();
+    uint64_t tot = 0;
+    for (uint64_t v : n_live) tot += v;
+    *tot_out = tot;
+    gck_rec *h = nullptr;
+    if (!rc && tot && h_out) {
+        h = static_cast<gck_rec *>(res_alloc(tot * sizeof(gck_rec), false));  // filled by the host below
+        if (!h) rc = GCK_ENOMEM;
+    }
+    uint64_t at = 0;
+    std::vector<uint8_t> kblob;  // GCK_OPT_KEYS: the entries' key bytes in output order
+    for (uint32_t p = 0; p < ndev && !rc && h_out; ++p) {
+        uint64_t n = 0, nk = 0;
+        if ((rc = gck_kd_fetch_merged(mctx[p], nullptr, 0, nullptr, 0, &n, &nk))) break;
+        if (!n) continue;
+        std::vector<gck_kd_entry> ents(n);
+        std::vector<uint8_t> keys(nk + 1);
+        if ((rc = gck_kd_fetch_merged(mctx[p], ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
+        for (uint64_t i = 0; i < n; ++i) {
+            h[at + i] = ents[i].rec;
+            if (want_keys) kblob.insert(kblob.end(), keys.begin() + (ptrdiff_t)ents[i].key_off,
+                                        keys.begin() + (ptrdiff_t)(ents[i].key_off + ents[i].key_len));
+        }
+        at += n;
+    }
+    if (!rc && want_keys && h_out) {
+        out->keys = static_cast<uint8_t *>(res_alloc(kblob.size(), false));
+        if (!out->keys) rc = GCK_ENOMEM;
+        else if (!kblob.empty()) memcpy(out->keys, kblob.data(), kblob.size());
+        out->keys_len = kblob.size();
+    }
+    if (ph_ms) ph_ms[2] = ms_since(t_fe);
+    free_recv();
+    if (rc) res_free(h);
+    else if (h_out) *h_out = h;
+    return rc;
+}
+
 // devs[s]: the device of shard s (distinct devices; loopback: several shards
 // on one device, their partitions moved by device copies -- the N-owner
 // orchestration without RCCL, libgocask_diag.so's test entry).
@@ -286,7 +453,6 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
     };
     std::vector<ShardRun> sr(ndev);
     std::vector<gck_ctx *> mctx(ndev, nullptr);      // per owner: the merge context (pooled)
-    std::vector<void *> r_ents(ndev, nullptr), r_keys(ndev, nullptr);
     std::vector<gck_opts> dopt(ndev);
     for (uint32_t s = 0; s < ndev; ++s) {
         if (opts) dopt[s] = *opts;
@@ -302,8 +468,6 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
             for (auto &p : sr[s].parts)
                 for (void *q : {p.d_ents, p.d_keys})
                     if (q) (void)hipFree(q);
-            for (void *q : {r_ents[s], r_keys[s]})
-                if (q) (void)hipFree(q);
             if (mctx[s]) pool_give(&dopt[s], mctx[s]);
         }
     };
@@ -353,157 +517,122 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
     }
     out->n_groups = ng;
     out->n_resident = nr;
-    // 3. the sources in walk order: every packed group of the contributing
-    // shards (a failing shard's groups end with the one that failed)
-    struct SrcRef {
-        uint32_t shard;
-        const Part *part;
-    };
+    // 3.-5. the sources in walk order (every packed group of the contributing
+    // shards; a failing shard's groups end with the one that failed), the
+    // exchange, the per-owner merges, the live entries
     std::vector<SrcRef> srcs;
     for (uint32_t s = 0; s < ndev; ++s)
         if (contrib[s])
             for (const Part &p : sr[s].parts) srcs.push_back(SrcRef{s, &p});
-    const uint32_t nsrc = (uint32_t)srcs.size();
-    if (nsrc > 65536) {
-        cleanup();
-        return GCK_EINVAL;
-    }
-    std::vector<uint64_t> cnt((uint64_t)nsrc * ndev), kb((uint64_t)nsrc * ndev);
-    for (uint32_t i = 0; i < nsrc; ++i)
-        for (uint32_t p = 0; p < ndev; ++p) {
-            cnt[(uint64_t)i * ndev + p] = srcs[i].part->counts[p];
-            kb[(uint64_t)i * ndev + p] = srcs[i].part->kbytes[p];
-        }
-    std::vector<uint64_t> e_off((uint64_t)ndev * (nsrc + 1)), k_off((uint64_t)ndev * (nsrc + 1));
-    multi_recv_offsets(cnt.data(), nsrc, ndev, e_off.data());
-    multi_recv_offsets(kb.data(), nsrc, ndev, k_off.data());
-    auto EO = [&](uint32_t p, uint32_t i) { return e_off[(uint64_t)p * (nsrc + 1) + i]; };
-    auto KO = [&](uint32_t p, uint32_t i) { return k_off[(uint64_t)p * (nsrc + 1) + i]; };
-    for (uint32_t p = 0; p < ndev && !rc; ++p) {
-        if (hipSetDevice(devs[p]) != hipSuccess ||
-            hipMalloc(&r_ents[p], EO(p, nsrc) * sizeof(gck_kd_entry) + 64) != hipSuccess ||
-            hipMalloc(&r_keys[p], KO(p, nsrc) + 64) != hipSuccess) {
-            (void)hipGetLastError();
-            rc = GCK_ENOMEM;
-        }
-    }
-    mark("packed");
-    // 4. the exchange: partition p of source i into owner p's buffers at
-    // (p, i); device copies on one device, RCCL send / receive pairs in one
-    // group across devices (every count is known here: no size exchange)
     join_comm();
     mark("comms");
-    if (!rc && need_rccl) rc = comm_rc;
-    if (!rc) {
-        std::unique_lock<std::mutex> lk;
-        if (need_rccl) lk = std::unique_lock<std::mutex>(*cset.mu);
-        // RCCL only when a pair crosses devices: loading librccl registers its
-        // kernels, 1.1-4.7 s of a one-device call (GCK_REPLAY_TRACE, round 4)
-        static const Rccl kNone{};
-        const Rccl &R = need_rccl ? rccl() : kNone;
-        bool grouped = false;
-        ncclResult_t r = ncclSuccess;
-        for (uint32_t i = 0; i < nsrc && !rc && r == ncclSuccess; ++i) {
-            const uint32_t s = srcs[i].shard;
-            const Part &pt = *srcs[i].part;
-            uint64_t eo = 0, ko = 0;  // the part's offsets of partition p
-            for (uint32_t p = 0; p < ndev && !rc && r == ncclSuccess; ++p) {
-                const uint64_t ne = pt.counts[p], nk = pt.kbytes[p];
-                const uint8_t *se = static_cast<const uint8_t *>(pt.d_ents) + eo * sizeof(gck_kd_entry);
-                const uint8_t *sk = static_cast<const uint8_t *>(pt.d_keys) + ko;
-                uint8_t *re = static_cast<uint8_t *>(r_ents[p]) + EO(p, i) * sizeof(gck_kd_entry);
-                uint8_t *rk = static_cast<uint8_t *>(r_keys[p]) + KO(p, i);
-                hipStream_t sp = mctx[p]->c.stream, ss = mctx[s]->c.stream;
-                eo += ne;
-                ko += nk;
-                if (devs[s] == devs[p] && !rccl_self) {
-                    (void)hipSetDevice(devs[p]);
-                    const auto tc = std::chrono::steady_clock::now();
-                    if ((ne && hipMemcpyAsync(re, se, ne * sizeof(gck_kd_entry), hipMemcpyDeviceToDevice, sp) != hipSuccess) ||
-                        (nk && hipMemcpyAsync(rk, sk, nk, hipMemcpyDeviceToDevice, sp) != hipSuccess))
-                        rc = GCK_EDEVICE;
-                    if (trace)
-                        fprintf(stderr, "gck_replay_multi copy src %u -> owner %u: %llu entries, %llu key bytes, %.2f ms\n", i, p,
-                                (unsigned long long)ne, (unsigned long long)nk,
-                                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count());
-                    continue;
-                }
-                if (!grouped) {
-                    r = R.group_start();
-                    grouped = true;
-                    if (r != ncclSuccess) break;
-                }
-                if (ne) {
-                    r = R.send(se, ne * sizeof(gck_kd_entry), ncclUint8, (int)p, cset.comms[s], ss);
-                    if (r == ncclSuccess) r = R.recv(re, ne * sizeof(gck_kd_entry), ncclUint8, (int)s, cset.comms[p], sp);
-                }
-                if (nk && r == ncclSuccess) {
-                    r = R.send(sk, nk, ncclUint8, (int)p, cset.comms[s], ss);
-                    if (r == ncclSuccess) r = R.recv(rk, nk, ncclUint8, (int)s, cset.comms[p], sp);
-                }
-            }
-        }
-        if (grouped) {
-            const ncclResult_t r2 = R.group_end();
-            if (r == ncclSuccess) r = r2;
-        }
-        if (r != ncclSuccess) {
-            set_error(R.err ? R.err(r) : "rccl", hipErrorUnknown, __FILE__, __LINE__);
-            rc = GCK_EDEVICE;
-        }
-        mark("exch issued");
-        // the exchange is complete (and the communicators free for another
-        // call) once every owner's stream is
-        for (uint32_t p = 0; p < ndev; ++p) {
-            (void)hipSetDevice(devs[p]);
-            if (hipStreamSynchronize(mctx[p]->c.stream) != hipSuccess && !rc) rc = GCK_EDEVICE;
-        }
-    }
-    mark("exchanged");
-    // 5. per owner, the merge (sources in walk order: the last writer wins, a
-    // winning tombstone drops the key); the live entries gathered in owner order
-    std::vector<uint64_t> n_live(ndev, 0);
-    for (uint32_t p = 0; p < ndev && !rc; ++p) {
-        std::vector<uint64_t> sc(nsrc ? nsrc : 1, 0), sk(nsrc ? nsrc : 1, 0);
-        for (uint32_t i = 0; i < nsrc; ++i) {
-            sc[i] = cnt[(uint64_t)i * ndev + p];
-            sk[i] = kb[(uint64_t)i * ndev + p];
-        }
-        rc = gck_kd_merge(mctx[p], static_cast<const gck_kd_entry *>(r_ents[p]), static_cast<const uint8_t *>(r_keys[p]),
-                          sc.data(), sk.data(), nsrc ? nsrc : 1, &n_live[p], nullptr);
-    }
-    uint64_t tot = 0;
-    for (uint64_t v : n_live) tot += v;
+    if (need_rccl) rc = comm_rc;
     gck_rec *h = nullptr;
-    if (!rc && tot) {
-        h = static_cast<gck_rec *>(res_alloc(tot * sizeof(gck_rec), false));  // filled by the host below
-        if (!h) rc = GCK_ENOMEM;
-    }
-    uint64_t at = 0;
-    std::vector<uint8_t> kblob;  // GCK_OPT_KEYS: the entries' key bytes in output order
-    for (uint32_t p = 0; p < ndev && !rc; ++p) {
-        uint64_t n = 0, nk = 0;
-        if ((rc = gck_kd_fetch_merged(mctx[p], nullptr, 0, nullptr, 0, &n, &nk))) break;
-        if (!n) continue;
-        std::vector<gck_kd_entry> ents(n);
-        std::vector<uint8_t> keys(nk + 1);
-        if ((rc = gck_kd_fetch_merged(mctx[p], ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
-        for (uint64_t i = 0; i < n; ++i) {
-            h[at + i] = ents[i].rec;
-            if (want_keys) kblob.insert(kblob.end(), keys.begin() + (ptrdiff_t)ents[i].key_off,
-                                        keys.begin() + (ptrdiff_t)(ents[i].key_off + ents[i].key_len));
-        }
-        at += n;
-    }
-    if (!rc && want_keys) {
-        out->keys = static_cast<uint8_t *>(res_alloc(kblob.size(), false));
-        if (!out->keys) rc = GCK_ENOMEM;
-        else if (!kblob.empty()) memcpy(out->keys, kblob.data(), kblob.size());
-        out->keys_len = kblob.size();
-    }
+    uint64_t tot = 0;
+    if (!rc) rc = exchange_merge(srcs, devs, mctx, need_rccl, rccl_self, cset, want_keys, trace, &h, &tot, out, nullptr);
     mark("merged+fetched");
     cleanup();
     mark("freed");
+    if (rc) {
+        res_free(h);
+        res_free(out->keys);
+        memset(out, 0, sizeof(*out));
+        return rc;
+    }
+    out->recs = h;
+    out->n = tot;
+    return out->status;
+}
+
+// gck_ctx_multi_keydir: steps 1 (keydir + pack per shard, a host thread
+// each), 2 (the global outcome) and 3-5 (exchange_merge) of a sharded replay
+// over shards already resident and replayed in their own contexts; owner p's
+// merge runs in ctxs[p].
+int ctx_multi_keydir(gck_ctx *const *ctxs, uint32_t n, uint32_t flags, gck_result *out, double *ms) {
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+    std::vector<int> devs(n);
+    for (uint32_t s = 0; s < n; ++s) devs[s] = ctxs[s]->c.device;
+    std::vector<int> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    const bool loopback = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+    const bool rccl_self = !loopback && getenv("GCK_MULTI_RCCL_SELF") != nullptr;
+    const bool need_rccl = !loopback && (n > 1 || rccl_self);
+    const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
+    CommSet cset;
+    int comm_rc = GCK_OK;
+    std::thread comm_th;
+    if (need_rccl) comm_th = std::thread([&]() { comm_rc = comms_for(devs, cset); });
+    std::vector<Part> parts(n);
+    std::vector<int> prc(n, GCK_OK);
+    std::vector<uint32_t> fbase(n + 1, 0);
+    for (uint32_t s = 0; s < n; ++s) fbase[s + 1] = fbase[s] + ctxs[s]->c.nfiles;
+    const auto t_loc = clk::now();
+    auto local = [&](uint32_t s) {
+        gck_ctx *ctx = ctxs[s];
+        Part &p = parts[s];
+        p.file0 = fbase[s];
+        uint64_t nl = 0;
+        int r = hipSetDevice(devs[s]) != hipSuccess ? GCK_EDEVICE : GCK_OK;
+        if (r || (r = gck_ctx_keydir(ctx, GCK_KD_KEEP_TOMBSTONES, &nl, nullptr)) ||
+            (r = gck_kd_pack_sizes(ctx, n, p.counts, p.kbytes))) {
+            prc[s] = r;
+            return;
+        }
+        uint64_t ne = 0, nk = 0;
+        for (uint32_t o = 0; o < n; ++o) {
+            ne += p.counts[o];
+            nk += p.kbytes[o];
+        }
+        if (hipMalloc(&p.d_ents, ne * sizeof(gck_kd_entry) + 64) != hipSuccess ||
+            hipMalloc(&p.d_keys, nk + 64) != hipSuccess) {
+            (void)hipGetLastError();
+            prc[s] = GCK_ENOMEM;
+            return;
+        }
+        prc[s] = gck_kd_pack(ctx, s, p.file0, static_cast<gck_kd_entry *>(p.d_ents), ne,
+                             static_cast<uint8_t *>(p.d_keys), nk);
+        if (!prc[s] && hipStreamSynchronize(ctx->c.stream) != hipSuccess) prc[s] = GCK_EDEVICE;
+    };
+    {
+        std::vector<std::thread> th;
+        for (uint32_t s = 1; s < n; ++s) th.emplace_back(local, s);
+        local(0);
+        for (auto &t : th) t.join();
+    }
+    if (ms) ms[0] = ms_since(t_loc);
+    int rc = GCK_OK;
+    for (uint32_t s = 0; s < n && !rc; ++s) rc = prc[s];
+    std::vector<MultiOutcome> oc(n);
+    for (uint32_t s = 0; s < n; ++s) {
+        const Ctx &c = ctxs[s]->c;
+        oc[s] = MultiOutcome{c.status, c.nfiles, c.err_file, c.files_walked, c.final_last_offset, c.err_off,
+                             c.n_crc_fail};
+    }
+    std::vector<uint8_t> contrib(n, 0);
+    multi_resolve(oc.data(), n, fbase[n], out, contrib.data());
+    std::vector<SrcRef> srcs;
+    for (uint32_t s = 0; s < n; ++s)
+        if (contrib[s]) srcs.push_back(SrcRef{s, &parts[s]});
+    if (comm_th.joinable()) comm_th.join();
+    if (!rc && need_rccl) rc = comm_rc;
+    gck_rec *h = nullptr;
+    uint64_t tot = 0;
+    double ph[3] = {0, 0, 0};
+    const std::vector<gck_ctx *> owners(ctxs, ctxs + n);
+    if (!rc)
+        rc = exchange_merge(srcs, devs, owners, need_rccl, rccl_self, cset, (flags & GCK_MULTI_KEYS) != 0, trace,
+                            (flags & GCK_MULTI_FETCH) ? &h : nullptr, &tot, out, ph);
+    if (ms) {
+        ms[1] = ph[0];
+        ms[2] = ph[1];
+        ms[3] = ph[2];
+    }
+    for (uint32_t s = 0; s < n; ++s) {
+        (void)hipSetDevice(devs[s]);
+        for (void *q : {parts[s].d_ents, parts[s].d_keys})
+            if (q) (void)hipFree(q);
+    }
     if (rc) {
         res_free(h);
         res_free(out->keys);
@@ -539,4 +668,13 @@ extern "C" int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, co
     rc = replay_multi(v.data(), nfiles, std::vector<int>(devices, devices + ndev), opts, out, false);
     close_srcs(v);
     return rc;
+}
+
+extern "C" int gck_ctx_multi_keydir(gck_ctx *const *ctxs, uint32_t n, uint32_t flags, gck_result *out, double *ms) {
+    if (!out) return GCK_EINVAL;
+    memset(out, 0, sizeof(*out));
+    if (!ctxs || n == 0 || n > 64) return GCK_EINVAL;
+    for (uint32_t s = 0; s < n; ++s)
+        if (!ctxs[s] || ctxs[s]->c.n_runs == 0) return GCK_EINVAL;  // every shard replayed first
+    return gck::ctx_multi_keydir(ctxs, n, flags, out, ms);
 }

@@ -324,6 +324,22 @@ int gck_replay_multi(const gck_file *files, uint32_t nfiles, const int32_t *devi
  * in out->keys, in the order of out->recs (either call). */
 int gck_replay_multi_paths(const gck_path *files, uint32_t nfiles, const int32_t *devices, uint32_t ndev,
                            const gck_opts *opts, gck_result *out);
+/* gck_replay_multi's keydir merge over shards that are already resident and
+ * replayed: ctxs[s] holds shard s (a contiguous walk-order run of files, each
+ * but the last shard's last file resetting lastOffset) after gck_ctx_run, on
+ * its own device (several contexts on one device: every pair a device copy).
+ * Per shard the keydir with tombstones packed over the n owners
+ * (gck_ctx_keydir, gck_kd_pack), the partitions exchanged (RCCL across
+ * devices, as gck_replay_multi), per owner the merge in ctxs[p] (gck_kd_merge).
+ * out: status, err_file / files_walked (global walk indices), err_off,
+ * final_last_offset and n_crc_fail resolved over the shards in order; n = live
+ * keys; with GCK_MULTI_FETCH recs = the live entries (rec.file global; freed by
+ * gck_result_free), with GCK_MULTI_KEYS also their key bytes.  ms (optional, 4
+ * doubles): wall ms of keydir + pack, exchange, merge, fetch.  This is the
+ * one-process multi-GPU path's exchange step, timed by bench.py --lib-multi. */
+#define GCK_MULTI_FETCH 1u
+#define GCK_MULTI_KEYS 2u
+int gck_ctx_multi_keydir(gck_ctx *const *ctxs, uint32_t n, uint32_t flags, gck_result *out, double *ms);
 /* The shard plan (host only, no device): shard s = files [ranges[2 s],
  * ranges[2 s + 1]); empty shards when there are fewer allowed cuts than
  * shards.  A cut at i needs reset_after[i - 1] (core/db.go:117-119). */

@@ -17,12 +17,23 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_launcher_cmd_shape():
     import bench
 
-    cmd = bench.launcher_cmd(4, 29512, ["--gpus", "4", "--steps", "3"], script="/x/bench.py")
+    cmd = bench.launcher_cmd(4, ["--gpus", "4", "--steps", "3"], script="/x/bench.py")
     assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd
-    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29512" in cmd
+    # the launcher's own store picks the port (no port chosen here and freed
+    # before the launcher binds it) on 127.0.0.1
+    assert "--standalone" in cmd and "--local-addr=127.0.0.1" in cmd
+    assert not any(a.startswith("--master-port") for a in cmd)
     assert cmd[-4:] == ["/x/bench.py", "--gpus", "4", "--steps", "3"][-4:]
-    assert cmd.index("/x/bench.py") > cmd.index("--master-port=29512")
+    assert cmd.index("/x/bench.py") > cmd.index("--local-addr=127.0.0.1")
+
+
+def test_nested_relaunch_refused():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["GCK_BENCH_LAUNCHED"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "nested relaunch" in r.stderr
 
 
 def test_world_size_must_match_gpus():
@@ -74,3 +85,31 @@ def test_bench_gpus2_launches_its_ranks():
     assert d["roofline"]["traffic"] is None  # a rehearsal carries no C4 counter bytes
     km = d["keydir_merge"]
     assert km["global_status"]["status"] == 0 and km["live_entries"] > 0
+    # the drop-in multi-GPU path's exchange (gck_ctx_multi_keydir, one
+    # process; on one GPU the two shards' partitions move by device copies):
+    # the same global keydir as the torch path's merge
+    kl = d["keydir_merge_lib"]
+    assert "error" not in kl, kl
+    assert kl["live_entries"] == km["live_entries"] and kl["global_status"] == 0
+    assert kl["transport"].startswith("device copies")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,self_rccl", [(1, True), (3, False)])
+def test_bench_lib_multi(n, self_rccl):
+    """`bench.py --gpus N --lib-multi`: one process, a context per device (on
+    the one-GPU box: N=1 through the library's RCCL path as a self send /
+    receive, N=3 as a loopback of three contexts on device 0), the library's
+    keydir exchange + merge timed as keydir_merge_lib."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if self_rccl:
+        env["GCK_MULTI_RCCL_SELF"] = "1"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--lib-multi", "--steps", "2",
+           "--warmup", "1", "--c4-files-per-gpu", "2", "--c4-file-mib", "64"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["n_gpus"] == n and d["value"] > 0
+    kl = d["keydir_merge_lib"]
+    assert kl["live_entries"] > 0 and kl["global_status"] == 0 and kl["ms"] > 0
+    assert kl["transport"] == ("RCCL over xGMI" if n == 1 else "device copies (loopback)")
