@@ -95,6 +95,7 @@ struct Ctx {
     DBuf d_fbase, d_flen, d_ffirst, d_fnch, d_fbad, d_fterm, d_ftpos, d_fnrec, d_ffirstrec, d_carry;
     DBuf d_ch_file, d_ch_start, d_ch_end, d_ch_entry, d_ch_exit, d_ch_count, d_ch_term, d_ch_tpos, d_ch_bad;
     DBuf d_ch_wend;              // where each chunk's walk stopped (its bound, walk_bound)
+    DBuf d_ch_aentry;            // each chunk's walked entry as an arena offset (k_compact's record base)
     uint32_t chunk_shift = 17;   // log2(opts.chunk_bytes)
     DBuf d_rec_base, d_bsum, d_stage, d_counters;  // d_stage: (KeySize, ValueSize) per walked record (stage_slot)
     DBuf d_freset;                   // per file: 1 = lastOffset resets after it

@@ -60,6 +60,7 @@ constexpr uint32_t kClkWaves = 16384;
 constexpr int kClkKinds = 6;  // 0 k_crc_rows, 1 k_clk_stream, 2 k_spec_entry, 3 k_walk, 4 k_compact, 5 k_finalize
 __device__ uint64_t g_clk[kClkKinds][4 * kClkWaves];
 __device__ uint32_t g_clk_xcc[kClkKinds][kClkWaves];
+__device__ uint64_t g_fin_split[2 * kClkWaves];  // k_finalize: (wait, compute) cycles per wavefront
 __device__ __forceinline__ void clk_put(int which, uint32_t wi, uint64_t t0, uint64_t r0) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     if ((threadIdx.x & 63) == 0 && wi < kClkWaves) {
@@ -195,18 +196,11 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {
 // the largest that chains): a true header has plausible "shadows" 1..3 bytes
 // earlier (Timestamp's top bytes + KeySize shifted).  Keys longer than 65535
 // bytes are never speculated here; validation finds their chunks and re-walks.
-__global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
-                                                    const uint64_t *__restrict__ fbase,
-                                                    const uint64_t *__restrict__ flen,
-                                                    const uint32_t *__restrict__ ch_file,
-                                                    const uint64_t *__restrict__ ch_start,
-                                                    const uint64_t *__restrict__ ch_end,
-                                                    uint64_t *__restrict__ ch_entry, uint32_t n_chunks,
-                                                    uint32_t max_key, uint64_t window) {
+__device__ void spec_chunk(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
+                           const uint64_t *__restrict__ flen, const uint32_t *__restrict__ ch_file,
+                           const uint64_t *__restrict__ ch_start, const uint64_t *__restrict__ ch_end,
+                           uint64_t *__restrict__ ch_entry, uint32_t c, uint32_t max_key, uint64_t window) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
-    if (c >= n_chunks) return;
-    GCK_CLK_BEGIN();
     const uint32_t f = ch_file[c];
     const uint64_t cs = ch_start[c], ce = ch_end[c], base = fbase[f], len = flen[f];
     const uint32_t mk = min(max_key, 65535u);
@@ -361,6 +355,20 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
         }
     }
     if (lane == 0) ch_entry[c] = found;
+}
+
+__global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
+                                                    const uint64_t *__restrict__ fbase,
+                                                    const uint64_t *__restrict__ flen,
+                                                    const uint32_t *__restrict__ ch_file,
+                                                    const uint64_t *__restrict__ ch_start,
+                                                    const uint64_t *__restrict__ ch_end,
+                                                    uint64_t *__restrict__ ch_entry, uint32_t n_chunks,
+                                                    uint32_t max_key, uint64_t window) {
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
+    if (c >= n_chunks) return;
+    GCK_CLK_BEGIN();
+    spec_chunk(arena, fbase, flen, ch_file, ch_start, ch_end, ch_entry, c, max_key, window);
     GCK_CLK_END(2, c);
 }
 
@@ -416,13 +424,17 @@ __device__ uint64_t walk_bound(const uint64_t *__restrict__ ch_entry, const uint
 __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_t *fbase,
                                 const uint64_t *flen, uint32_t c, uint32_t f, uint64_t ce, uint64_t entry,
                                 uint32_t cap, uint2 *s_kv, uint32_t *ch_count,
-                                uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *ch_wend) {
+                                uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *ch_wend,
+                                uint64_t *ch_aentry) {
     uint32_t count = 0, term = T_NONE;
-    uint64_t exit = kNone, tpos = 0;
+    uint64_t exit = kNone, tpos = 0, aentry = 0;
     if (entry != kNone) {
         ScratchEmit em{s_kv + stage_slot(c, 0, cap), cap};
-        walk_chain(arena, fbase[f], flen[f], ce, entry, em, count, exit, term, tpos);
+        const uint64_t base = fbase[f];
+        aentry = base + entry;
+        walk_chain(arena, base, flen[f], ce, entry, em, count, exit, term, tpos);
     }
+    ch_aentry[c] = aentry;
     ch_count[c] = count;
     ch_exit[c] = exit;
     ch_term[c] = term;
@@ -440,7 +452,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint32_t *__restrict__ f_nchunks,
                                               const uint64_t *__restrict__ ch_entry, uint32_t *ch_count,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
-                                              uint64_t *ch_wend, uint2 *s_kv, uint32_t cap,
+                                              uint64_t *ch_wend, uint64_t *ch_aentry, uint2 *s_kv, uint32_t cap,
                                               uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end) {
     GCK_CLK_BEGIN();
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
@@ -449,7 +461,7 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
     const uint64_t entry = ch_entry[c];
     const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
     walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
-                    ch_wend);
+                    ch_wend, ch_aentry);
     GCK_CLK_END(3, (c - c_begin) >> 6);
 }
 
@@ -502,7 +514,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
                                                const uint32_t *__restrict__ f_nchunks,
                                                const uint32_t *__restrict__ ch_bad, uint64_t *ch_entry,
                                                uint32_t *ch_count, uint64_t *ch_exit, uint32_t *ch_term,
-                                               uint64_t *ch_tpos, uint64_t *ch_wend, uint2 *s_kv,
+                                               uint64_t *ch_tpos, uint64_t *ch_wend, uint64_t *ch_aentry, uint2 *s_kv,
                                                uint32_t cap, uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end,
                                                uint32_t *counter, const uint32_t *__restrict__ bad_counter) {
     if (bad_counter && *bad_counter == 0) return;  // nothing to fix (the common case)
@@ -521,7 +533,7 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
     atomicAdd(counter, 1u);
     const uint64_t ce = e_new != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
     walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
-                    ch_wend);
+                    ch_wend, ch_aentry);
 }
 
 // Exclusive scan of per-chunk record counts -> rec_base[0..n] (one wavefront
@@ -837,19 +849,30 @@ struct DirectEmit {
     __device__ void prime() const {}
 };
 
-// Record table in walk order: one wavefront per chunk c0 + c (the chunk
-// arrays are passed offset by c0; the stage is indexed by global chunk) copies
-// its staged (KeySize, ValueSize) pairs and rebuilds the record offsets from the chunk's
-// entry by a scan of the entry sizes; chunks that overflowed the stage re-walk
-// straight into the table.  A workgroup takes 16 consecutive chunks, so the
-// stage lines it reads (slot i of kStageIl consecutive chunks, stage_slot)
-// are fetched once per CU.
+// Record table in walk order: a wavefront per kCompactChunks consecutive
+// chunks c0 + c (the chunk arrays are passed offset by c0; the stage is
+// indexed by global chunk) copies their staged (KeySize, ValueSize) pairs and
+// rebuilds the record offsets from each chunk's entry (an arena offset, left
+// by the walk) by a scan of the entry sizes; chunks that overflowed the stage
+// re-walk straight into the table.  Every load a chunk needs -- count, record
+// base, file, entry and the first kPreBatches batches of its stage -- is
+// issued for all of the wavefront's chunks before the first is written: one
+// round trip per wavefront instead of two per chunk (the file's base was a
+// second, dependent one), and a quarter of the wavefronts (the grid ran in
+// eight rounds of resident wavefronts, each paying its round trips).  The
+// stage interleaves slot i of kStageIl consecutive chunks, so a workgroup's
+// stage lines are fetched once per CU.
+#ifndef GCK_COMPACT_CHUNKS
+#define GCK_COMPACT_CHUNKS 1
+#endif
+constexpr uint32_t kCompactChunks = GCK_COMPACT_CHUNKS;
 __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint64_t *__restrict__ flen,
                                                   const uint32_t *__restrict__ ch_file,
                                                   const uint64_t *__restrict__ ch_wend,
                                                   const uint64_t *__restrict__ ch_entry,
+                                                  const uint64_t *__restrict__ ch_aentry,
                                                   const uint32_t *__restrict__ ch_count,
                                                   const uint64_t *__restrict__ rec_base,
                                                   const uint2 *__restrict__ s_kv, uint32_t cap, uint32_t c0,
@@ -857,61 +880,69 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   uint2 *rec_kv, uint32_t *rec_file, uint32_t *row_first,
                                                   uint32_t *counters) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = blockIdx.x * 16 + (threadIdx.x >> 6);
-    if (c >= n_chunks) return;
+    const uint32_t cw = (blockIdx.x * 16 + (threadIdx.x >> 6)) * kCompactChunks;
+    if (cw >= n_chunks) return;
     GCK_CLK_BEGIN();
-    // everything a chunk needs in one round trip: its entry, count, record
-    // base and file, and the first kPreBatches batches of its stage (slots
-    // past the count or the capacity read the chunk's scratch slot, which
-    // exists); then the file's base.  (Loaded in turn, these were four
-    // dependent round trips before the first record.)
-    const uint64_t entry = ch_entry[c];
-    const uint32_t cnt = ch_count[c];
-    const uint64_t rb = rec_base[c];
-    const uint32_t f = ch_file[c];
-    uint2 pre[kPreBatches];
+    constexpr uint32_t K = kCompactChunks;
+    uint32_t cnt[K], f[K];
+    uint64_t rb[K], ae[K];
+    uint2 pre[K][kPreBatches];
 #pragma unroll
-    for (uint32_t k = 0; k < kPreBatches; ++k) pre[k] = s_kv[stage_slot(c0 + c, 64 * k + lane, cap)];
-    if (entry == kNone || cnt == 0 || rb >= n_total) return;
-    const uint64_t base = fbase[f];
-    if (cnt <= cap) {
-        uint64_t run = base + entry;  // arena offset of the next record
-        // batches past the preloaded ones: the next batch's stage entries
-        // are loaded while this batch is written
-        uint2 nxt = make_uint2(0u, 0u);
-        for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const bool in = i < cnt;
-            const uint32_t b = i0 / 64;  // (uniform)
-            uint2 kv = nxt;
+    for (uint32_t j = 0; j < K; ++j) {
+        const uint32_t c = min(cw + j, n_chunks - 1);  // (a chunk past the end repeats the last: skipped below)
+        cnt[j] = ch_count[c];
+        rb[j] = rec_base[c];
+        f[j] = ch_file[c];
+        ae[j] = ch_aentry[c];
 #pragma unroll
-            for (uint32_t k = 0; k < kPreBatches; ++k)
-                if (b == k) kv = pre[k];
-            if (!in) kv = make_uint2(0u, 0u);
-            if (b + 1 >= kPreBatches) nxt = i + 64 < cnt ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
-            // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
-            // inclusive scan is exact in 24-bit halves (entries < 2^33)
-            const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
-            const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
-            const uint64_t r = rb + i;
-            if (in && r < n_total) {
-                const uint64_t ve = run + (((uint64_t)hi << 24) + lo);
-                rec_off[r] = ve - e;
-                rec_kv[r] = kv;
-                rec_file[r] = f;
-                set_row_first(row_first, r, ve - e, ve);
-            }
-            run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
-                   (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
-        }
-    } else if (lane == 0) {
-        atomicAdd(&counters[2], 1u);
-        DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb, n_total, base, f};
-        uint32_t count, term;
-        uint64_t exit, tpos;
-        walk_chain(arena, base, flen[f], ch_wend[c], entry, em, count, exit, term, tpos);
+        for (uint32_t k = 0; k < kPreBatches; ++k) pre[j][k] = s_kv[stage_slot(c0 + c, 64 * k + lane, cap)];
     }
-    GCK_CLK_END(4, c);
+#pragma unroll
+    for (uint32_t j = 0; j < K; ++j) {
+        const uint32_t c = cw + j;
+        // no entry (count 0), nothing staged, or past the record capacity
+        if (c >= n_chunks || cnt[j] == 0 || rb[j] >= n_total) continue;
+        if (cnt[j] <= cap) {
+            uint64_t run = ae[j];  // arena offset of the next record
+            // batches past the preloaded ones: the next batch's stage entries
+            // are loaded while this batch is written
+            uint2 nxt = make_uint2(0u, 0u);
+            for (uint32_t i0 = 0; i0 < cnt[j]; i0 += 64) {
+                const uint32_t i = i0 + lane;
+                const bool in = i < cnt[j];
+                const uint32_t b = i0 / 64;  // (uniform)
+                uint2 kv = nxt;
+#pragma unroll
+                for (uint32_t k = 0; k < kPreBatches; ++k)
+                    if (b == k) kv = pre[j][k];
+                if (!in) kv = make_uint2(0u, 0u);
+                if (b + 1 >= kPreBatches)
+                    nxt = i + 64 < cnt[j] ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
+                // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
+                // inclusive scan is exact in 24-bit halves (entries < 2^33)
+                const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
+                const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
+                const uint64_t r = rb[j] + i;
+                if (in && r < n_total) {
+                    const uint64_t ve = run + (((uint64_t)hi << 24) + lo);
+                    rec_off[r] = ve - e;
+                    rec_kv[r] = kv;
+                    rec_file[r] = f[j];
+                    set_row_first(row_first, r, ve - e, ve);
+                }
+                run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
+                       (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+            }
+        } else if (lane == 0) {
+            atomicAdd(&counters[2], 1u);
+            const uint64_t base = fbase[f[j]];
+            DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb[j], n_total, base, f[j]};
+            uint32_t count, term;
+            uint64_t exit, tpos;
+            walk_chain(arena, base, flen[f[j]], ch_wend[c], ch_entry[c], em, count, exit, term, tpos);
+        }
+    }
+    GCK_CLK_END(4, cw / K);
 }
 
 __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uint2 *rec_kv, uint64_t r) {
@@ -1095,14 +1126,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     auto store_blk = [&](uint32_t off8, const u32x4 &v) {
         __builtin_amdgcn_raw_buffer_store_b128(v, blk_rsrc, (int)(off8 == kDrop ? kDrop : off8 * 2u), 0, 0);
     };
-    auto pick_blk = [&](const uint32_t *wv, uint32_t b) {
-        u32x4 v;
-        v.x = b == 0 ? wv[0] : b == 1 ? wv[4] : b == 2 ? wv[8] : wv[12];
-        v.y = b == 0 ? wv[1] : b == 1 ? wv[5] : b == 2 ? wv[9] : wv[13];
-        v.z = b == 0 ? wv[2] : b == 1 ? wv[6] : b == 2 ? wv[10] : wv[14];
-        v.w = b == 0 ? wv[3] : b == 1 ? wv[7] : b == 2 ? wv[11] : wv[15];
-        return v;
-    };
+#define GCK_PICK_BLK(wv, b)                                                                          \
+    u32x4 {(b) == 0 ? wv[0] : (b) == 1 ? wv[4] : (b) == 2 ? wv[8] : wv[12],                          \
+           (b) == 0 ? wv[1] : (b) == 1 ? wv[5] : (b) == 2 ? wv[9] : wv[13],                          \
+           (b) == 0 ? wv[2] : (b) == 1 ? wv[6] : (b) == 2 ? wv[10] : wv[14],                         \
+           (b) == 0 ? wv[3] : (b) == 1 ? wv[7] : (b) == 2 ? wv[11] : wv[15]}
 #endif
 
     // Work assignment: the first rounds are static (wavefront w of W takes
@@ -1313,7 +1341,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
                 store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
 #ifdef GCK_XP_EBLK
-                store_blk(m ? (ra + idx - ra0) * 8u : kDrop, pick_blk(w[i], (uint32_t)__builtin_ctz(m | 16u) & 3u));
+                { const uint32_t bb = (uint32_t)__builtin_ctz(m | 16u) & 3u; store_blk(m ? (ra + idx - ra0) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
 #endif
             } else {
                 // a slab with 2..4 record ends (records under 64 B): ids by
@@ -1325,7 +1353,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 for (uint32_t q = 0; q < 4; ++q) {
                     store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
 #ifdef GCK_XP_EBLK
-                    store_blk(q < n ? (ra + ex + q - ra0) * 8u : kDrop, pick_blk(w[i], (uint32_t)__builtin_ctz(mm | 16u) & 3u));
+                    { const uint32_t bb = (uint32_t)__builtin_ctz(mm | 16u) & 3u; store_blk(q < n ? (ra + ex + q - ra0) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
 #endif
                     mm &= mm - 1;
                 }
@@ -1604,6 +1632,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         uint32_t pw[12], rr[12];
         uint32_t xhi, cf;
         uint64_t fb;
+#ifdef GCK_FIN_GTAB
+        uint32_t xi, xv;
+#endif
     };
     auto issue = [&](const Geo &g, Dep &o) {
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(arena + g.w0);
@@ -1641,6 +1672,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             o.rr[4 * i + 3] = v.w;
         }
         o.xhi = g.V >= 65536 ? xa[g.V >> 16] : 0u;
+#ifdef GCK_FIN_GTAB
+        o.xi = xinv[g.d];          // x^{-8d}, d < 4096 (16 KiB table, L2)
+        o.xv = xb[g.V & 0xFFFFu];  // x^{8 (V mod 2^16)} (256 KiB table, L2)
+#endif
         o.cf = carry[g.f];
         o.fb = fbase[g.f];
     };
@@ -1681,7 +1716,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         // (a bit-serial VALU product in place of any of these four measured
         // slower: 0.47-0.64 ms against 0.46-0.47, profiles/r3j/ab_finvalu.log)
         auto mul = [&](uint32_t a, uint32_t b) { return gf_mul_lds(ldsb, mw, rxb, a, b); };
+#ifdef GCK_FIN_GTAB
+        const uint32_t xi = o.xi;
+#else
         const uint32_t xi = mul(Xi[64 + (g.d >> 6)], Xi[g.d & 63]);  // x^{-8d}
+#endif
         const uint32_t chain = ft ^ mul(xi, acc);
         // F(s, prefix): header + key bytes [rs, vs) as aligned words from
         // rs & ~3; the first word's bytes before rs are shifted out
@@ -1703,7 +1742,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         if (nw >= 12) y = wp[nw];
         if (L & 3) p = partial_word(T, p, y, L & 3);  // L >= 16: y is never the masked word
         // x^(8V) = xa[V >> 16] * x^(8 (V & 0xFF00)) * x^(8 (V & 0xFF))
+#ifdef GCK_FIN_GTAB
+        uint32_t xv = o.xv;
+#else
         uint32_t xv = mul(Xb[256 + ((V >> 8) & 0xFF)], Xb[V & 0xFF]);
+#endif
         if (V >= 65536) xv = mul(xhi, xv);
         // crc = F(0, value) ^ crc32(0^V), crc32(0^V) = Z_V(~0) ^ ~0, and Z_V is
         // linear: one multiply covers the prefix and the init term (no
@@ -1743,6 +1786,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // two iterations ahead and the dependent loads one ahead measured slower:
     // 0.517-0.520 vs 0.496-0.498 ms)
     GCK_CLK_BEGIN();
+#ifdef GCK_CLOCK_STAMPS
+    // stamps build only: per wavefront, the shader cycles spent waiting for
+    // an iteration's loads (forced vmcnt(0)) and computing it
+    uint64_t fin_wait = 0, fin_comp = 0;
+#endif
     uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
     Rec cur, nxt;
     if (base < re) load_rec(base, cur);
@@ -1751,9 +1799,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         Dep dc;
         issue(g, dc);
         if (base + G < re) load_rec(base + G, nxt);
+#ifdef GCK_CLOCK_STAMPS
+        const uint64_t fa = __builtin_amdgcn_s_memtime();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t fb = __builtin_amdgcn_s_memtime();
+        fin_wait += fb - fa;
+#endif
         compute(cur, g, dc, base);
+#ifdef GCK_CLOCK_STAMPS
+        fin_comp += __builtin_amdgcn_s_memtime() - fb;
+#endif
         cur = nxt;
     }
+#ifdef GCK_CLOCK_STAMPS
+    if ((threadIdx.x & 63) == 0 && blockIdx.x * 4 + (threadIdx.x >> 6) < kClkWaves) {
+        g_fin_split[2 * (blockIdx.x * 4 + (threadIdx.x >> 6))] = fin_wait;
+        g_fin_split[2 * (blockIdx.x * 4 + (threadIdx.x >> 6)) + 1] = fin_comp;
+    }
+#endif
     GCK_CLK_END(5, blockIdx.x * 4 + (threadIdx.x >> 6));
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
@@ -1887,7 +1950,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
 static void ctx_free(Ctx *c) {
     DBuf *all[] = {&c->arena, &c->d_fbase, &c->d_flen, &c->d_ffirst, &c->d_fnch, &c->d_fbad, &c->d_fterm,
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
-                   &c->d_ch_end, &c->d_ch_wend, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
+                   &c->d_ch_end, &c->d_ch_wend, &c->d_ch_aentry, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
@@ -1969,7 +2032,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ffirstrec.ensure(nf * 8)) || (rc = c->d_carry.ensure(nf * 4)) ||
         (rc = c->d_ch_file.ensure((nc + 1) * 4)) || (rc = c->d_ch_start.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_end.ensure((nc + 1) * 8)) || (rc = c->d_ch_entry.ensure((nc + 1) * 8)) ||
-        (rc = c->d_ch_wend.ensure((nc + 1) * 8)) ||
+        (rc = c->d_ch_wend.ensure((nc + 1) * 8)) || (rc = c->d_ch_aentry.ensure((nc + 1) * 8)) ||
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + 4) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
@@ -2036,7 +2099,7 @@ static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, const 
         c->d_ch_end.as<uint64_t>(), c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_bad.as<uint32_t>(),
         c->d_ch_entry.as<uint64_t>(), c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(),
-        c->d_stage.as<uint2>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
+        c->d_ch_aentry.as<uint64_t>(), c->d_stage.as<uint2>(), c->opts.chunk_cap, c->chunk_shift, c0, c1,
         c->d_counters.as<uint32_t>() + CNT_FIXUP, bad_cnt);
 }
 
@@ -2054,7 +2117,8 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
                                         c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
                                         c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
                                         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
-                                        c->d_ch_wend.as<uint64_t>(), c->d_stage.as<uint2>(), cap, c->chunk_shift, c0, c1);
+                                        c->d_ch_wend.as<uint64_t>(), c->d_ch_aentry.as<uint64_t>(), c->d_stage.as<uint2>(),
+                                        cap, c->chunk_shift, c0, c1);
     for (int r = 0; r <= kRounds; ++r) {
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
@@ -2089,9 +2153,11 @@ static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint
     const uint32_t grid = (uint32_t)c->n_cu * 4;
     k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
     if (n)
-        k_compact<<<nblk(n, 16), 1024, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+        k_compact<<<nblk(n, 16 * kCompactChunks), 1024, 0, s>>>(
+                                             c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                              c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
-                                             c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_count.as<uint32_t>() + c0,
+                                             c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_aentry.as<uint64_t>() + c0,
+                                             c->d_ch_count.as<uint32_t>() + c0,
                                              c->d_rec_base.as<uint64_t>() + c0,
                                              c->d_stage.as<uint2>(), ccap, c0, n, cap,
                                              c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
@@ -2313,7 +2379,9 @@ static int ctx_run_device(Ctx *c) {
     // between the other phases only with phase timing on (each event between
     // two kernels costs ~6 us of the run)
     const bool ph = c->phase_timing;
-    GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
+    // (without phase timing only the CRC pass is bracketed: an event between
+    // two kernels costs ~5-6 us of the run, kernel trace profiles/r5a)
+    if (ph) GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
     k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
     launch_boundary(c, m, 0, nc, cnt + CNT_VAL);
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
@@ -2325,7 +2393,7 @@ static int ctx_run_device(Ctx *c) {
     if ((rc = launch_crc(c, m, 0, c->n_rows, cap, kQueueCrc, true))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
     launch_finalize(c, m, rng, cap);
-    GCK_HIP(hipEventRecord(c->ev[PH_END], m));
+    if (ph) GCK_HIP(hipEventRecord(c->ev[PH_END], m));
     k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
     GCK_HIP(hipStreamSynchronize(m));
     GCK_HIP(hipGetLastError());
@@ -2352,12 +2420,10 @@ static int ctx_run_device(Ctx *c) {
         c->ms_phase[PH_BOUNDARY] = el(PH_BOUNDARY, PH_SCAN);
         c->ms_phase[PH_SCAN] = el(PH_SCAN, PH_RECORDS);  // scans, file summaries, bookkeeping: one kernel
         c->ms_phase[PH_RECORDS] = el(PH_RECORDS, PH_CRC);
-    } else {
-        c->ms_phase[PH_BOUNDARY] = el(PH_BOUNDARY, PH_CRC);  // every phase before the CRC pass
+        c->ms_phase[PH_FINAL] = el(PH_FINAL, PH_END);
+        c->ms_phase[PH_PIPE] = el(PH_BOUNDARY, PH_END);
     }
     c->ms_phase[PH_CRC] = el(PH_CRC, PH_FINAL);
-    c->ms_phase[PH_FINAL] = el(PH_FINAL, PH_END);
-    c->ms_phase[PH_PIPE] = el(PH_BOUNDARY, PH_END);
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3148,6 +3214,13 @@ int gck_xp_clock_read(int which, uint64_t *out) {
     GCK_HIP(hipDeviceSynchronize());
     GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clk), sizeof(uint64_t) * 4 * kClkWaves,
                                 sizeof(uint64_t) * 4 * kClkWaves * which));
+    return GCK_OK;
+}
+// k_finalize's per-wavefront (load wait, compute) shader cycles of the last run
+int gck_xp_fin_split(uint64_t *out) {
+    if (!out) return GCK_EINVAL;
+    GCK_HIP(hipDeviceSynchronize());
+    GCK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_split), sizeof(uint64_t) * 2 * kClkWaves, 0));
     return GCK_OK;
 }
 // the XCC id of each stamped wavefront (kClkWaves entries)

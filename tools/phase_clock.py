@@ -70,6 +70,15 @@ def main():
         assert L.gck_xp_clock_read(k, buf.ctypes.data) == 0
         out[name] = summary(buf.reshape(-1, 4))
         starts[name] = out[name].pop("t0_realtime", None)
+    if hasattr(L, "gck_xp_fin_split"):
+        L.gck_xp_fin_split.argtypes = [ctypes.c_void_p]
+        fs = np.zeros(2 * 16384, dtype=np.uint64)
+        assert L.gck_xp_fin_split(fs.ctypes.data) == 0
+        fs = fs.reshape(-1, 2).astype(np.float64)
+        fs = fs[fs.sum(axis=1) > 0]
+        if len(fs):
+            out["k_finalize"]["split_cycles_median"] = dict(wait=float(np.median(fs[:, 0])),
+                                                            compute=float(np.median(fs[:, 1])))
     base = min(v for v in starts.values() if v)
     for name, v in starts.items():
         if v:
