@@ -985,7 +985,18 @@ __global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *_
 
 constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
 constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
-constexpr uint32_t kClaim = 2;   // consecutive row blocks per k_crc_rows queue claim
+#ifndef GCK_CLAIM
+#define GCK_CLAIM 1
+#endif
+constexpr uint32_t kClaim = GCK_CLAIM;   // consecutive row blocks per k_crc_rows queue claim
+#ifndef GCK_LATE_CLAIM
+#define GCK_LATE_CLAIM 13
+#endif
+// the quad of a block at which k_crc_rows claims the block after next (-1: at
+// the block's start).  Claiming one block, late, holds a wave's look-ahead to
+// ~1.2 blocks instead of up to 3 when the queue runs dry: the kernel's tail
+// (wave-end spread) shrinks, -0.04 ms at C3 (profiles/r5f)
+constexpr int kLateClaim = GCK_LATE_CLAIM;
 #ifndef GCK_STATIC_EIGHTHS
 #define GCK_STATIC_EIGHTHS 4
 #endif
@@ -1389,10 +1400,13 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         // the one after it (both land during this block)
         // pn (block qn) landed during the previous block: its record ends now,
         // the plan of the block after it next
-        const uint64_t qnn = grab();
+        uint64_t qnn = 0;
         Plan pnn;
         load_batch(pn, bn);
-        load_plan(qnn, pnn);
+        if constexpr (kLateClaim < 0) {
+            qnn = grab();
+            load_plan(qnn, pnn);
+        }
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
@@ -1411,6 +1425,12 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             for (int d = 1; d < 8; ++d)
                 if (qd * NR / 2 == d) nib = nibs[d];
             if constexpr (NR == 1) nib >>= 16 * (qd & 1);
+            if constexpr (kLateClaim >= 0) {
+                if (qd == kLateClaim) {  // (uniform)
+                    qnn = grab();
+                    load_plan(qnn, pnn);
+                }
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int st = qd * 4 + u;
@@ -2435,6 +2455,7 @@ static int ctx_run(Ctx *c) {
     c->n_live = 0;  // the keydir (and its pack) belong to the previous run
     c->kd_nparts = 0;
     c->kd_valid = false;
+    c->kd_hashed = false;
     if (c->rec_cap > 0 && c->nfiles > 0) {
         const int rc = ctx_run_device(c);
         if (rc != GCK_ERERUN) return rc;
