@@ -33,16 +33,18 @@ namespace {
 // CRC-32/IEEE for the read path (Get's lazy check, core/db.go:311).  Replay never
 // calls this: its verdicts come from the device pipeline.
 uint32_t crc32_host(const uint8_t *p, uint64_t n) {
-    static uint32_t T[256];
-    static bool ready = false;
-    if (!ready) {
-        for (uint32_t i = 0; i < 256; ++i) {
-            uint32_t c = i;
-            for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
-            T[i] = c;
+    struct Table {  // built once, thread-safe (a function-local static's initializer)
+        uint32_t t[256];
+        Table() {
+            for (uint32_t i = 0; i < 256; ++i) {
+                uint32_t c = i;
+                for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+                t[i] = c;
+            }
         }
-        ready = true;
-    }
+    };
+    static const Table tab;
+    const uint32_t *T = tab.t;
     uint32_t c = 0xFFFFFFFFu;
     for (uint64_t i = 0; i < n; ++i) c = T[(c ^ p[i]) & 0xff] ^ (c >> 8);
     return ~c;

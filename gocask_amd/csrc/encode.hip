@@ -22,21 +22,26 @@ namespace gck {
 
 constexpr uint32_t kZipfN = 65473;
 
-static std::vector<uint32_t> &zipf_thr() {
-    static std::vector<uint32_t> thr;
-    if (thr.empty()) {
+// Built once per process by a function-local static's initializer, which C++
+// runs exactly once even when several threads encode at once (bench.py
+// --lib-multi encodes a corpus per device from one thread each; a lazily
+// filled vector let a second thread sample a half-built table: a different
+// corpus, now and then).
+static const std::vector<uint32_t> &zipf_thr() {
+    static const std::vector<uint32_t> thr = [] {
         std::vector<double> cum(kZipfN);
         double acc = 0.0;
         for (uint32_t r = 1; r <= kZipfN; ++r) {
             acc += std::pow((double)r, -1.1);
             cum[r - 1] = acc;
         }
-        thr.resize(kZipfN - 1);
+        std::vector<uint32_t> t(kZipfN - 1);
         for (uint32_t k = 0; k + 1 < kZipfN; ++k) {
             const double v = std::floor(cum[k] / acc * 4294967296.0);
-            thr[k] = v >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)v;
+            t[k] = v >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)v;
         }
-    }
+        return t;
+    }();
     return thr;
 }
 

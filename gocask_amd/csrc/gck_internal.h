@@ -158,10 +158,21 @@ struct Ctx {
 
 int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after);
 
+// A data file: caller memory (data), or a path the copier opens per chunk it
+// reads (no descriptor is held across the call: a database with more files
+// than RLIMIT_NOFILE still opens, as the reference's Walk does, one at a time)
+struct Src {
+    const uint8_t *data;
+    const char *path;
+    uint64_t len;
+    bool reset_after;
+    uint64_t dev, ino;  // a path's file as stat saw it (each chunk's read checks it is the same)
+};
+
 // Host-to-device copies of gck_replay's file groups on one copy stream
 // (staging.hip): registered memory by the DMA engine directly (direct), the
 // rest through page-locked staging buffers filled by host threads (add:
-// memcpy from src, or pread from fd when src is null).  Group g's event is
+// memcpy from src, or pread of its path when src is null).  Group g's event is
 // recorded on the stream once every chunk of the group is queued (seal, then
 // wait_recorded before a stream waits on it).
 class Copier {
@@ -169,7 +180,7 @@ class Copier {
     Copier();
     ~Copier();
     int start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev);
-    void add(uint32_t group, const uint8_t *src, const char *path, uint64_t off, uint64_t len, uint8_t *dst);
+    void add(uint32_t group, const Src &src, uint64_t off, uint64_t len, uint8_t *dst);
     int direct(const uint8_t *src, uint64_t len, uint8_t *dst);
     void seal(uint32_t group);
     int wait_recorded(uint32_t group);
@@ -189,16 +200,6 @@ void *res_alloc(uint64_t bytes, bool pinned);
 void res_free(void *p);
 // dst = the segments back to back (host threads for large totals)
 void par_gather(uint8_t *dst, const std::vector<std::pair<const void *, uint64_t>> &segs);
-// A data file to replay: caller memory (data), or an open file (fd, data null)
-// A data file: caller memory (data), or a path the copier opens per chunk it
-// reads (no descriptor is held across the call: a database with more files
-// than RLIMIT_NOFILE still opens, as the reference's Walk does, one at a time)
-struct Src {
-    const uint8_t *data;
-    const char *path;
-    uint64_t len;
-    bool reset_after;
-};
 std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles);
 // gck_replay's ring of file groups with a hook instead of tuple delivery:
 // group(g, first file of the group, its context) runs after each group has
@@ -210,6 +211,8 @@ struct GroupSink {
     virtual int group(uint32_t g, uint32_t file0, gck_ctx *ctx) = 0;
 };
 int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, GroupSink *sink, gck_result *out);
+// the ring's data-byte budget when gck_opts.max_resident is 0 (replay.hip)
+int auto_budget(const gck_opts *opts, uint64_t *budget);
 // gck_replay_multi (multi.hip): one shard's outcome, the global outcome over
 // shards in walk order, the exchange's receive offsets, and the call itself
 // (loopback: several shards may share a device; every pair is a device copy)

@@ -460,6 +460,16 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
         dopt[s].device = devs[s];
         dopt[s].flags &= ~GCK_OPT_KEYS;
     }
+    // shards sharing a device (loopback) split its budget: each one sizing
+    // its ring from the same free memory and pool would overstate it k times
+    if (loopback && !(opts && opts->max_resident)) {
+        for (uint32_t s = 0; s < ndev; ++s) {
+            const uint64_t k = (uint64_t)std::count(devs.begin(), devs.end(), devs[s]);
+            uint64_t b = 0;
+            if ((rc = auto_budget(&dopt[s], &b))) return rc;
+            dopt[s].max_resident = std::max<uint64_t>(1, b / k);
+        }
+    }
     auto cleanup = [&]() {
         join_comm();
         for (uint32_t s = 0; s < ndev; ++s) {

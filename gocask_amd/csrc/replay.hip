@@ -2728,6 +2728,7 @@ uint64_t pool_bytes(const gck_opts *o) {
 }
 }  // namespace
 
+
 void gck_replay_release_cache(void) {
     std::vector<PoolEntry> all;
     {
@@ -2776,6 +2777,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     for (uint32_t f = 0; f < nfiles; ++f)
         if (files[f].len && !files[f].data && !files[f].path) return GCK_EINVAL;
     const uint64_t budget_opt = opts ? opts->max_resident : 0;
+    int rc0 = GCK_OK;
     // group target: about a quarter of the database (at least kGroupBytes),
     // or a third of a tight budget (so at least two groups of files smaller
     // than that fit at once).  Few groups: each is a device context, and
@@ -2805,15 +2807,13 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     const uint64_t maxg = std::max<uint64_t>(*std::max_element(gbytes.begin(), gbytes.end()), kRow);
     // ring size R: every group when the bytes fit the budget
     uint64_t budget = budget_opt;
-    if (!budget) {
-        size_t fr = 0, tt = 0;
-        if (hipSetDevice(opts ? opts->device : 0) != hipSuccess || hipMemGetInfo(&fr, &tt) != hipSuccess) {
-            (void)hipGetLastError();
-            return GCK_EDEVICE;
-        }
-        // records, stage and output add about a third to the data bytes
-        budget = (uint64_t)(kAutoBudgetShare * (double)(fr + pool_bytes(opts)) / 1.35);
-    }
+    if (!budget && (rc0 = auto_budget(opts, &budget))) return rc0;
+    // a sink (gck_replay_multi, GCK_OPT_LIVE) keeps each group's packed
+    // keydir on the device until the exchange: an eighth of the budget is
+    // left for those (C3: packs are ~1 % of the data bytes; a database of
+    // records under ~600 B can need more, and its pack allocation then fails
+    // with GCK_ENOMEM as a group that does not fit does)
+    if (sink) budget -= budget / 8;
     uint64_t fit = 0;
     for (uint32_t g = 0; g < G; ++g) fit += gbytes[g];
     const uint32_t R = fit <= budget ? G : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(G, budget / maxg));
@@ -2938,7 +2938,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
             if (pinned[f0 + k]) {
                 if ((r = cp.direct(f.data, f.len, d))) return r;
             } else {
-                cp.add(g, f.data, f.path, 0, f.len, d);
+                cp.add(g, f, 0, f.len, d);
             }
         }
         cp.seal(g);  // its event follows its last chunk on the copy stream
@@ -3211,6 +3211,18 @@ const char *gck_last_error(void) { return gck::last_error(); }
 }  // extern "C"
 
 namespace gck {
+// The data bytes a ring may hold when max_resident is 0: a share of the
+// device's free memory plus the arenas pooled for these options (records,
+// stage and output add about a third to the data bytes).
+int auto_budget(const gck_opts *opts, uint64_t *budget) {
+    size_t fr = 0, tt = 0;
+    if (hipSetDevice(opts ? opts->device : 0) != hipSuccess || hipMemGetInfo(&fr, &tt) != hipSuccess) {
+        (void)hipGetLastError();
+        return GCK_EDEVICE;
+    }
+    *budget = (uint64_t)(kAutoBudgetShare * (double)(fr + pool_bytes(opts)) / 1.35);
+    return GCK_OK;
+}
 int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, GroupSink *sink, gck_result *out) {
     if (!out || !sink || (nfiles && !files)) return GCK_EINVAL;
     return replay_grouped(files, nfiles, opts, false, nullptr, 0, out, sink);

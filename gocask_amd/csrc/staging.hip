@@ -105,7 +105,7 @@ int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const 
             if (src[f].data && host_pinned(src[f].data))
                 rc = cp.direct(src[f].data, src[f].len, dst[f]);
             else
-                cp.add(0, src[f].data, src[f].path, 0, src[f].len, dst[f]);
+                cp.add(0, src[f], 0, src[f].len, dst[f]);
         }
         cp.seal(0);
         if (!rc) rc = cp.wait_recorded(0);
@@ -119,12 +119,12 @@ int copy_files_sync(int dev, hipStream_t stream, const Src *src, uint8_t *const 
 
 std::vector<Src> mem_srcs(const gck_file *files, uint32_t nfiles) {
     std::vector<Src> v(nfiles);
-    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, nullptr, files[f].len, files[f].reset_after != 0};
+    for (uint32_t f = 0; f < nfiles; ++f) v[f] = Src{files[f].data, nullptr, files[f].len, files[f].reset_after != 0, 0, 0};
     return v;
 }
 
 int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &v) {
-    v.assign(nfiles, Src{nullptr, nullptr, 0, false});
+    v.assign(nfiles, Src{nullptr, nullptr, 0, false, 0, 0});
     for (uint32_t f = 0; f < nfiles; ++f) {
         struct stat st;
         if (!files[f].path || stat(files[f].path, &st) != 0 || !S_ISREG(st.st_mode)) {
@@ -136,6 +136,8 @@ int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &v) {
         v[f].path = files[f].path;
         v[f].len = (uint64_t)st.st_size;
         v[f].reset_after = files[f].reset_after != 0;
+        v[f].dev = (uint64_t)st.st_dev;
+        v[f].ino = (uint64_t)st.st_ino;
     }
     return GCK_OK;
 }
@@ -218,6 +220,7 @@ struct Copier::Impl {
     struct Job {
         const uint8_t *src;  // caller memory, or nullptr: pread of path at off
         const char *path;
+        uint64_t dev, ino;  // the file stat saw at path
         uint64_t off, len;
         uint8_t *dst;
         uint32_t group;
@@ -270,15 +273,23 @@ struct Copier::Impl {
             }
             (void)hipEventSynchronize(buf_ev[b]);  // the buffer's previous transfer
             uint8_t *stage = static_cast<uint8_t *>(bufs[b]);
-            bool ok = true;
+            bool ok = true, replaced = false;
             if (j.src) {
                 memcpy(stage, j.src + j.off, j.len);
             } else {
                 // the file is opened per chunk: at most one descriptor per
-                // copy thread is ever open
+                // copy thread is ever open.  Every chunk must come from the
+                // file open_srcs stat'ed (a rename over the path or an unlink
+                // and re-create in between would mix two files' bytes into
+                // one image): otherwise GCK_EIO, like an unreadable file
                 const int fd = open(j.path, O_RDONLY | O_CLOEXEC);
                 uint64_t got = 0;
                 ok = fd >= 0;
+                struct stat st;
+                if (ok && (fstat(fd, &st) != 0 || (uint64_t)st.st_dev != j.dev || (uint64_t)st.st_ino != j.ino)) {
+                    ok = false;
+                    replaced = true;
+                }
                 while (ok && got < j.len) {
                     const ssize_t r = pread(fd, stage + got, j.len - got, (off_t)(j.off + got));
                     if (r <= 0) {
@@ -290,10 +301,11 @@ struct Copier::Impl {
                 if (fd >= 0) close(fd);
             }
             std::lock_guard<std::mutex> lk(mu);
-            if (!ok && !err) {  // the file shrank or could not be read
+            if (!ok && !err) {  // the file shrank, could not be read, or was replaced
                 err = GCK_EIO;
-                set_error("pread of a data file failed (unreadable, or shorter than its stat size)", hipSuccess, __FILE__,
-                          __LINE__);
+                set_error(replaced ? "a data file was replaced while it was read (another inode at its path)"
+                                   : "pread of a data file failed (unreadable, or shorter than its stat size)",
+                          hipSuccess, __FILE__, __LINE__);
             }
             if (ok && (hipMemcpyAsync(j.dst, stage, j.len, hipMemcpyHostToDevice, stream) != hipSuccess ||
                        hipEventRecord(buf_ev[b], stream) != hipSuccess) &&
@@ -337,12 +349,12 @@ int Copier::start(int dev, hipStream_t stream, std::vector<hipEvent_t> *group_ev
     return GCK_OK;
 }
 
-void Copier::add(uint32_t group, const uint8_t *src, const char *path, uint64_t off, uint64_t len, uint8_t *dst) {
+void Copier::add(uint32_t group, const Src &src, uint64_t off, uint64_t len, uint8_t *dst) {
     std::lock_guard<std::mutex> lk(p->mu);
     const uint64_t C = stage_chunk();
     for (uint64_t o = 0; o < len; o += C) {
         const uint64_t n = std::min(C, len - o);
-        p->jobs.push_back(Impl::Job{src, path, off + o, n, dst + o, group});
+        p->jobs.push_back(Impl::Job{src.data, src.path, src.dev, src.ino, off + o, n, dst + o, group});
         ++p->pending[group];
     }
     p->cv_job.notify_all();
