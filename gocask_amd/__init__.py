@@ -9,14 +9,14 @@ from .core import (GB, KB, MB, TB, Config, DB, DefaultConfig, ErrCRCFailed, ErrI
                    NewInMemory, Open, ReplayContext, StartupError, WithDataDir, WithMaxDataFileSize, device_count,
                    host_register, host_unregister, keydir, plan_shards, release_cache, replay, replay_into, replay_paths,
                    replay_multi, replay_multi_paths, zipf_table, multi_resolve, multi_recv_offsets,
-                   replay_multi_loopback, multi_keydir)
-from ._lib import F_CRC_OK, F_TOMBSTONE, REC_DTYPE
+                   replay_multi_loopback, multi_keydir, replay_hints)
+from ._lib import F_CRC_OK, F_HINT, F_TOMBSTONE, REC_DTYPE
 
 __all__ = [
     "GB", "KB", "MB", "TB", "Config", "DB", "DefaultConfig", "ErrCRCFailed", "ErrInvalidKey", "ErrInvalidValue",
     "ErrKeyNotFound", "ErrPartialWrite", "ErrUnexpectedEOF", "GoCaskError", "InMemoryDB", "NewDB", "NewDisk",
     "NewInMemory", "Open", "ReplayContext", "StartupError", "WithDataDir", "WithMaxDataFileSize", "device_count",
     "host_register", "host_unregister", "keydir", "plan_shards", "release_cache", "replay", "replay_into", "replay_paths",
-    "replay_multi", "replay_multi_paths", "zipf_table", "multi_resolve", "multi_recv_offsets", "replay_multi_loopback", "multi_keydir",
-    "F_CRC_OK", "F_TOMBSTONE", "REC_DTYPE",
+    "replay_multi", "replay_multi_paths", "zipf_table", "multi_resolve", "multi_recv_offsets", "replay_multi_loopback", "multi_keydir", "replay_hints",
+    "F_CRC_OK", "F_HINT", "F_TOMBSTONE", "REC_DTYPE",
 ]

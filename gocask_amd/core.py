@@ -257,6 +257,24 @@ def replay(files, reset_after=None, device=0, chunk_bytes=0, max_key=0, chunk_ca
         L.gck_result_free(ctypes.byref(res))
 
 
+def replay_hints(hint_files, reset_after=None, device=0, keys=False, live=False):
+    """gck_replay_hints: the tuples of the data files behind hint_files (one
+    per data file, walk order; reset_after as for the data files) from the
+    hints alone.  Returns (records, status); live=True: the keydir (last entry
+    per key); keys=True: status["keys"] = the records' key bytes."""
+    L = _lib.load()
+    if reset_after is None:
+        reset_after = [True] * len(hint_files)
+    fa, arrs = _files_struct(hint_files, reset_after)
+    res = GckResult()
+    rc = L.gck_replay_hints(fa, len(arrs), ctypes.byref(_opts(device, 0, 0, 0, 0, 0, keys, live)), ctypes.byref(res))
+    try:
+        check(rc)
+        return _result(res)
+    finally:
+        L.gck_result_free(ctypes.byref(res))
+
+
 def replay_paths(paths, reset_after=None, device=0, chunk_bytes=0, max_resident=0, keys=False, live=False):
     """gck_replay_paths: the same replay of files named by path (read by the
     library with pread into page-locked staging buffers).  Returns (records,
@@ -561,6 +579,15 @@ class ReplayContext:
             a += int(fsz[k])
             b += int(hsz[k])
         return files, hfiles, ms.value
+
+    def replay_hints(self):
+        """Hint-driven replay of the hint files loaded into this context
+        (gck_ctx_replay_hints): the tuples a run of their data files gives,
+        flags F_HINT, from the hints alone.  Returns the device ms; fetch() /
+        keydir() then work as after run()."""
+        ms = ctypes.c_double()
+        check(self._L.gck_ctx_replay_hints(self._h, ctypes.byref(ms)))
+        return ms.value
 
     # -- batched Get / scrub (include/gocask_hip.h, SURVEY.md §8f f3) --
     def get_batch(self, keys, values=True):

@@ -6,11 +6,14 @@
 // database with MaxDataFileSize M (core/db.go:185-231: an entry that does not
 // fit rotates first, rotateDataFile:214-231), each record's bytes verbatim
 // (header, key, value: CRCs and timestamps unchanged).  One hint file per data
-// file lists its records as hint entries (invented here, no CRC), little-endian
-//   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
+// file (format invented here, include/gocask_hip.h GCK_HINT_*), little-endian:
+//   entries [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][CRC u32][key]
+//   index   [hint offset u64][data-file offset u64] of every GCK_HINT_BLOCK-th entry
+//   tail    [entries u64][entry bytes u64][data-file bytes u64][magic u32][version u32]
 // (ValuePos = the value's offset in the merged file mod 2^32, as
-// core/keydir.go:25 would set it), so a later start can fill the keydir
-// without reading values.
+// core/keydir.go:25 would set it; CRC = kdEntry.CRC), so a later start fills
+// the keydir without reading values (hints.hip), in parallel over the blocks
+// the index lists.
 //
 // Kernels: sizes and two-level exclusive scans of record and hint-entry
 // sizes; the rotation points (few files: one wavefront, a 64-way search per
@@ -26,6 +29,12 @@ namespace gck {
 typedef uint32_t u32x4_a4c __attribute__((ext_vector_type(4), aligned(4)));
 
 constexpr uint32_t kCmpBlock = 1024;  // records per first-level scan block
+constexpr uint64_t kHintHdr = 20;      // hint entry header bytes (GCK_HINT_*)
+constexpr uint64_t kHintTail = 32;
+// index + tail bytes of a hint file of n entries
+__host__ __device__ __forceinline__ uint64_t hint_footer(uint64_t n) {
+    return 16 * ((n + GCK_HINT_BLOCK - 1) / GCK_HINT_BLOCK) + kHintTail;
+}
 
 __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
 #pragma unroll
@@ -36,7 +45,7 @@ __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
     return v;
 }
 
-// Per record: data size 16 + KeySize + ValueSize and hint size 16 + KeySize;
+// Per record: data size 16 + KeySize + ValueSize and hint size 20 + KeySize;
 // exclusive scans within blocks of kCmpBlock, block totals to bsum / hbsum.
 __global__ __launch_bounds__(kCmpBlock) void k_cmp_sizes(const gck_rec *__restrict__ kd, uint64_t n,
                                                          uint64_t *__restrict__ pos, uint64_t *__restrict__ hpos,
@@ -48,7 +57,7 @@ __global__ __launch_bounds__(kCmpBlock) void k_cmp_sizes(const gck_rec *__restri
     if (i < n) {
         const gck_rec r = kd[i];
         sz = 16ull + r.key_len + r.value_size;
-        hs = 16ull + r.key_len;
+        hs = kHintHdr + r.key_len;
     }
     const uint64_t a = wave_incl_sum64(sz), b = wave_incl_sum64(hs);
     if (lane == 63) {
@@ -270,6 +279,10 @@ __device__ __forceinline__ void st16u(uint8_t *dst, uint4 v) {
     x.w = v.w;
     *reinterpret_cast<u32x4_a1 *>(dst) = x;
 }
+__device__ __forceinline__ void st4u(uint8_t *dst, uint32_t v) {
+    typedef uint32_t u32_a1 __attribute__((aligned(1)));
+    *reinterpret_cast<u32_a1 *>(dst) = v;
+}
 __device__ __forceinline__ uint4 ld16u(const uint8_t *p) {
     const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
     const uint8_t *a = p - sh;
@@ -374,11 +387,13 @@ __global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ ar
     }
 }
 
-// Hint entries: a lane per record (16 + KeySize bytes each).
+// Hint entries: a lane per record (20 + KeySize bytes each), at hpos[i] plus
+// the index and tail bytes of the files before its own (foot[f]); the lane of
+// every GCK_HINT_BLOCK-th record of a file writes its index entry.
 __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
                             const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
-                            const uint64_t *__restrict__ hpos, const uint32_t *__restrict__ fstart, uint32_t nf,
-                            uint64_t n, uint8_t *__restrict__ hints) {
+                            const uint64_t *__restrict__ hpos, const uint32_t *__restrict__ fstart,
+                            const uint64_t *__restrict__ foot, uint32_t nf, uint64_t n, uint8_t *__restrict__ hints) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const gck_rec r = kd[i];
@@ -388,8 +403,9 @@ __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *_
         const uint32_t mid = (lo + hi + 1) / 2;
         if (fstart[mid] <= i) lo = mid; else hi = mid - 1;
     }
-    const uint64_t fo = pos[i] - pos[fstart[lo]];  // the record's offset in its merged file
-    uint8_t *d = hints + hpos[i];
+    const uint64_t i0 = fstart[lo], fo = pos[i] - pos[i0];  // the record's offset in its merged file
+    const uint64_t h0 = hpos[i0] + foot[lo];                // the hint file's first byte
+    uint8_t *d = hints + hpos[i] + foot[lo];
     const uint8_t *key = arena + fbase[r.file] + r.rec_off + 16;
     // 16 B pieces at any alignment: the key's last 16 bytes first (a key
     // under 16 B reaches back into the entry's header, from the record's
@@ -397,9 +413,29 @@ __global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *_
     // the header -- one thread's stores land in program order.  (Byte stores:
     // 370 us for C3's 138 MB of hints, pieces 215 us, profiles/r4zzf.)
     const uint32_t kl = r.key_len;
-    if (kl & 15) st16u(d + kl, ld16u(key + kl - 16));
-    for (uint32_t k = 0; k + 16 <= kl; k += 16) st16u(d + 16 + k, ld16u(key + k));
+    if (kl & 15) st16u(d + kHintHdr + kl - 16, ld16u(key + kl - 16));
+    for (uint32_t k = 0; k + 16 <= kl; k += 16) st16u(d + kHintHdr + k, ld16u(key + k));
     st16u(d, make_uint4(r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)));
+    st4u(d + 16, r.crc);
+    const uint64_t j = i - i0;
+    if (j % GCK_HINT_BLOCK == 0) {  // the block's index entry, after the file's entries
+        const uint64_t ebytes = hpos[fstart[lo + 1]] - hpos[i0];
+        uint8_t *x = hints + h0 + ebytes + 16 * (j / GCK_HINT_BLOCK);
+        st16u(x, make_uint4((uint32_t)(hpos[i] - hpos[i0]), (uint32_t)((hpos[i] - hpos[i0]) >> 32), (uint32_t)fo,
+                            (uint32_t)(fo >> 32)));
+    }
+}
+
+// Every hint file's tail (a lane per file; a file may have no entries).
+__global__ void k_cmp_hint_tails(const uint64_t *__restrict__ pos, const uint64_t *__restrict__ hpos,
+                                 const uint32_t *__restrict__ fstart, const uint64_t *__restrict__ foot, uint32_t nf,
+                                 uint8_t *__restrict__ hints) {
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= nf) return;
+    const uint64_t a = fstart[f], b = fstart[f + 1], ne = b - a, eb = hpos[b] - hpos[a], db = pos[b] - pos[a];
+    uint8_t *t = hints + hpos[a] + foot[f] + eb + hint_footer(ne) - kHintTail;
+    st16u(t, make_uint4((uint32_t)ne, (uint32_t)(ne >> 32), (uint32_t)eb, (uint32_t)(eb >> 32)));
+    st16u(t + 16, make_uint4((uint32_t)db, (uint32_t)(db >> 32), GCK_HINT_MAGIC, GCK_HINT_VERSION));
 }
 
 }  // namespace gck
@@ -425,7 +461,7 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
     // the keydir must describe the last run (gck_ctx_run invalidates it), and
     // that run must have opened: the reference refuses a database whose replay
     // hit a startup error (core/db.go:134-138), so there is nothing to merge
-    if (!c->kd_valid || c->status != GCK_OK) return GCK_EINVAL;
+    if (!c->kd_valid || c->status != GCK_OK || c->from_hints) return GCK_EINVAL;  // (a hint replay holds no records)
     if (c->kd_flags & GCK_KD_KEEP_TOMBSTONES) return GCK_EINVAL;  // a merge keeps Puts only
     GCK_HIP(hipSetDevice(c->device));
     const uint64_t n = c->n_live;
@@ -477,7 +513,20 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
     }
     GCK_HIP(hipMemcpyAsync(&nf, c->d_cnf.p, 4, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
-    if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16))) return rc;
+    // each hint file's index and tail follow its entries: foot[f] = the index
+    // and tail bytes of the files before f (from the files' record counts)
+    std::vector<uint32_t> fs(nf + 1);
+    GCK_HIP(hipMemcpy(fs.data(), c->d_cfstart.p, (nf + 1) * 4ull, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> foot(nf + 1, 0);
+    for (uint32_t k = 0; k < nf; ++k) {
+        if (fs[k] > fs[k + 1] || fs[k + 1] > n) return GCK_EDEVICE;  // file starts in order (never trusted blindly)
+        foot[k + 1] = foot[k] + hint_footer(fs[k + 1] - fs[k]);
+    }
+    tot[1] += foot[nf];
+    if ((rc = c->d_cdata.ensure(tot[0] + 16)) || (rc = c->d_chint.ensure(tot[1] + 16)) ||
+        (rc = c->d_cfoot.ensure((nf + 1) * 8ull)))
+        return rc;
+    GCK_HIP(hipMemcpyAsync(c->d_cfoot.p, foot.data(), (nf + 1) * 8ull, hipMemcpyHostToDevice, s));
     if (n) {
         const uint64_t groups = (n + 63) / 64;
         // 16 wavefronts per CU, groups from an atomic queue: 6.41-6.43 ms on
@@ -491,9 +540,12 @@ extern "C" int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n
                                         c->d_cdata.as<uint8_t>(), queue);
         k_cmp_hints<<<(uint32_t)((n + 255) / 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(),
                                                                c->d_kdout.as<gck_rec>(), pos, hpos,
-                                                               c->d_cfstart.as<uint32_t>(), nf, n,
-                                                               c->d_chint.as<uint8_t>());
+                                                               c->d_cfstart.as<uint32_t>(), c->d_cfoot.as<uint64_t>(),
+                                                               nf, n, c->d_chint.as<uint8_t>());
     }
+    if (nf)
+        k_cmp_hint_tails<<<(nf + 255) / 256, 256, 0, s>>>(pos, hpos, c->d_cfstart.as<uint32_t>(), c->d_cfoot.as<uint64_t>(),
+                                                         nf, c->d_chint.as<uint8_t>());
     GCK_HIP(hipGetLastError());
     GCK_HIP(hipEventRecord(ev.b, s));
     GCK_HIP(hipEventSynchronize(ev.b));
@@ -526,7 +578,7 @@ extern "C" int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file
         GCK_HIP(hipMemcpy(hpos.data(), c->d_chpos.p, (n + 1) * 8, hipMemcpyDeviceToHost));
         for (uint32_t k = 0; k < nf; ++k) {
             if (file_sizes) file_sizes[k] = pos[fs[k + 1]] - pos[fs[k]];
-            if (hint_sizes) hint_sizes[k] = hpos[fs[k + 1]] - hpos[fs[k]];
+            if (hint_sizes) hint_sizes[k] = hpos[fs[k + 1]] - hpos[fs[k]] + hint_footer(fs[k + 1] - fs[k]);
         }
     }
     if (data && c->cmp_data) GCK_HIP(hipMemcpy(data, c->d_cdata.p, c->cmp_data, hipMemcpyDeviceToHost));

@@ -120,7 +120,7 @@ struct Ctx {
     uint32_t kd_flags = 0;                                // flags of the last gck_ctx_keydir
     // compaction (compact.hip): record / hint-entry offsets, block sums, file
     // starts, file count, merged data and hint bytes
-    DBuf d_cpos, d_chpos, d_cbsum, d_cfstart, d_cnf, d_cdata, d_chint;
+    DBuf d_cpos, d_chpos, d_cbsum, d_cfstart, d_cnf, d_cdata, d_chint, d_cfoot;
     DBuf d_cjmp, d_con;  // many-file rotation points: jump pointers (two copies), start marks
     uint32_t cmp_files = 0;
     uint64_t cmp_data = 0, cmp_hint = 0;
@@ -144,6 +144,7 @@ struct Ctx {
     uint32_t err_file = 0, files_walked = 0, final_last_offset = 0;
     uint64_t err_off = 0, n_crc_fail = 0, n_fixups = 0, n_overflow = 0;
     bool device_path = false;  // the last run had no host round trip (ctx_run_device)
+    bool from_hints = false;   // the tuples came from hint files (hints.hip): the arena holds no data files
     uint32_t n_reruns = 0;     // device-only runs redone on the host path
     double ms_total = 0, ms_phase[PH_NPHASE] = {};
     bool phase_timing = false;  // an event between every phase (gck_ctx_phase_timing)
@@ -228,6 +229,8 @@ int replay_multi(const Src *files, uint32_t nfiles, const std::vector<int> &devs
 // the pool of idle contexts behind gck_replay (per device, one options key each)
 int pool_take(const gck_opts *o, gck_ctx **out);
 void pool_give(const gck_opts *o, gck_ctx *c);
+// the last run's key bytes back to back into a new pinned host buffer (replay.hip)
+int ctx_gather_keys(Ctx *c, void **host, uint64_t *len);
 // stats every path (GCK_EIO when one fails); the paths must outlive the call
 int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &out);
 void close_srcs(std::vector<Src> &v);

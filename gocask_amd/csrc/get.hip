@@ -225,7 +225,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
                       uint64_t *val_off, double *ms) {
     if (!ctx || !key_off || !status || !value_size || !crc_calc || (values && !val_off)) return GCK_EINVAL;
     Ctx *c = &ctx->c;
-    if (!c->kd_valid) return GCK_EINVAL;  // gck_ctx_keydir after the run first
+    if (!c->kd_valid || c->from_hints) return GCK_EINVAL;  // gck_ctx_keydir after the run first (values: data files)
     if (ms) *ms = 0;
     if (!n) return GCK_OK;
     for (uint32_t i = 0; i < n; ++i)
@@ -312,7 +312,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
 int gck_ctx_scrub_keydir(gck_ctx *ctx, int32_t *status, uint32_t *crc_calc, uint64_t *n_bad, double *ms) {
     if (!ctx || !n_bad) return GCK_EINVAL;
     Ctx *c = &ctx->c;
-    if (!c->kd_valid) return GCK_EINVAL;
+    if (!c->kd_valid || c->from_hints) return GCK_EINVAL;  // (a hint replay's arena holds no values)
     *n_bad = 0;
     if (ms) *ms = 0;
     const uint64_t n = c->n_live;

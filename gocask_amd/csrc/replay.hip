@@ -1979,7 +1979,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
                    &c->d_gvoff, &c->d_gvals, &c->d_gscan, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
-                   &c->d_cdata, &c->d_chint, &c->d_cjmp, &c->d_con, &c->d_klb, &c->d_koff, &c->d_keyblob};
+                   &c->d_cdata, &c->d_chint, &c->d_cfoot, &c->d_cjmp, &c->d_con, &c->d_klb, &c->d_koff, &c->d_keyblob};
     for (DBuf *b : all) b->release();
     if (c->h_mbox) (void)hipHostFree(c->h_mbox);
     c->h_mbox = c->d_mbox = nullptr;
@@ -2456,6 +2456,7 @@ static int ctx_run(Ctx *c) {
     c->kd_nparts = 0;
     c->kd_valid = false;
     c->kd_hashed = false;
+    c->from_hints = false;
     if (c->rec_cap > 0 && c->nfiles > 0) {
         const int rc = ctx_run_device(c);
         if (rc != GCK_ERERUN) return rc;
@@ -3229,6 +3230,7 @@ int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, Gr
 }
 int pool_take(const gck_opts *o, gck_ctx **out) { return pool_take_(o, out); }
 void pool_give(const gck_opts *o, gck_ctx *c) { pool_give_(o, c); }
+int ctx_gather_keys(Ctx *c, void **host, uint64_t *len) { return gather_keys(c, host, len); }
 }  // namespace gck
 
 extern "C" {

@@ -60,6 +60,7 @@ typedef struct gck_file {
 
 #define GCK_F_TOMBSTONE 1u /* header KeySize == 0 (core/header.go:54-56)              */
 #define GCK_F_CRC_OK 2u    /* CRC-32/IEEE(last ValueSize bytes) == header CRC           */
+#define GCK_F_HINT 4u      /* from a hint file (gck_ctx_replay_hints): value not read   */
 
 /* One record per header decoded, in walk order (superseded records and tombstones
  * included).  40 bytes, no padding. */
@@ -224,17 +225,44 @@ int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * not fit rotates first, core/db.go:214-231; a first record larger than the
  * limit leaves the first file empty), each record's bytes verbatim (header,
  * key, value: CRCs and timestamps unchanged).  One hint file per data file
- * lists its records as little-endian hint entries (format invented here, parity
- * unpinned: the reference has no hint files; the header CRC is not included)
- *   [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][key bytes]
+ * (format invented here, parity unpinned: the reference has no hint files),
+ * little-endian:
+ *   entries [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][CRC u32][key bytes]
+ *   index   [hint-file offset u64][data-file offset u64] of entries 0, B, 2B, ...
+ *           (B = GCK_HINT_BLOCK)
+ *   tail    [entries u64][entry bytes u64][data-file bytes u64][GCK_HINT_MAGIC u32]
+ *           [GCK_HINT_VERSION u32]
  * (ValuePos = the value's offset in its merged file mod 2^32, as
- * core/keydir.go:25 sets it on a replay of the merged files).  The outputs stay
+ * core/keydir.go:25 sets it on a replay of the merged files; CRC = the
+ * record header's, kdEntry.CRC), so gck_replay_hints fills the keydir without
+ * reading the data files, in parallel over the index's blocks.  The outputs stay
  * on the device: *n_files, *data_bytes (all files back to back), *hint_bytes;
  * gck_ctx_fetch_compact copies them and the per-file sizes out (any pointer
  * may be NULL).  *ms (optional) = device time. */
+#define GCK_HINT_BLOCK 16u
+#define GCK_HINT_MAGIC 0x484B4347u /* "GCKH" */
+#define GCK_HINT_VERSION 2u
 int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n_files, uint64_t *data_bytes,
                     uint64_t *hint_bytes, double *ms);
 int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file_sizes, uint8_t *hints, uint64_t *hint_sizes);
+
+/* Hint-driven replay (row f4; the reference's roadmap "hint files",
+ * README.md:60): the tuples of a database whose data files all have hint files
+ * (gck_ctx_compact's), from the hints alone -- no data-file byte is read.
+ * The context's arena holds the hint files (gck_ctx_load, in walk order, each
+ * with its data file's reset_after); afterwards the context's tuples are one
+ * gck_rec per hint entry in walk order, each equal to the one gck_ctx_run
+ * gives for that record on the data files (rec_off, file, key_len, value_pos
+ * with the carried lastOffset, value_size, crc, ts) except flags = GCK_F_HINT
+ * and crc_calc = 0 (the value is not read, so there is no CRC verdict), with
+ * status GCK_OK, files_walked and final_last_offset as a replay; gck_ctx_fetch,
+ * gck_ctx_keydir (last entry per key across several merges' hints) and the
+ * rest work on them as on a run's.  GCK_EINVAL when a hint file is malformed
+ * (tail, index and entries must agree).  *ms (optional) = device time. */
+int gck_ctx_replay_hints(gck_ctx *ctx, double *ms);
+/* One-shot form (host hint files in, tuples out, as gck_replay; GCK_OPT_KEYS
+ * returns the key bytes, GCK_OPT_LIVE the keydir: last entry per key). */
+int gck_replay_hints(const gck_file *files, uint32_t nfiles, const gck_opts *opts, gck_result *out);
 
 /* ---- batched Get / keydir scrub -------------------------
  * DB.Get (core/db.go:287-316) for n keys against the device keydir of the last

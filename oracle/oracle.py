@@ -284,6 +284,28 @@ def tombstone(now: int, key: bytes) -> bytes:
     return struct.pack("<IIII", zlib.crc32(key), now & 0xFFFFFFFF, 0, len(key)) + key
 
 
+HINT_MAGIC, HINT_VERSION, HINT_BLOCK = 0x484B4347, 2, 16
+
+
+def hint_file(entries, data_bytes):
+    """One hint file (format invented here, parity unpinned: the reference has
+    no hint files).  entries: [(ts, key, value_size, value_pos, crc, rec_off)]
+    of one merged data file in record order; little-endian
+      entries [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][CRC u32] + key
+      index   per block of HINT_BLOCK entries: [hint offset u64][data-file offset u64]
+              of the block's first entry
+      tail    [entries u64][entry bytes u64][data-file bytes u64][magic u32][version u32]
+    so a reader finds every block of entries without walking the file, and a
+    record's offset in its data file (rec_off) past 4 GiB, where ValuePos wraps."""
+    body, index = bytearray(), bytearray()
+    for j, (ts, key, vs, vpos, crc, rec_off) in enumerate(entries):
+        if j % HINT_BLOCK == 0:
+            index += struct.pack("<QQ", len(body), rec_off)
+        body += struct.pack("<IIIII", ts, len(key), vs, vpos, crc) + key
+    tail = struct.pack("<QQQII", len(entries), len(body), data_bytes, HINT_MAGIC, HINT_VERSION)
+    return bytes(body + index + tail)
+
+
 def compact(files, recs, reset_after, max_file_size):
     """Merge (compaction) restated — the reference's roadmap item "merging and
     hint files" (README.md:60), defined as: the live records of the keydir
@@ -292,31 +314,41 @@ def compact(files, recs, reset_after, max_file_size):
     DB.Put (core/db.go:185-212) rotates when the active file's size + the
     entry > MaxDataFileSize (rotateDataFile, :214-231; the fresh database's
     first file starts empty) — each record's bytes verbatim.  Per merged file
-    its hint entries, little-endian [Timestamp][KeySize][ValueSize][ValuePos]
-    u32 + key (Bitcask's hint layout; ValuePos = the value's offset in the
-    merged file mod 2^32, as core/keydir.go:25 sets it).
+    a hint file (hint_file): per record [Timestamp][KeySize][ValueSize]
+    [ValuePos][CRC] + key, ValuePos = the value's offset in the merged file
+    mod 2^32 as core/keydir.go:25 sets it, CRC = the header's (kdEntry.CRC),
+    so the keydir can be filled without reading the data files.
     Returns (list of data-file bytes, list of hint-file bytes)."""
     kd = keydir(files, recs, reset_after)
     live = sorted(kd.values(), key=lambda r: (int(r["file"]), int(r["rec_off"])))
-    data, hints = [bytearray()], [bytearray()]
+    data, ents = [bytearray()], [[]]
     for r in live:
         f, o = files[int(r["file"])], int(r["rec_off"])
         kl, vs = int(r["key_len"]), int(r["value_size"])
         b = bytes(f[o:o + 16 + kl + vs])
         if len(data[-1]) + len(b) > max_file_size:
             data.append(bytearray())
-            hints.append(bytearray())
+            ents.append([])
         vpos = (len(data[-1]) + 16 + kl) & 0xFFFFFFFF
-        hints[-1] += struct.pack("<IIII", int(r["ts"]), kl, vs, vpos) + b[16:16 + kl]
+        ents[-1].append((int(r["ts"]), b[16:16 + kl], vs, vpos, int(r["crc"]), len(data[-1])))
         data[-1] += b
-    return [bytes(d) for d in data], [bytes(h) for h in hints]
+    return [bytes(d) for d in data], [hint_file(e, len(d)) for e, d in zip(ents, data)]
 
 
 def parse_hints(h):
-    """Hint entries of one hint file: [(timestamp, key, value_size, value_pos)]."""
-    out, p = [], 0
-    while p < len(h):
-        ts, kl, vs, vpos = struct.unpack_from("<IIII", h, p)
-        out.append((ts, bytes(h[p + 16:p + 16 + kl]), vs, vpos))
-        p += 16 + kl
+    """Hint entries of one hint file (hint_file's format), walked from the
+    start and checked against its index and tail: [(timestamp, key,
+    value_size, value_pos, crc, rec_off)]."""
+    n, nbytes, dbytes, magic, ver = struct.unpack_from("<QQQII", h, len(h) - 32)
+    nb = (n + HINT_BLOCK - 1) // HINT_BLOCK
+    assert magic == HINT_MAGIC and ver == HINT_VERSION and len(h) == nbytes + 16 * nb + 32
+    out, p, d = [], 0, 0
+    for j in range(n):
+        if j % HINT_BLOCK == 0:
+            assert struct.unpack_from("<QQ", h, nbytes + 16 * (j // HINT_BLOCK)) == (p, d)
+        ts, kl, vs, vpos, crc = struct.unpack_from("<IIIII", h, p)
+        out.append((ts, bytes(h[p + 20:p + 20 + kl]), vs, vpos, crc, d))
+        p += 20 + kl
+        d += 16 + kl + vs
+    assert p == nbytes and d == dbytes
     return out
