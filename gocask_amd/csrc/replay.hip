@@ -1540,7 +1540,20 @@ __device__ __forceinline__ uint32_t crc_block(const uint32_t *T, uint32_t c, con
     return c;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_finalize(const uint8_t *__restrict__ arena,
+// 8 wavefronts per workgroup share one set of tables, among them x^{-8d} for
+// every d < 4096 (16 KiB: a lookup instead of a multiply; 61 KiB per
+// workgroup, two per CU): 0.467-0.473 against 0.476-0.477 ms with 4
+// wavefronts and the two-table multiply (profiles/r5k)
+#ifndef GCK_FIN_XI
+#define GCK_FIN_XI 1
+#endif
+#if GCK_FIN_XI
+constexpr uint32_t kFinThreads = 512;
+#else
+constexpr uint32_t kFinThreads = 256;
+#endif
+constexpr uint32_t kFinWaves = kFinThreads / 64;
+__global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint2 *__restrict__ rec_kv,
                                                   const uint32_t *__restrict__ rec_file,
@@ -1559,32 +1572,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     // R[y & 15]) in 32 copies.  A wave's output staging (64 gck_rec = 2560 B)
     // reuses bytes 256.. of its region (the M entries 1..15, rewritten by every
     // gf_mul_lds; LDS operations of one wave execute in order)
-    __shared__ uint32_t Gm[4 * 1024 + 512];
+    __shared__ uint32_t Gm[kFinWaves * 1024 + 512];
     // the shift constants every record needs, from small LDS tables instead
     // of random global loads (each a distinct line per lane for the TA):
     // x^{-8d}, d < 4096, as two 64-entry tables (d & 63, 64 (d >> 6)), and
     // x^{8v}, v < 65536, as two byte tables (v & 0xFF, 256 (v >> 8)); one
     // more multiply each
+#if GCK_FIN_XI
+    __shared__ uint32_t Xi[4096];  // x^{-8d}, d < 4096: no multiply
+#else
     __shared__ uint32_t Xi[128];
+#endif
     __shared__ uint32_t Xb[512];
     for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) {
         Tz[i] = zrow[i];
         T[i] = g_slice[i];
     }
+#if GCK_FIN_XI
+    for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) Xi[i] = xinv[i];
+#else
     for (uint32_t i = threadIdx.x; i < 64; i += blockDim.x) {
         Xi[i] = xinv[i];
         Xi[64 + i] = xinv[64 * i];
     }
+#endif
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
         Xb[i] = xb[i];
         Xb[256 + i] = xb[256 * i];
     }
-    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) Gm[4096 + i] = mulx(mulx(mulx(mulx(i >> 5))));
+    for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) Gm[kFinWaves * 1024 + i] = mulx(mulx(mulx(mulx(i >> 5))));
     Gm[(threadIdx.x >> 6) * 1024 + (threadIdx.x & 63)] = 0;  // entry 0 of every lane
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     char *const ldsb = reinterpret_cast<char *>(Gm);  // byte offsets into Gm
-    const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = 4096 * 4 + (lane & 31) * 4;
+    const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = kFinWaves * 4096 + (lane & 31) * 4;
     uint4 *const Ost = reinterpret_cast<uint4 *>(ldsb + (threadIdx.x >> 6) * 4096 + 256);
     const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
     uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
@@ -1736,8 +1757,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         // (a bit-serial VALU product in place of any of these four measured
         // slower: 0.47-0.64 ms against 0.46-0.47, profiles/r3j/ab_finvalu.log)
         auto mul = [&](uint32_t a, uint32_t b) { return gf_mul_lds(ldsb, mw, rxb, a, b); };
-#ifdef GCK_FIN_GTAB
+#if defined(GCK_FIN_GTAB)
         const uint32_t xi = o.xi;
+#elif GCK_FIN_XI
+        const uint32_t xi = Xi[g.d];  // x^{-8d}
 #else
         const uint32_t xi = mul(Xi[64 + (g.d >> 6)], Xi[g.d & 63]);  // x^{-8d}
 #endif
@@ -1832,12 +1855,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         cur = nxt;
     }
 #ifdef GCK_CLOCK_STAMPS
-    if ((threadIdx.x & 63) == 0 && blockIdx.x * 4 + (threadIdx.x >> 6) < kClkWaves) {
-        g_fin_split[2 * (blockIdx.x * 4 + (threadIdx.x >> 6))] = fin_wait;
-        g_fin_split[2 * (blockIdx.x * 4 + (threadIdx.x >> 6)) + 1] = fin_comp;
+    if ((threadIdx.x & 63) == 0 && blockIdx.x * kFinWaves + (threadIdx.x >> 6) < kClkWaves) {
+        g_fin_split[2 * (blockIdx.x * kFinWaves + (threadIdx.x >> 6))] = fin_wait;
+        g_fin_split[2 * (blockIdx.x * kFinWaves + (threadIdx.x >> 6)) + 1] = fin_comp;
     }
 #endif
-    GCK_CLK_END(5, blockIdx.x * 4 + (threadIdx.x >> 6));
+    GCK_CLK_END(5, blockIdx.x * kFinWaves + (threadIdx.x >> 6));
     // one global atomic per block (per-record or per-wavefront atomics on one
     // address serialise: C5 has ~100k rejects)
     __shared__ uint32_t blk_rej;
@@ -1932,7 +1955,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
     int bpc = 0;
-    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), 256, 0));
+    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), kFinThreads, 0));
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
@@ -2214,9 +2237,9 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
     if (!max_recs) return;
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
-    const uint64_t want = nblk(max_recs, 256), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
+    const uint64_t want = nblk(max_recs, kFinThreads), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
     const uint32_t grid = (uint32_t)(want < res ? want : res);
-    k_finalize<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
+    k_finalize<<<grid, kFinThreads, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
