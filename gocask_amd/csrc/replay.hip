@@ -1090,7 +1090,10 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 // 0.6 ms after the median against 0.13 now): 5.45-5.56 against 5.18-5.20 ms on
 // one box (profiles/r4f/ab_r2_head_port.log, profiles/r4a/bisect_r3_commits.log).
 // Compare the ISA (hipcc --cuda-device-only -S) before and after any edit.
-constexpr int kPrefetch = 1;  // steps between a row's loads and its processing (2, 3 measured slower)
+#ifndef GCK_PREFETCH
+#define GCK_PREFETCH 1
+#endif
+constexpr int kPrefetch = GCK_PREFETCH;  // steps between a row's loads and its processing (2, 3 measured slower)
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
                                                    const uint32_t *__restrict__ row_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
