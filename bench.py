@@ -526,9 +526,12 @@ def main():
         dist1.destroy_process_group()
     elif dist is not None and not args.no_merge:
         merge = keydir_merge(g, ctx, dist, info["n_files"])
-    stream_gbs = None
+    stream_gbs = blocks_gbs = None
     if rank == 0:
         _, stream_gbs = ctx.stream_read_ceiling(5)
+        # the balanced ceiling: k_crc_rows' own work split (64-row blocks, half
+        # static, half from the queue) streamed with no compute
+        _, blocks_gbs = ctx.stream_blocks_ceiling(5)
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
         value = total_bytes * args.steps / elapsed / GiB
@@ -580,6 +583,11 @@ def main():
                         "averaged over the timed steps (one launch per step over all files)",
                 "stream_read_gbs": round(stream_gbs, 1),
                 "frac_of_stream_read": round(achieved / stream_gbs, 4),
+                "balanced_ceiling_gbs": round(blocks_gbs, 1),
+                "frac_of_balanced_ceiling": round(achieved / blocks_gbs, 4),
+                "ceilings_note": "stream_read: a static grid-stride non-temporal read of the arena; balanced: the same "
+                                 "bytes in k_crc_rows' 64-row blocks and work split, no compute (both right after "
+                                 "the timed steps, HIP events)",
             },
             "phase_ms": {k: round(v / n_phase, 4) for k, v in phases_sum.items()},
         }
