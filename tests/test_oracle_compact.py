@@ -38,3 +38,32 @@ def test_oracle_compact_roundtrip(orc, name, max_size):
     ents = [e for h in hints for e in orc.parse_hints(h)]
     assert [(e[0], e[2], e[3]) for e in ents] == [(int(r["ts"]), int(r["value_size"]), int(r["value_pos"]))
                                                   for r in got_recs]
+
+
+def test_oracle_hint_format(orc):
+    """hint_file's layout (the format gck_replay_hints reads; invented here,
+    parity unpinned): entries [Timestamp][KeySize][ValueSize][ValuePos][CRC] +
+    key, an index entry (hint offset, data offset) per HINT_BLOCK entries, a
+    32-byte tail; parse_hints walks it and checks index and tail; the CRC
+    field is the record header's (kdEntry.CRC, core/keydir.go:3-9)."""
+    import struct
+
+    files, names = orc.gen_corpus(seed=61, val_fixed=0, key_min=8, key_max=40, key_universe=300,
+                                  tomb_permille=50, max_file_size=1 << 18, n_files=2)
+    wf = [files[i] for i in sorted(range(len(files)), key=lambda i: names[i])]
+    reset = [True, False]
+    recs, _ = orc.replay(wf, reset)
+    data, hints = orc.compact(wf, recs, reset, 1 << 15)
+    B = orc.HINT_BLOCK
+    for d, h in zip(data, hints):
+        ents = orc.parse_hints(h)
+        n, eb, db, magic, ver = struct.unpack_from("<QQQII", h, len(h) - 32)
+        assert (n, db, magic, ver) == (len(ents), len(d), orc.HINT_MAGIC, orc.HINT_VERSION)
+        assert len(h) == eb + 16 * ((n + B - 1) // B) + 32
+        for ts, key, vs, vpos, crc, rec_off in ents:  # each entry describes its record in the data file
+            hcrc, hts, ks, hvs = struct.unpack_from("<IIII", d, rec_off)
+            assert (hcrc, hts, ks, hvs) == (crc, ts, len(key), vs)
+            assert d[rec_off + 16:rec_off + 16 + ks] == key and vpos == rec_off + 16 + ks
+    # an empty merge: one empty data file, a tail-only hint file
+    assert orc.hint_file([], 0) == struct.pack("<QQQII", 0, 0, 0, orc.HINT_MAGIC, orc.HINT_VERSION)
+    assert orc.parse_hints(orc.hint_file([], 0)) == []
