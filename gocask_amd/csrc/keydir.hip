@@ -44,19 +44,48 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
         const uint32_t tag = slot_tag(h);
         const unsigned long long mine = ((unsigned long long)tag << 32) | r;
         for (uint64_t s = h & mask;; s = (s + 1) & mask) {
+            unsigned long long *slot = table + kSlotWords * s;
             // a plain read: a slot only goes EMPTY -> (tag, i) -> (tag, larger
             // i), so a stale value is EMPTY (the CAS then returns the truth) or
             // an older record of the same key
-            unsigned long long cur = table[s];
+#if GCK_KD_WIDE
+            const ulonglong2 sv = *reinterpret_cast<const ulonglong2 *>(slot);
+            unsigned long long cur = sv.x, kw = sv.y;
+#else
+            unsigned long long cur = slot[0];
+#endif
             if (cur == kEmptySlot) {
-                const unsigned long long prev = atomicCAS(table + s, kEmptySlot, mine);
-                if (prev == kEmptySlot) break;  // claimed
+                const unsigned long long prev = atomicCAS(slot, kEmptySlot, mine);
+                if (prev == kEmptySlot) {  // claimed
+#if GCK_KD_WIDE
+                    slot[1] = slot_key_word(rec_off[r] + 16, len);
+#endif
+                    break;
+                }
                 cur = prev;
+#if GCK_KD_WIDE
+                kw = kEmptySlot;
+#endif
             }
             if ((uint32_t)(cur >> 32) != tag) continue;
             const uint32_t ci = (uint32_t)cur;
+#if GCK_KD_WIDE
+            if (kw == kEmptySlot) kw = slot[1];  // (the claimer's key word may have landed since)
+            bool same;
+            if (kw != kEmptySlot && (uint32_t)(kw >> 48) != 0xFFFFu) {
+                same = (uint32_t)(kw >> 48) == len;
+                if (same) {
+                    const KeyWords ka(arena, kw & kKeyOffMask, len), kb(arena, rec_off[r] + 16, len);
+                    for (uint32_t w = 0; same && 4 * w < len; ++w) same = ka[w] == kb[w];
+                }
+            } else {
+                same = key_len(rec_kv[ci]) == len && same_key(arena, rec_off, ci, r, len);
+            }
+            if (same) {
+#else
             if (key_len(rec_kv[ci]) == len && same_key(arena, rec_off, ci, r, len)) {
-                if (ci < r) atomicMax(table + s, mine);  // same key: the later record wins
+#endif
+                if (ci < r) atomicMax(slot, mine);  // same key: the later record wins
                 break;
             }
         }
@@ -70,7 +99,7 @@ __global__ __launch_bounds__(256) void k_kd_mark(const unsigned long long *__res
                                                  const uint2 *__restrict__ rec_kv, uint32_t keep_tombstones,
                                                  uint32_t *__restrict__ live) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
-        const unsigned long long v = table[s];
+        const unsigned long long v = table[kSlotWords * s];
         if (v == kEmptySlot) continue;
         const uint32_t r = (uint32_t)v;
         if (keep_tombstones || rec_kv[r].x != 0) live[r] = 1;
@@ -357,7 +386,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     while (slots < n + n / 4) slots <<= 1;  // load <= 0.8 with every key distinct; slots hold keys, not records
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
     int rc;
-    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 8)) || (rc = c->d_live.ensure(n * 4)) ||
+    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_live.ensure(n * 4)) ||
         (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))) ||
         (rc = c->d_kdidx.ensure(n * 4)))
         return rc;
@@ -365,7 +394,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
     GCK_HIP(hipEventRecord(a, s));
-    GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8, s));
+    GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
     GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
     const uint32_t grid = (uint32_t)c->n_cu * 8;
     k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), n,
