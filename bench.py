@@ -603,13 +603,24 @@ def main():
             out["roofline"]["frac_max_over_ranks"] = max(fr)
         if args.keydir:
             ctx.keydir()  # warm-up (allocations)
+            ctx.phase_timing(True)
             ctx.run()  # a fresh run: its first keydir hashes every key
+            fin_plain = ctx.stats()["ms_phase"]["finalize"]
             live, kd_ms = ctx.keydir()
             _, kd_again_ms = ctx.keydir(fetch=False)
+            ctx.keydir_hash(True)  # the run's finalize hashes the keys instead
+            ctx.run()
+            fin_hash = ctx.stats()["ms_phase"]["finalize"]
+            _, kd_hashed_ms = ctx.keydir(fetch=False)
+            ctx.keydir_hash(False)
+            ctx.phase_timing(False)
             out["keydir"] = dict(ms=round(kd_ms, 3), live_entries=len(live), records=st["n_recs"],
-                                 rebuild_ms=round(kd_again_ms, 3),
+                                 rebuild_ms=round(kd_again_ms, 3), after_finalize_hash_ms=round(kd_hashed_ms, 3),
+                                 finalize_ms_plain=round(fin_plain, 4), finalize_ms_hashing=round(fin_hash, 4),
                                  note="gck_ctx_keydir, the first after a run (row f1): last record per key, Puts "
                                       "kept; rebuild_ms = a second keydir of the same run (key hashes kept); "
+                                      "after_finalize_hash_ms = the first keydir after a run whose finalize hashed "
+                                      "the keys (gck_ctx_keydir_hash), which costs finalize the difference shown; "
                                       "not part of value")
             ctx.scrub_keydir()  # warm-up
             _, _, bad, sc_ms = ctx.scrub_keydir()

@@ -54,7 +54,7 @@ assert KD_ENTRY_DTYPE.itemsize == 64
 # Every symbol include/gocask_hip.h declares (tests check the .so exports them).
 EXPORTED = [
     "gck_replay", "gck_replay_into", "gck_replay_paths", "gck_result_free", "gck_replay_release_cache", "gck_ctx_create", "gck_ctx_destroy", "gck_ctx_load", "gck_ctx_run", "gck_ctx_phase_timing",
-    "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_ctx_compact", "gck_ctx_fetch_compact", "gck_ctx_replay_hints", "gck_replay_hints", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_replay_multi", "gck_replay_multi_paths", "gck_ctx_multi_keydir", "gck_plan_shards", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
+    "gck_ctx_fetch", "gck_ctx_fetch_into", "gck_ctx_keydir", "gck_ctx_keydir_hash", "gck_ctx_fetch_keydir", "gck_ctx_get_batch", "gck_ctx_scrub_keydir", "gck_ctx_compact", "gck_ctx_fetch_compact", "gck_ctx_replay_hints", "gck_replay_hints", "gck_kd_pack_sizes", "gck_kd_pack", "gck_kd_merge", "gck_kd_fetch_merged", "gck_replay_multi", "gck_replay_multi_paths", "gck_ctx_multi_keydir", "gck_plan_shards", "gck_ctx_stats", "gck_phase_name", "gck_ctx_device_recs", "gck_ctx_stream",
     "gck_ctx_read_file", "gck_encode_corpus", "gck_encode_files", "gck_encode_walk_order", "gck_encode_zipf_table", "gck_encode_batch", "gck_db_open",
     "gck_db_open_mem", "gck_db_get", "gck_db_keys", "gck_db_key", "gck_db_entry", "gck_db_last_offset",
     "gck_db_active_file", "gck_db_nfiles", "gck_db_file_name", "gck_db_close", "gck_device_count", "gck_host_register", "gck_host_unregister",
@@ -198,6 +198,7 @@ def load():
         "gck_ctx_fetch_into": (ctypes.c_int, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
         "gck_ctx_keydir": (ctypes.c_int, [vp, ctypes.c_uint32, P(ctypes.c_uint64), P(ctypes.c_double)]),
         "gck_ctx_fetch_keydir": (ctypes.c_int, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
+        "gck_ctx_keydir_hash": (ctypes.c_int, [vp, ctypes.c_int]),
         "gck_ctx_get_batch": (ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint64, vp,
                                              P(ctypes.c_double)]),
         "gck_ctx_scrub_keydir": (ctypes.c_int, [vp, vp, vp, P(ctypes.c_uint64), P(ctypes.c_double)]),

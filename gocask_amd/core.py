@@ -540,6 +540,11 @@ class ReplayContext:
         check(self._L.gck_ctx_fetch_into(self._h, recs.ctypes.data, recs.size, ctypes.byref(n)))
         return n.value
 
+    def keydir_hash(self, on=True):
+        """gck_ctx_keydir_hash: the next runs hash every record's key in their
+        finalize pass, so keydir() reads no key bytes to hash them."""
+        check(self._L.gck_ctx_keydir_hash(self._h, 1 if on else 0))
+
     def keydir(self, keep_tombstones=False, fetch=True):
         """Device keydir of the last run (gck_ctx_keydir + gck_ctx_fetch_keydir):
         (live REC_DTYPE records in walk order, device ms); with fetch=False

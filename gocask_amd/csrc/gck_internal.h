@@ -117,6 +117,7 @@ struct Ctx {
     DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout, d_kdidx;
     uint64_t n_live = 0;
     bool kd_hashed = false;  // d_khash holds the key hashes of the last run's records
+    bool hash_keys = false;  // runs hash every record's key in finalize (gck_ctx_keydir_hash)
     uint32_t kd_flags = 0;                                // flags of the last gck_ctx_keydir
     // compaction (compact.hip): record / hint-entry offsets, block sums, file
     // starts, file count, merged data and hint bytes

@@ -26,6 +26,7 @@
 #include <thread>
 
 #include "gck_internal.h"
+#include "kd_common.h"
 #include "gck_crc_lds.h"
 #include "gck_crc_wave.h"
 
@@ -1556,6 +1557,10 @@ constexpr uint32_t kFinThreads = 512;
 constexpr uint32_t kFinThreads = 256;
 #endif
 constexpr uint32_t kFinWaves = kFinThreads / 64;
+// HASH: also each record's key hash (kd_common.h key_hash, what k_kd_insert
+// would compute) into khash[r], from the key words the record's header + key
+// CRC already holds in registers (gck_ctx_keydir_hash)
+template <bool HASH>
 __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
                                                   const uint2 *__restrict__ rec_kv,
@@ -1568,7 +1573,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                                                   const uint32_t *__restrict__ zrow,
                                                   const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
-                                                  uint32_t *counters) {
+                                                  uint32_t *counters, uint64_t *__restrict__ khash) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
     // gf_mul_lds: one 4 KiB table region per wave, then R (y * x^4 = (y >> 4) ^
@@ -1825,6 +1830,29 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
             }
             __builtin_amdgcn_wave_barrier();
             n_rej += valid && calc != hcrc;
+            if constexpr (HASH) {
+                // key_hash (kd_common.h) of the record's key: KeySize bytes at
+                // rs + 16, or ValueSize for a tombstone (core/db.go:151-155).
+                // A Put's key of up to 28 - lead bytes is in pw (words 4..11,
+                // byte shift lead); other keys are read again.
+                const uint32_t klen = kv.x ? kv.x : kv.y;
+                uint64_t hh = 0x9E3779B97F4A7C15ull ^ ((uint64_t)klen << 32);
+                if (kv.x != 0 && klen + lead <= 28) {
+#pragma unroll
+                    for (uint32_t i = 0; i < 7; ++i) {
+                        if (4 * i < klen) {
+                            uint32_t v = __builtin_amdgcn_alignbyte(pw[5 + i], pw[4 + i], lead);
+                            const uint32_t left = klen - 4 * i;
+                            v = left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
+                            hh = mix64d(hh ^ v) + i;
+                        }
+                    }
+                } else {
+                    const KeyWords k(arena, rs + 16, klen);
+                    for (uint32_t i = 0; 4 * i < klen; ++i) hh = mix64d(hh ^ k[i]) + i;
+                }
+                if (valid) khash[base + lane] = mix64d(hh);
+            }
         }
     };
     // The record table one iteration ahead, the loads that depend on it
@@ -1958,7 +1986,7 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
     int bpc = 0;
-    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize), kFinThreads, 0));
+    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize<false>), kFinThreads, 0));
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
@@ -2237,18 +2265,20 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
 }
 
 static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
+    auto kern = c->hash_keys ? k_finalize<true> : k_finalize<false>;
     if (!max_recs) return;
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
     const uint64_t want = nblk(max_recs, kFinThreads), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
     const uint32_t grid = (uint32_t)(want < res ? want : res);
-    k_finalize<<<grid, kFinThreads, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
+    kern<<<grid, kFinThreads, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
                                     rng, c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>(),
                                     c->d_slice.as<uint32_t>(), c->d_xinv.as<uint32_t>(),
                                     c->d_zrow.as<uint32_t>(),
                                     c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
-                                    c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>());
+                                    c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>(),
+                                    c->hash_keys ? c->d_khash.as<uint64_t>() : nullptr);
 }
 
 static int ensure_records(Ctx *c, uint64_t nr) {
@@ -2256,7 +2286,7 @@ static int ensure_records(Ctx *c, uint64_t nr) {
     int rc;
     if ((rc = c->d_rec_off.ensure(nr * 8)) || (rc = c->d_rec_kv.ensure(nr * 8)) ||
         (rc = c->d_rec_file.ensure(nr * 4)) || (rc = c->d_ep.ensure((nr + kEpScratch) * kEpBytes)) ||
-        (rc = c->d_out.ensure(nr * sizeof(gck_rec))))
+        (rc = c->d_out.ensure(nr * sizeof(gck_rec))) || (c->hash_keys && (rc = c->d_khash.ensure(nr * 8))))
         return rc;
     return GCK_OK;
 }
@@ -2391,6 +2421,7 @@ static int ctx_run_host(Ctx *c) {
     c->ms_phase[PH_PIPE] = span;
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
+    c->kd_hashed = c->hash_keys;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
 }
@@ -2472,9 +2503,18 @@ static int ctx_run_device(Ctx *c) {
     c->ms_phase[PH_CRC] = el(PH_CRC, PH_FINAL);
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
+    c->kd_hashed = c->hash_keys;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
+}
+
+// gck_ctx_keydir_hash: finalize also hashes every record's key into d_khash
+// (sized for the record table's capacity now; ensure_records keeps it so)
+static int ctx_set_hash_keys(Ctx *c, bool on) {
+    c->hash_keys = on;
+    if (on && c->rec_cap) return c->d_khash.ensure(c->rec_cap * 8);
+    return GCK_OK;
 }
 
 static int ctx_run(Ctx *c) {
@@ -2545,6 +2585,12 @@ int gck_ctx_load(gck_ctx *ctx, const gck_file *files, uint32_t nfiles) {
     if (!ctx || (nfiles && !files)) return GCK_EINVAL;
     const std::vector<Src> v = mem_srcs(files, nfiles);
     return ctx_load_srcs(&ctx->c, v.data(), nfiles);
+}
+
+int gck_ctx_keydir_hash(gck_ctx *ctx, int on) {
+    if (!ctx) return GCK_EINVAL;
+    if (hipSetDevice(ctx->c.device) != hipSuccess) return GCK_EDEVICE;
+    return ctx_set_hash_keys(&ctx->c, on != 0);
 }
 
 int gck_ctx_run(gck_ctx *ctx) {
@@ -2998,6 +3044,12 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
             break;
         }
         const auto tr0 = std::chrono::steady_clock::now();
+        // a sink builds each group's keydir: its keys are hashed in the
+        // group's finalize pass (gck_ctx_keydir then reads no key for them)
+        if (int hr = ctx_set_hash_keys(c, sink != nullptr)) {
+            rc = hr;
+            break;
+        }
         const int r = ctx_run(c);
         if (trace)
             fprintf(stderr, "[gck_replay] group %u (slot %u) run returned at %.2f ms (run call %.2f ms, device path %d)\n",

@@ -214,6 +214,11 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * sets db.kd.entries[key] for each (key bytes at rec_off + 16 in the file). */
 #define GCK_KD_KEEP_TOMBSTONES 1u
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
+/* on: the next runs also hash every record's key in their finalize pass (the
+ * key bytes are in registers there), so gck_ctx_keydir reads no key bytes to
+ * hash them; off (the default) for runs that build no keydir.  gck_replay*
+ * with GCK_OPT_LIVE and gck_replay_multi* turn it on for their groups. */
+int gck_ctx_keydir_hash(gck_ctx *ctx, int on);
 int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 
 /* ---- merge (compaction) and hint files ------------------

@@ -1,0 +1,73 @@
+"""Keys hashed in the finalize pass (gck_ctx_keydir_hash): the keydir built
+from those hashes must be the oracle's keydir (keyDir.set / unset over every
+record in walk order, core/keydir.go:22-49) and the keydir of a run that did
+not hash -- Puts whose key sits in the record's header + key registers and
+the others (tombstones, keys longer than 28 - (offset mod 4) bytes), with and
+without tombstones kept, for a second keydir of the same run, and after the
+flag is turned off again."""
+import numpy as np
+import pytest
+
+from golden_cases import case_names, load_case
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def g():
+    import __graft_entry__
+
+    __graft_entry__.build()
+    import gocask_amd
+
+    assert gocask_amd.device_count() > 0, "no GPU visible"
+    return gocask_amd
+
+
+def _keydirs(g, files, reset, keep):
+    with g.ReplayContext() as ctx:
+        ctx.load(files, reset)
+        ctx.run()
+        plain, _ = ctx.keydir(keep_tombstones=keep)
+        ctx.keydir_hash(True)
+        ctx.run()
+        hashed, _ = ctx.keydir(keep_tombstones=keep)
+        again, _ = ctx.keydir(keep_tombstones=keep)  # the same run: the kept hashes
+        ctx.keydir_hash(False)
+        ctx.run()
+        off, _ = ctx.keydir(keep_tombstones=keep)
+    return plain, hashed, again, off
+
+
+def _check(g, orc, files, reset, keep):
+    plain, hashed, again, off = _keydirs(g, files, reset, keep)
+    for other in (hashed, again, off):
+        assert np.array_equal(other, plain)
+    if not keep:
+        want, _ = orc.replay(files, reset)
+        kd = orc.keydir(files, want, reset)
+        assert len(plain) == len(kd)
+
+
+@pytest.mark.parametrize("name", case_names())
+@pytest.mark.parametrize("keep", [False, True])
+def test_keydir_hash_golden(g, orc, name, keep):
+    _, files, reset = load_case(name)
+    _check(g, orc, files, reset, keep)
+
+
+@pytest.mark.parametrize("seed,kw", [
+    (101, dict(val_fixed=0, key_min=8, key_max=24, key_universe=2000, tomb_permille=100, max_file_size=1 << 20,
+               n_files=3)),
+    (102, dict(val_fixed=0, key_min=8, key_max=200, key_universe=500, tomb_permille=200, max_file_size=1 << 20,
+               n_files=2)),
+    (103, dict(val_fixed=17, key_min=9, key_max=31, key_universe=300, tomb_permille=50, flip_permille=50,
+               max_file_size=1 << 19, n_files=4)),
+])
+@pytest.mark.parametrize("keep", [False, True])
+def test_keydir_hash_random(g, orc, seed, kw, keep):
+    files, names = orc.gen_corpus(seed=seed, **kw)
+    walk = sorted(range(len(files)), key=lambda i: names[i])
+    wf = [files[i] for i in walk]
+    reset = [i + 1 < len(wf) for i in range(len(wf))]
+    _check(g, orc, wf, reset, keep)

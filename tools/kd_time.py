@@ -9,8 +9,13 @@ import gocask_amd as g  # noqa: E402
 ctx = g.ReplayContext()
 ctx.encode(**bench.CONFIGS["c3"])
 ctx.run()
-for _ in range(3):
-    ctx.run()  # the first keydir of a run hashes every key
-    n, ms = ctx.keydir(fetch=False)
-    _, again = ctx.keydir(fetch=False)  # the same run: hashes kept
-    print("keydir_ms", round(ms, 3), "rebuild_ms", round(again, 3), "live", n, flush=True)
+ctx.phase_timing(True)
+for hashed in (False, True, False, True):
+    ctx.keydir_hash(hashed)  # on: the run's finalize hashes the keys
+    for _ in range(2):
+        ctx.run()
+        st = ctx.stats()
+        n, ms = ctx.keydir(fetch=False)
+        _, again = ctx.keydir(fetch=False)  # the same run: hashes kept
+        print("finalize_hash", int(hashed), "finalize_ms", round(st["ms_phase"]["finalize"], 4),
+              "keydir_ms", round(ms, 3), "rebuild_ms", round(again, 3), "live", n, flush=True)
