@@ -618,9 +618,10 @@ def main():
                                  rebuild_ms=round(kd_again_ms, 3), after_finalize_hash_ms=round(kd_hashed_ms, 3),
                                  finalize_ms_plain=round(fin_plain, 4), finalize_ms_hashing=round(fin_hash, 4),
                                  note="gck_ctx_keydir, the first after a run (row f1): last record per key, Puts "
-                                      "kept; rebuild_ms = a second keydir of the same run (key hashes kept); "
-                                      "after_finalize_hash_ms = the first keydir after a run whose finalize hashed "
-                                      "the keys (gck_ctx_keydir_hash), which costs finalize the difference shown; "
+                                      "kept; rebuild_ms = a second keydir of the same run (its table kept: marking and compaction only); "
+                                      "after_finalize_hash_ms = the keydir after a run whose finalize hashed the keys "
+                                      "and inserted them into the keydir table (gck_ctx_keydir_hash; what GCK_OPT_LIVE "
+                                      "runs), which costs finalize the difference shown; "
                                       "not part of value")
             ctx.scrub_keydir()  # warm-up
             _, _, bad, sc_ms = ctx.scrub_keydir()

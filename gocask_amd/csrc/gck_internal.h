@@ -115,8 +115,12 @@ struct Ctx {
     // device keydir (keydir.hip): key hashes, slot table, live flags, tile
     // ranks, the live records
     DBuf d_khash, d_ktab, d_live, d_ktile, d_kdout, d_kdidx;
+    DBuf d_kdstat;  // keydir table: [0] overflow (a key found no slot in kMaxProbe), [1] keys (claimed slots)
     uint64_t n_live = 0;
     bool kd_hashed = false;  // d_khash holds the key hashes of the last run's records
+    bool kd_inserted = false;  // d_ktab holds the last run's records (its finalize inserted them)
+    uint64_t kd_tab_slots = 0;  // d_ktab's slots then
+    uint64_t kd_keys_hint = 0;  // distinct keys of the last keydir built here (sizes the next table)
     bool hash_keys = false;  // runs hash every record's key in finalize (gck_ctx_keydir_hash)
     uint32_t kd_flags = 0;                                // flags of the last gck_ctx_keydir
     // compaction (compact.hip): record / hint-entry offsets, block sums, file

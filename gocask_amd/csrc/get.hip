@@ -39,27 +39,17 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
             const uint32_t len = (uint32_t)len64;
             const KeyWords k(keys, koff[q], len);
             const uint64_t h = key_hash(k, len), mask = slots - 1;
-            const uint32_t tag = slot_tag(h);
-            for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-#if GCK_KD_WIDE
-                const ulonglong2 sv = *reinterpret_cast<const ulonglong2 *>(table + kSlotWords * s);
-                const unsigned long long v = sv.x;
-                if (v == kEmptySlot) break;
-                const uint32_t cur = (uint32_t)v;
-                if ((uint32_t)(v >> 32) != tag) continue;
-                const bool kw_ok = sv.y != kEmptySlot && (uint32_t)(sv.y >> 48) != 0xFFFFu;
-                if ((kw_ok ? (uint32_t)(sv.y >> 48) : key_len(rec_kv[cur])) != len) continue;
-                const KeyWords a(arena, kw_ok ? (sv.y & kKeyOffMask) : rec_off[cur] + 16, len);
-#else
-                const unsigned long long v = table[s];
-                if (v == kEmptySlot) break;
-                const uint32_t cur = (uint32_t)v;
-                if ((uint32_t)(v >> 32) != tag || key_len(rec_kv[cur]) != len) continue;
-                const KeyWords a(arena, rec_off[cur] + 16, len);
-#endif
-                bool same = true;
-                for (uint32_t i = 0; same && 4 * i < len; ++i) same = a[i] == k[i];
-                if (!same) continue;
+            const unsigned long long want = slot_word0(h, len, 0) >> 32;  // tag | length
+            uint64_t s = h & mask;
+            for (uint32_t probe = 0; probe < kMaxProbe; ++probe, s = (s + 1) & mask) {  // (kd_insert_rec's bound)
+                const unsigned long long *slot = table + kSlotWords * s;
+                const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(slot);
+                if (a.x == kEmptySlot) break;
+                if ((a.x >> 32) != want) continue;
+                const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(slot + 2);
+                const unsigned long long w[3] = {a.y, b.x, b.y};
+                const uint32_t cur = (uint32_t)a.x;
+                if (!slot_key_equal(arena, rec_off, rec_kv, w, cur, [&](uint32_t i) { return k[i]; }, len)) continue;
                 const gck_rec r = recs[cur];
                 if (!(r.flags & GCK_F_TOMBSTONE)) {
                     // os.File.ReadAt into an empty buffer returns (0, nil) at any

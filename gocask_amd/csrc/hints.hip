@@ -197,6 +197,7 @@ int gck_ctx_replay_hints(gck_ctx *ctx, double *ms) {
     c->kd_nparts = 0;
     c->kd_valid = false;
     c->kd_hashed = false;
+    c->kd_inserted = false;
     c->from_hints = true;
     c->n_recs = 0;
     const uint32_t nf = c->nfiles;

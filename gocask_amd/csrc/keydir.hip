@@ -11,21 +11,8 @@
 
 namespace gck {
 
-__device__ bool same_key(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off, uint64_t a,
-                         uint64_t b, uint32_t len) {
-    const KeyWords ka(arena, rec_off[a] + 16, len), kb(arena, rec_off[b] + 16, len);
-    for (uint32_t i = 0; 4 * i < len; ++i)
-        if (ka[i] != kb[i]) return false;
-    return true;
-}
-
 // k_kd_insert: one lane per record: the 64-bit hash of its key (kept in
-// khash for the merge), then an open-addressing insert into a table of
-// (tag, record index) slots.  A slot is claimed by CAS; a probe compares the
-// slot's tag before any key bytes; records of the same key (tag, length and
-// bytes equal) keep the largest index with a 64-bit atomicMax, so the last
-// writer in walk order wins whatever order the lanes run in.  Keys are never
-// removed, so a probe sequence never skips a key's slot.  Lanes take the
+// khash for the merge), then its insert (kd_common.h kd_insert_rec).  Lanes take the
 // records from the last one back: a key's later record then mostly claims its
 // slot first and the earlier ones skip the atomicMax (C3: 1.85 -> 1.78 ms).
 // A second keydir of the same run (hashed) reads the hashes kept in khash
@@ -35,75 +22,35 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
                                                    const uint2 *__restrict__ rec_kv, uint64_t n,
                                                    uint64_t *__restrict__ khash,
                                                    unsigned long long *__restrict__ table, uint64_t mask,
-                                                   int hashed) {
+                                                   int hashed, uint32_t *__restrict__ kstat) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = n - 1 - i;
         const uint32_t len = key_len(rec_kv[r]);
-        const uint64_t h = hashed ? khash[r] : key_hash(KeyWords(arena, rec_off[r] + 16, len), len);
+        const KeyRegs k(arena, rec_off[r] + 16, len);
+        const uint64_t h = hashed ? khash[r] : key_hash(k.m, len);
         if (!hashed) khash[r] = h;
-        const uint32_t tag = slot_tag(h);
-        const unsigned long long mine = ((unsigned long long)tag << 32) | r;
-        for (uint64_t s = h & mask;; s = (s + 1) & mask) {
-            unsigned long long *slot = table + kSlotWords * s;
-            // a plain read: a slot only goes EMPTY -> (tag, i) -> (tag, larger
-            // i), so a stale value is EMPTY (the CAS then returns the truth) or
-            // an older record of the same key
-#if GCK_KD_WIDE
-            const ulonglong2 sv = *reinterpret_cast<const ulonglong2 *>(slot);
-            unsigned long long cur = sv.x, kw = sv.y;
-#else
-            unsigned long long cur = slot[0];
-#endif
-            if (cur == kEmptySlot) {
-                const unsigned long long prev = atomicCAS(slot, kEmptySlot, mine);
-                if (prev == kEmptySlot) {  // claimed
-#if GCK_KD_WIDE
-                    slot[1] = slot_key_word(rec_off[r] + 16, len);
-#endif
-                    break;
-                }
-                cur = prev;
-#if GCK_KD_WIDE
-                kw = kEmptySlot;
-#endif
-            }
-            if ((uint32_t)(cur >> 32) != tag) continue;
-            const uint32_t ci = (uint32_t)cur;
-#if GCK_KD_WIDE
-            if (kw == kEmptySlot) kw = slot[1];  // (the claimer's key word may have landed since)
-            bool same;
-            if (kw != kEmptySlot && (uint32_t)(kw >> 48) != 0xFFFFu) {
-                same = (uint32_t)(kw >> 48) == len;
-                if (same) {
-                    const KeyWords ka(arena, kw & kKeyOffMask, len), kb(arena, rec_off[r] + 16, len);
-                    for (uint32_t w = 0; same && 4 * w < len; ++w) same = ka[w] == kb[w];
-                }
-            } else {
-                same = key_len(rec_kv[ci]) == len && same_key(arena, rec_off, ci, r, len);
-            }
-            if (same) {
-#else
-            if (key_len(rec_kv[ci]) == len && same_key(arena, rec_off, ci, r, len)) {
-#endif
-                if (ci < r) atomicMax(slot, mine);  // same key: the later record wins
-                break;
-            }
-        }
+        if (!kd_insert_rec(arena, rec_off, rec_kv, table, mask, h, r, k, len))
+            atomicOr(kstat, 1u);
     }
 }
 
 // k_kd_mark: one lane per slot; the key's winning record is live if it is a
 // Put (or, for a merge across shards, always: tombstones then stay as delete
-// markers).
+// markers).  The keys (claimed slots) are counted into
+// kstat[1]: the next table of this context is sized by them.
 __global__ __launch_bounds__(256) void k_kd_mark(const unsigned long long *__restrict__ table, uint64_t slots,
                                                  const uint2 *__restrict__ rec_kv, uint32_t keep_tombstones,
-                                                 uint32_t *__restrict__ live) {
+                                                 uint32_t *__restrict__ live, uint32_t *__restrict__ kstat) {
+    uint32_t keys = 0;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long v = table[kSlotWords * s];
         if (v == kEmptySlot) continue;
+        ++keys;
         const uint32_t r = (uint32_t)v;
         if (keep_tombstones || rec_kv[r].x != 0) live[r] = 1;
     }
+    for (int o = 32; o > 0; o >>= 1) keys += __shfl_down(keys, o);
+    if ((threadIdx.x & 63) == 0 && keys) atomicAdd(kstat + 1, keys);
 }
 
 // Exclusive rank of v inside a workgroup of kKdTile lanes; the total is out.
@@ -382,42 +329,71 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     if (n >= kEmpty) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
-    uint64_t slots = 1024;
-    while (slots < n + n / 4) slots <<= 1;  // load <= 0.8 with every key distinct; slots hold keys, not records
+    // the run's finalize may have filled the table already (gck_ctx_keydir_hash):
+    // then only the marking and the compaction are left, for every keydir of
+    // that run (they do not change the table)
+    bool filled = c->kd_inserted;
+    uint64_t slots = filled ? c->kd_tab_slots : kd_table_slots(kd_keys_expected(c->kd_keys_hint, n));
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
     int rc;
-    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_live.ensure(n * 4)) ||
+    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_live.ensure(n * 4)) || (rc = c->d_kdstat.ensure(8)) ||
         (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))) ||
         (rc = c->d_kdidx.ensure(n * 4)))
         return rc;
-    hipEvent_t a, b;
-    GCK_HIP(hipEventCreate(&a));
-    GCK_HIP(hipEventCreate(&b));
-    GCK_HIP(hipEventRecord(a, s));
-    GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
-    GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
-    const uint32_t grid = (uint32_t)c->n_cu * 8;
-    k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), n,
-                                     c->d_khash.as<uint64_t>(), c->d_ktab.as<unsigned long long>(), slots - 1,
-                                     c->kd_hashed ? 1 : 0);
-    c->kd_hashed = true;
-    k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_kv.as<uint2>(),
-                                   (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>());
-    k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
-    k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);
-    k_kd_scatter<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>(),
-                                                  c->d_out.as<gck_rec>(), c->d_kdout.as<gck_rec>(),
-                                                  c->d_kdidx.as<uint32_t>());
-    GCK_HIP(hipEventRecord(b, s));
-    uint32_t live = 0;
-    GCK_HIP(hipMemcpyAsync(&live, c->d_ktile.as<uint32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
-    GCK_HIP(hipStreamSynchronize(s));
-    GCK_HIP(hipGetLastError());
+    uint32_t *kstat = c->d_kdstat.as<uint32_t>();
+    struct Ev {
+        hipEvent_t a = nullptr, b = nullptr;
+        ~Ev() {
+            if (a) (void)hipEventDestroy(a);
+            if (b) (void)hipEventDestroy(b);
+        }
+    } ev;
+    GCK_HIP(hipEventCreate(&ev.a));
+    GCK_HIP(hipEventCreate(&ev.b));
+    GCK_HIP(hipEventRecord(ev.a, s));
+    uint32_t live = 0, hst[2] = {0, 0};
+    for (int attempt = 0;; ++attempt) {
+        if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords))) return rc;
+        if (filled) {
+            GCK_HIP(hipMemsetAsync(kstat + 1, 0, 4, s));  // (word 0: the finalize's overflow)
+        } else {
+            GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
+            GCK_HIP(hipMemsetAsync(kstat, 0, 8, s));
+        }
+        GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
+        const uint32_t grid = (uint32_t)c->n_cu * 8;
+        if (!filled)
+            k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(),
+                                             c->d_rec_kv.as<uint2>(), n, c->d_khash.as<uint64_t>(),
+                                             c->d_ktab.as<unsigned long long>(), slots - 1, c->kd_hashed ? 1 : 0,
+                                             kstat);
+        c->kd_hashed = true;
+        k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_kv.as<uint2>(),
+                                       (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>(), kstat);
+        k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
+        k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);
+        k_kd_scatter<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>(),
+                                                      c->d_out.as<gck_rec>(), c->d_kdout.as<gck_rec>(),
+                                                      c->d_kdidx.as<uint32_t>());
+        GCK_HIP(hipEventRecord(ev.b, s));
+        GCK_HIP(hipMemcpyAsync(&live, c->d_ktile.as<uint32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(hst, kstat, 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipStreamSynchronize(s));
+        GCK_HIP(hipGetLastError());
+        if (!hst[0]) break;
+        // a key found no slot within kMaxProbe probes (more keys than the
+        // table was sized for): again, sized for every record distinct
+        if (attempt == 2) return GCK_EDEVICE;
+        filled = false;
+        const uint64_t all = kd_table_slots(n);
+        slots = slots < all ? all : 2 * slots;
+    }
     float t = 0;
-    (void)hipEventElapsedTime(&t, a, b);
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
+    (void)hipEventElapsedTime(&t, ev.a, ev.b);
     if (ms) *ms = t;
+    c->kd_inserted = true;  // the table holds this run's records: a rebuild only marks and compacts
+    c->kd_tab_slots = slots;
+    c->kd_keys_hint = hst[1];
     c->n_live = live;
     c->kd_valid = true;
     c->kd_slots = slots;

@@ -1559,7 +1559,8 @@ constexpr uint32_t kFinThreads = 256;
 constexpr uint32_t kFinWaves = kFinThreads / 64;
 // HASH: also each record's key hash (kd_common.h key_hash, what k_kd_insert
 // would compute) into khash[r], from the key words the record's header + key
-// CRC already holds in registers (gck_ctx_keydir_hash)
+// CRC already holds in registers, and the record into the keydir table ktab
+// (kd_insert_rec, as k_kd_insert would: gck_ctx_keydir_hash)
 template <bool HASH>
 __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_finalize(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ rec_off,
@@ -1573,7 +1574,9 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                                                   const uint32_t *__restrict__ zrow,
                                                   const uint32_t *__restrict__ xa,
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
-                                                  uint32_t *counters, uint64_t *__restrict__ khash) {
+                                                  uint32_t *counters, uint64_t *__restrict__ khash,
+                                                  unsigned long long *__restrict__ ktab, uint64_t kmask,
+                                                  uint32_t *__restrict__ kstat) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
     // gf_mul_lds: one 4 KiB table region per wave, then R (y * x^4 = (y >> 4) ^
@@ -1851,7 +1854,36 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const KeyWords k(arena, rs + 16, klen);
                     for (uint32_t i = 0; 4 * i < klen; ++i) hh = mix64d(hh ^ k[i]) + i;
                 }
-                if (valid) khash[base + lane] = mix64d(hh);
+                if (valid) {
+                    const uint64_t h = mix64d(hh);
+                    khash[base + lane] = h;
+                    bool ok;
+                    if (kv.x != 0 && klen + lead <= 28) {
+                        // the key words as values (an indexed register array
+                        // would go to scratch)
+                        const uint32_t k0 = ab(pw[5], pw[4], lead), k1 = ab(pw[6], pw[5], lead),
+                                       k2 = ab(pw[7], pw[6], lead), k3 = ab(pw[8], pw[7], lead),
+                                       k4 = ab(pw[9], pw[8], lead), k5 = ab(pw[10], pw[9], lead),
+                                       k6 = ab(pw[11], pw[10], lead);
+                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane,
+                                      [=](uint32_t i) {
+                                          const uint32_t v = i == 0   ? k0
+                                                             : i == 1 ? k1
+                                                             : i == 2 ? k2
+                                                             : i == 3 ? k3
+                                                             : i == 4 ? k4
+                                                             : i == 5 ? k5
+                                                                      : k6;
+                                          const uint32_t left = klen - 4 * i;
+                                          return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
+                                      },
+                                      klen);
+                    } else {
+                        const KeyWords k(arena, rs + 16, klen);
+                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane, [&](uint32_t i) { return k[i]; }, klen);
+                    }
+                    if (!ok) atomicOr(kstat, 1u);  // gck_ctx_keydir builds the table again
+                }
             }
         }
     };
@@ -1865,14 +1897,20 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     // an iteration's loads (forced vmcnt(0)) and computing it
     uint64_t fin_wait = 0, fin_comp = 0;
 #endif
-    uint64_t base = rb + (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    // 64-record pieces, wavefront w taking pieces w, w + W, ...; from the last
+    // piece back when the keys are inserted here (a key's later record then
+    // mostly claims its slot first, as in k_kd_insert)
+    const uint64_t npc = re > rb ? (re - rb + 63) / 64 : 0, W = G / 64;
+    auto at = [&](uint64_t k) { return rb + 64 * (HASH ? npc - 1 - k : k); };
+    uint64_t pc = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
     Rec cur, nxt;
-    if (base < re) load_rec(base, cur);
-    for (; base < re; base += G) {
+    if (pc < npc) load_rec(at(pc), cur);
+    for (; pc < npc; pc += W) {
+        const uint64_t base = at(pc);
         const Geo g = geo(cur, base);
         Dep dc;
         issue(g, dc);
-        if (base + G < re) load_rec(base + G, nxt);
+        if (pc + W < npc) load_rec(at(pc + W), nxt);
 #ifdef GCK_CLOCK_STAMPS
         const uint64_t fa = __builtin_amdgcn_s_memtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2028,7 +2066,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
                    &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
-                   &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_live, &c->d_ktile,
+                   &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_kdstat, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
                    &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
@@ -2264,9 +2302,23 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     return GCK_OK;
 }
 
-static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
+static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
     auto kern = c->hash_keys ? k_finalize<true> : k_finalize<false>;
-    if (!max_recs) return;
+    if (!max_recs) return GCK_OK;
+    // the keydir table, filled by this finalize (gck_ctx_keydir then only
+    // marks and compacts), sized for the record table's capacity
+    unsigned long long *ktab = nullptr;
+    uint64_t kmask = 0;
+    if (c->hash_keys) {
+        const uint64_t slots = kd_table_slots(kd_keys_expected(c->kd_keys_hint, max_recs));
+        int rc;
+        if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_kdstat.ensure(8))) return rc;
+        GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
+        GCK_HIP(hipMemsetAsync(c->d_kdstat.p, 0, 8, s));
+        c->kd_tab_slots = slots;
+        ktab = c->d_ktab.as<unsigned long long>();
+        kmask = slots - 1;
+    }
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
     const uint64_t want = nblk(max_recs, kFinThreads), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
@@ -2278,7 +2330,9 @@ static void launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t
                                     c->d_zrow.as<uint32_t>(),
                                     c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>(),
-                                    c->hash_keys ? c->d_khash.as<uint64_t>() : nullptr);
+                                    c->hash_keys ? c->d_khash.as<uint64_t>() : nullptr, ktab, kmask,
+                                    c->d_kdstat.as<uint32_t>());
+    return GCK_OK;
 }
 
 static int ensure_records(Ctx *c, uint64_t nr) {
@@ -2403,7 +2457,7 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
     if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, kQueueCrc))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
-    launch_finalize(c, s, gbase, n_total);
+    if ((rc = launch_finalize(c, s, gbase, n_total))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_END], s));
     GCK_HIP(hipMemcpyAsync(hcnt, cnt, 16, hipMemcpyDeviceToHost, s));
     GCK_HIP(hipStreamSynchronize(s));
@@ -2422,6 +2476,7 @@ static int ctx_run_host(Ctx *c) {
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
     c->kd_hashed = c->hash_keys;
+    c->kd_inserted = c->hash_keys;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
 }
@@ -2469,7 +2524,7 @@ static int ctx_run_device(Ctx *c) {
     int rc;
     if ((rc = launch_crc(c, m, 0, c->n_rows, cap, kQueueCrc, true))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
-    launch_finalize(c, m, rng, cap);
+    if ((rc = launch_finalize(c, m, rng, cap))) return rc;
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_END], m));
     k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
     GCK_HIP(hipStreamSynchronize(m));
@@ -2504,6 +2559,7 @@ static int ctx_run_device(Ctx *c) {
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
     c->kd_hashed = c->hash_keys;
+    c->kd_inserted = c->hash_keys;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
@@ -2522,6 +2578,7 @@ static int ctx_run(Ctx *c) {
     c->kd_nparts = 0;
     c->kd_valid = false;
     c->kd_hashed = false;
+    c->kd_inserted = false;
     c->from_hints = false;
     if (c->rec_cap > 0 && c->nfiles > 0) {
         const int rc = ctx_run_device(c);

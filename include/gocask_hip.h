@@ -215,9 +215,11 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 #define GCK_KD_KEEP_TOMBSTONES 1u
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
 /* on: the next runs also hash every record's key in their finalize pass (the
- * key bytes are in registers there), so gck_ctx_keydir reads no key bytes to
- * hash them; off (the default) for runs that build no keydir.  gck_replay*
- * with GCK_OPT_LIVE and gck_replay_multi* turn it on for their groups. */
+ * key bytes are in registers there) and insert the record into the keydir
+ * table, so gck_ctx_keydir only marks the winners and compacts them; off (the
+ * default) for runs that build no keydir.  gck_replay* with GCK_OPT_LIVE and
+ * gck_replay_multi* turn it on for their groups.  A second gck_ctx_keydir of
+ * the same run (either way) reuses the table. */
 int gck_ctx_keydir_hash(gck_ctx *ctx, int on);
 int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
 

@@ -71,3 +71,38 @@ def test_keydir_hash_random(g, orc, seed, kw, keep):
     wf = [files[i] for i in walk]
     reset = [i + 1 < len(wf) for i in range(len(wf))]
     _check(g, orc, wf, reset, keep)
+
+
+@pytest.mark.parametrize("hash_first", [False, True])
+def test_keydir_table_overflow(g, orc, hash_first):
+    """Mostly distinct keys: a fresh context sizes its table for half the
+    records, so keys run out of slots (kMaxProbe) and the table is built again
+    for every record distinct -- in k_kd_insert, or after the finalize that
+    inserted (hash_first); the next runs are sized by the key count.  Every
+    keydir equals the oracle's; Get finds every live key and no absent one."""
+    files, names = orc.gen_corpus(seed=111, val_fixed=8, key_min=8, key_max=20, key_universe=1 << 40,
+                                  tomb_permille=20, max_file_size=1 << 18, n_files=3)
+    walk = sorted(range(len(files)), key=lambda i: names[i])
+    wf = [files[i] for i in walk]
+    reset = [i + 1 < len(wf) for i in range(len(wf))]
+    want, _ = orc.replay(wf, reset)
+    kd = orc.keydir(wf, want, reset)
+    # more keys than the slots of a table sized for half the records (a power
+    # of two >= 1.25 n / 2): some must overflow
+    slots = 1024
+    while slots < len(want) // 2 + len(want) // 8:
+        slots *= 2
+    assert len(kd) > slots
+    with g.ReplayContext() as ctx:
+        ctx.load(wf, reset)
+        ctx.keydir_hash(hash_first)
+        for _ in range(2):  # the first: overflow and rebuild; the second: sized by the count
+            ctx.run()
+            live, _ = ctx.keydir()
+            assert len(live) == len(kd)
+            got = {bytes(wf[int(r["file"])][int(r["rec_off"]) + 16:int(r["rec_off"]) + 16 + int(r["key_len"])]):
+                   int(r["rec_off"]) for r in live}
+            assert got == {k: int(r["rec_off"]) for k, r in kd.items()}
+        keys = list(kd)[:500] + [b"absent-key-%d" % i for i in range(100)]
+        st, vs, _, _ = ctx.get_batch(keys, values=False)
+        assert (st[:500] == 0).all() and (st[500:] == g._lib.GCK_EKEY_NOT_FOUND).all()
