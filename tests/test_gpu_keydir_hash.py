@@ -106,3 +106,42 @@ def test_keydir_table_overflow(g, orc, hash_first):
         keys = list(kd)[:500] + [b"absent-key-%d" % i for i in range(100)]
         st, vs, _, _ = ctx.get_batch(keys, values=False)
         assert (st[:500] == 0).all() and (st[500:] == g._lib.GCK_EKEY_NOT_FOUND).all()
+
+
+@pytest.mark.parametrize("hash_first", [False, True])
+def test_keydir_inline_all_ones(g, orc, hash_first):
+    """Keys whose 8-byte words are all 0xFF look like a slot word that has not
+    landed: those probes compare from the arena.  Keys differing only past
+    their first 24 bytes, only in length, or only in a 0xFF word must stay
+    distinct; updates and deletes of each keep last-writer-wins (the oracle's
+    keydir); Get finds each live key's last value."""
+    ff = b"\xff" * 8
+    keys = [ff, ff * 2, ff * 3, ff * 3 + b"a", ff * 3 + b"b", ff + b"x" + ff, ff + b"y" + ff, b"k" + ff * 2,
+            b"\xff" * 7, b"\xff" * 9, b"p" * 24 + b"tail-1", b"p" * 24 + b"tail-2", b"p" * 24, b"p" * 23]
+    recs, ts = [], 1700000000
+    for rnd in range(3):
+        for i, k in enumerate(keys):
+            ts += 1
+            if (i + rnd) % 5 == 4:
+                recs.append(orc.tombstone(ts, k))
+            else:
+                recs.append(orc.entry(ts, k, b"v%d-%d" % (rnd, i)))
+    files = [np.frombuffer(b"".join(recs), np.uint8)]
+    want, _ = orc.replay(files, [False])
+    kd = orc.keydir(files, want, [False])
+    with g.ReplayContext() as ctx:
+        ctx.load(files, [False])
+        ctx.keydir_hash(hash_first)
+        ctx.run()
+        live, _ = ctx.keydir()
+        got = {bytes(files[0][int(r["rec_off"]) + 16:int(r["rec_off"]) + 16 + int(r["key_len"])]): int(r["rec_off"])
+               for r in live}
+        assert got == {k: int(r["rec_off"]) for k, r in kd.items()}
+        st, vs, _, vals = ctx.get_batch(keys)
+        for k, s, v in zip(keys, st, vals):
+            if k in kd:
+                assert s == 0
+                o = int(kd[k]["value_pos"])
+                assert v == bytes(files[0][o:o + int(kd[k]["value_size"])])
+            else:
+                assert s == g._lib.GCK_EKEY_NOT_FOUND
