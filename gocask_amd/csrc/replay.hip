@@ -176,6 +176,9 @@ __device__ void walk_chain(const uint8_t *__restrict__ arena, uint64_t base, uin
 }
 
 // ------------------------------------------------------------------ kernels ---
+#ifndef GCK_SPEC_DOT
+#define GCK_SPEC_DOT 1
+#endif
 // Bit 7 of each byte of the result is set iff that byte of w is zero (exact).
 __device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {
     return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
@@ -261,6 +264,30 @@ __device__ void spec_chunk(const uint8_t *__restrict__ arena, const uint64_t *__
             w[17] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].y, (int)w[1], 0x130, 0xF, 0xF, false);
             w[18] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].z, (int)w[2], 0x130, 0xF, 0xF, false);
             w[19] = (uint32_t)__builtin_amdgcn_update_dpp((int)v[4].w, (int)w[3], 0x130, 0xF, 0xF, false);
+#if GCK_SPEC_DOT
+            // nz(k): bit 7 of byte j set iff bytes 4k+j, 4k+j+1 are not both
+            // zero (x = the word OR'ed with itself one byte on; a zero byte of
+            // x = a zero pair).  Two words' flags become one byte with two
+            // v_dot4_u32_u8 (flag 0x80 times 1, 2, 4, ..., 128, summed): byte j of
+            // the 72-bit m = words 2 + 2j, 3 + 2j; position t = bit u of m - 2.
+            // The candidates are the complement.  About 7 VALU per word where
+            // the per-bit nibble gather took 15 (k_spec_entry is VALU-bound
+            // about half its cycles, profiles/r5end2 PMC)
+            auto nz = [&](int k) {
+                const uint32_t x = w[k] | __builtin_amdgcn_alignbyte(w[k + 1], w[k], 1);
+                return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+            };
+            uint32_t mb[9];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                mb[j] = __builtin_amdgcn_udot4(nz(2 + 2 * j), 0x08040201u,
+                                               __builtin_amdgcn_udot4(nz(3 + 2 * j), 0x80402010u, 0u, false), false) >> 7;
+            mb[8] = __builtin_amdgcn_udot4(nz(18), 0x08040201u, 0u, false) >> 7;
+            const uint32_t lo = mb[0] | (mb[1] << 8) | (mb[2] << 16) | (mb[3] << 24);
+            const uint32_t hi = mb[4] | (mb[5] << 8) | (mb[6] << 16) | (mb[7] << 24);
+            const uint32_t r0 = __builtin_amdgcn_alignbit(hi, lo, 2), r1 = __builtin_amdgcn_alignbit(mb[8], hi, 2);
+            return ~(((uint64_t)r1 << 32) | r0);
+#else
             uint32_t zf[20];
 #pragma unroll
             for (int k = 2; k < 20; ++k) zf[k] = zero_bytes(w[k]);
@@ -273,6 +300,7 @@ __device__ void spec_chunk(const uint8_t *__restrict__ arena, const uint64_t *__
                 cm |= t0 >= 0 ? (uint64_t)nib << t0 : (uint64_t)(nib >> -t0);
             }
             return cm;
+#endif
         };
         // positions searched: [cs, lim).  The next window is loaded one ahead,
         // unconditionally (the arena is padded past every file; a branch
