@@ -119,6 +119,7 @@ struct Ctx {
     uint64_t n_live = 0;
     bool kd_hashed = false;  // d_khash holds the key hashes of the last run's records
     bool kd_inserted = false;  // d_ktab holds the last run's records (its finalize inserted them)
+    bool kd_fin_table = false;  // the last finalize launch builds the keydir table
     uint64_t kd_tab_slots = 0;  // d_ktab's slots then
     uint64_t kd_keys_hint = 0;  // distinct keys of the last keydir built here (sizes the next table)
     bool hash_keys = false;  // runs hash every record's key in finalize (gck_ctx_keydir_hash)

@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
             const uint32_t len = (uint32_t)len64;
             const KeyWords k(keys, koff[q], len);
             const uint64_t h = key_hash(k, len), mask = slots - 1;
-            const unsigned long long want = slot_word0(h, len, 0) >> 32;  // tag | length
+            const unsigned long long want = slot_word0(h, len, 0, false) >> 32;  // tag | length
             uint64_t s = h & mask;
             for (uint32_t probe = 0; probe < kMaxProbe; ++probe, s = (s + 1) & mask) {  // (kd_insert_rec's bound)
                 const unsigned long long *slot = table + kSlotWords * s;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
                 if ((a.x >> 32) != want) continue;
                 const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(slot + 2);
                 const unsigned long long w[3] = {a.y, b.x, b.y};
-                const uint32_t cur = (uint32_t)a.x;
+                const uint32_t cur = slot_rec(a.x);
                 if (!slot_key_equal(arena, rec_off, rec_kv, w, cur, [&](uint32_t i) { return k[i]; }, len)) continue;
                 const gck_rec r = recs[cur];
                 if (!(r.flags & GCK_F_TOMBSTONE)) {

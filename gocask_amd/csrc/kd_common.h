@@ -69,8 +69,10 @@ __device__ __forceinline__ uint64_t key_hash(const KeyWords &k, uint32_t len) {
 
 // Table slot, 32 bytes: word 0 = the key's hash tag (bits 48..63 of its
 // hash) | its length (16 bits, 0xFFFF: 65,535 or longer) | the index of its
-// record; all ones = empty.  Same key => same tag and length, so a 64-bit max
-// on word 0 keeps the larger record index.  Words 1..3 = the key's first 24
+// record (31 bits) | 1 if that record is a tombstone; all ones = empty.  Same
+// key => same tag and length, so a 64-bit max on word 0 keeps the larger
+// record index (the tombstone bit never decides: indices differ), and the
+// marking reads the winner's kind from the slot, not from the record table.  Words 1..3 = the key's first 24
 // bytes (zero past its end), written by the lane that claimed the slot right
 // after its CAS: a probe compares keys of up to 24 bytes without reading the
 // arena.  A word still all ones (not landed yet, or a key whose 8 bytes are
@@ -80,9 +82,12 @@ __device__ __forceinline__ uint64_t key_hash(const KeyWords &k, uint32_t len) {
 // length) saved the record-table reads but not the arena's.
 constexpr unsigned long long kEmptySlot = ~0ull;
 constexpr uint32_t kSlotWords = 4, kInlineKey = 24;
-__device__ __forceinline__ unsigned long long slot_word0(uint64_t h, uint32_t len, uint64_t r) {
-    return ((h >> 48) << 48) | ((unsigned long long)(len < 0xFFFFu ? len : 0xFFFFu) << 32) | (uint32_t)r;
+constexpr uint64_t kKdMaxRecs = 1ull << 31;  // record indices in 31 bits
+__device__ __forceinline__ unsigned long long slot_word0(uint64_t h, uint32_t len, uint64_t r, bool tomb) {
+    return ((h >> 48) << 48) | ((unsigned long long)(len < 0xFFFFu ? len : 0xFFFFu) << 32) |
+           ((uint32_t)r << 1) | (tomb ? 1u : 0u);
 }
+__device__ __forceinline__ uint32_t slot_rec(unsigned long long w0) { return (uint32_t)w0 >> 1; }
 
 // Table slots for an expected number of distinct keys: a power of two, load
 // <= 0.8.  A table sized for the keys expected, not for every record (C3: 4.4
@@ -147,9 +152,10 @@ __device__ __forceinline__ bool slot_key_equal(const uint8_t *__restrict__ arena
 // (k_kd_insert, and k_finalize when the run builds the table: gck_ctx_keydir_hash)
 template <class Words>
 __device__ __forceinline__ bool kd_insert_rec(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off,
-                                              const uint2 *__restrict__ rec_kv, unsigned long long *__restrict__ table, uint64_t mask, uint64_t h,
-                                              uint64_t r, const Words &k, uint32_t len) {
-    const unsigned long long mine = slot_word0(h, len, r);
+                                              const uint2 *__restrict__ rec_kv, unsigned long long *__restrict__ table,
+                                              uint64_t mask, uint64_t h, uint64_t r, bool tomb, const Words &k,
+                                              uint32_t len) {
+    const unsigned long long mine = slot_word0(h, len, r, tomb);
     uint64_t s = h & mask;
     for (uint32_t probe = 0; probe < kMaxProbe; ++probe, s = (s + 1) & mask) {
         unsigned long long *slot = table + kSlotWords * s;
@@ -176,7 +182,7 @@ __device__ __forceinline__ bool kd_insert_rec(const uint8_t *__restrict__ arena,
             w[2] = b2.y;
         }
         if ((cur >> 32) != (mine >> 32)) continue;  // tag or length differ
-        const uint32_t ci = (uint32_t)cur;
+        const uint32_t ci = slot_rec(cur);
         if (slot_key_equal(arena, rec_off, rec_kv, w, ci, k, len)) {
             if (ci < r) atomicMax(slot, mine);  // same key: the later record wins
             return true;

@@ -25,11 +25,12 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
                                                    int hashed, uint32_t *__restrict__ kstat) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = n - 1 - i;
-        const uint32_t len = key_len(rec_kv[r]);
+        const uint2 kv = rec_kv[r];
+        const uint32_t len = key_len(kv);
         const KeyRegs k(arena, rec_off[r] + 16, len);
         const uint64_t h = hashed ? khash[r] : key_hash(k.m, len);
         if (!hashed) khash[r] = h;
-        if (!kd_insert_rec(arena, rec_off, rec_kv, table, mask, h, r, k, len))
+        if (!kd_insert_rec(arena, rec_off, rec_kv, table, mask, h, r, kv.x == 0, k, len))
             atomicOr(kstat, 1u);
     }
 }
@@ -39,15 +40,14 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
 // markers).  The keys (claimed slots) are counted into
 // kstat[1]: the next table of this context is sized by them.
 __global__ __launch_bounds__(256) void k_kd_mark(const unsigned long long *__restrict__ table, uint64_t slots,
-                                                 const uint2 *__restrict__ rec_kv, uint32_t keep_tombstones,
-                                                 uint32_t *__restrict__ live, uint32_t *__restrict__ kstat) {
+                                                 uint32_t keep_tombstones, uint32_t *__restrict__ live,
+                                                 uint32_t *__restrict__ kstat) {
     uint32_t keys = 0;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
         const unsigned long long v = table[kSlotWords * s];
         if (v == kEmptySlot) continue;
         ++keys;
-        const uint32_t r = (uint32_t)v;
-        if (keep_tombstones || rec_kv[r].x != 0) live[r] = 1;
+        if (keep_tombstones || !(v & 1)) live[slot_rec(v)] = 1;
     }
     for (int o = 32; o > 0; o >>= 1) keys += __shfl_down(keys, o);
     if ((threadIdx.x & 63) == 0 && keys) atomicAdd(kstat + 1, keys);
@@ -326,7 +326,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
         c->kd_slots = 0;
         return GCK_OK;
     }
-    if (n >= kEmpty) return GCK_EINVAL;
+    if (n >= kKdMaxRecs) return GCK_EINVAL;
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     // the run's finalize may have filled the table already (gck_ctx_keydir_hash):
@@ -368,7 +368,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
                                              c->d_ktab.as<unsigned long long>(), slots - 1, c->kd_hashed ? 1 : 0,
                                              kstat);
         c->kd_hashed = true;
-        k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots, c->d_rec_kv.as<uint2>(),
+        k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots,
                                        (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>(), kstat);
         k_kd_tiles<<<(uint32_t)nt, kKdTile, 0, s>>>(c->d_live.as<uint32_t>(), n, c->d_ktile.as<uint32_t>());
         k_kd_tile_scan<<<1, kKdTile, 0, s>>>(c->d_ktile.as<uint32_t>(), (uint32_t)nt);

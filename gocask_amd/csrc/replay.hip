@@ -1882,7 +1882,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                     const KeyWords k(arena, rs + 16, klen);
                     for (uint32_t i = 0; 4 * i < klen; ++i) hh = mix64d(hh ^ k[i]) + i;
                 }
-                if (valid) {
+                if (valid && ktab) {  // (no table: a run too large for one; gck_ctx_keydir refuses it)
                     const uint64_t h = mix64d(hh);
                     khash[base + lane] = h;
                     bool ok;
@@ -1893,7 +1893,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                                        k2 = ab(pw[7], pw[6], lead), k3 = ab(pw[8], pw[7], lead),
                                        k4 = ab(pw[9], pw[8], lead), k5 = ab(pw[10], pw[9], lead),
                                        k6 = ab(pw[11], pw[10], lead);
-                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane,
+                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane, kv.x == 0,
                                       [=](uint32_t i) {
                                           const uint32_t v = i == 0   ? k0
                                                              : i == 1 ? k1
@@ -1908,7 +1908,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                                       klen);
                     } else {
                         const KeyWords k(arena, rs + 16, klen);
-                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane, [&](uint32_t i) { return k[i]; }, klen);
+                        ok = kd_insert_rec(arena, rec_off, rec_kv, ktab, kmask, h, base + lane, kv.x == 0, [&](uint32_t i) { return k[i]; }, klen);
                     }
                     if (!ok) atomicOr(kstat, 1u);  // gck_ctx_keydir builds the table again
                 }
@@ -2337,7 +2337,8 @@ static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t 
     // marks and compacts), sized for the record table's capacity
     unsigned long long *ktab = nullptr;
     uint64_t kmask = 0;
-    if (c->hash_keys) {
+    c->kd_fin_table = c->hash_keys && max_recs < kKdMaxRecs;
+    if (c->kd_fin_table) {
         const uint64_t slots = kd_table_slots(kd_keys_expected(c->kd_keys_hint, max_recs));
         int rc;
         if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_kdstat.ensure(8))) return rc;
@@ -2503,8 +2504,8 @@ static int ctx_run_host(Ctx *c) {
     c->ms_phase[PH_PIPE] = span;
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
-    c->kd_hashed = c->hash_keys;
-    c->kd_inserted = c->hash_keys;
+    c->kd_hashed = c->kd_fin_table;  // (finalize hashed the keys)
+    c->kd_inserted = c->kd_fin_table;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return c->status;
 }
@@ -2586,8 +2587,8 @@ static int ctx_run_device(Ctx *c) {
     c->ms_phase[PH_CRC] = el(PH_CRC, PH_FINAL);
     c->ms_crc_sum += c->ms_phase[PH_CRC];
     ++c->n_runs;
-    c->kd_hashed = c->hash_keys;
-    c->kd_inserted = c->hash_keys;
+    c->kd_hashed = c->kd_fin_table;  // (finalize hashed the keys)
+    c->kd_inserted = c->kd_fin_table;
     c->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->device_path = true;
     return c->status;
