@@ -2332,6 +2332,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
 
 static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
     auto kern = c->hash_keys ? k_finalize<true> : k_finalize<false>;
+    c->kd_fin_table = false;
     if (!max_recs) return GCK_OK;
     // the keydir table, filled by this finalize (gck_ctx_keydir then only
     // marks and compacts), sized for the record table's capacity
