@@ -27,7 +27,9 @@ for s in $steps; do
   kt)
     bash tools/ktrace.sh $tag || exit $? ;;
   clock)
-    timeout -k 10 150 python tools/clock.py > $out/clock.log 2>&1 || { cat $out/clock.log; exit 1; }
+    # the stamps build (tools/clock.py's header: make ... EXTRA=-DGCK_CLOCK_STAMPS)
+    GCK_LIB_PATH=gocask_amd/var/libgocask_hip_clk.so timeout -k 10 150 python tools/clock.py > $out/clock.log 2>&1 \
+      || { cat $out/clock.log; exit 1; }
     cat $out/clock.log ;;
   secondary)
     for rep in 1 2 3; do timeout -k 10 120 python tools/bench_encode.py 2>/dev/null | tail -1 >> $out/bench_encode.log || exit 1; done
