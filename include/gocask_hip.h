@@ -211,7 +211,10 @@ int gck_ctx_fetch_into(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * tombstones are kept too, as delete markers for a merge across shards).
  * *n_live = the entries; *ms (optional) = device time.  The entries, in walk
  * order of their records, are fetched with gck_ctx_fetch_keydir; a Go caller
- * sets db.kd.entries[key] for each (key bytes at rec_off + 16 in the file). */
+ * sets db.kd.entries[key] for each (key bytes at rec_off + 16 in the file).
+ * GCK_EINVAL for a run of 2^31 records or more (the table's record index is
+ * 31 bits); GCK_EDEVICE if keys keep finding no free slot within 256 probes
+ * after the table was rebuilt for every record distinct (a hash flood). */
 #define GCK_KD_KEEP_TOMBSTONES 1u
 int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms);
 /* on: the next runs also hash every record's key in their finalize pass (the
