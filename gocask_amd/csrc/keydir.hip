@@ -133,20 +133,26 @@ struct LocalSrc {  // the keydir of the last run (gck_ctx_keydir)
     __device__ bool sel(uint64_t) const { return true; }
     __device__ uint64_t hash(uint64_t i) const { return khash[idx[i]]; }
     __device__ uint32_t klen(uint64_t i) const { return recs[i].key_len; }
+    // (the 64-byte entry as four 16-byte stores and the key as 8-byte ones:
+    // field by field, a lane's stores each wrote a piece of its line)
     __device__ void put(uint64_t i, gck_kd_entry *e, uint64_t key_rel, uint32_t *kdst) const {
         const uint32_t r = idx[i];
-        gck_rec rec = recs[i];
-        const uint32_t len = rec.key_len;
+        const uint2 *rp = reinterpret_cast<const uint2 *>(recs + i);  // gck_rec: 5 x 8 bytes
+        const uint2 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3], r4 = rp[4];
+        const uint32_t len = r1.y;  // key_len
         const KeyWords k(arena, rec_off[r] + 16, len);
-        for (uint32_t w = 0; 4ull * w < pad8(len); ++w) kdst[w] = 4 * w < len ? k[w] : 0u;
-        rec.file += file_base;
-        e->hash = khash[r];
-        e->key_off = key_rel;
-        e->key_len = len;
-        e->shard = shard;
-        e->rec = rec;
+        uint2 *kd = reinterpret_cast<uint2 *>(kdst);
+        for (uint32_t w = 0; 8ull * w < pad8(len); ++w)
+            kd[w] = make_uint2(8 * w < len ? k[2 * w] : 0u, 8 * w + 4 < len ? k[2 * w + 1] : 0u);
+        const uint64_t h = khash[r];
+        uint4 *ep = reinterpret_cast<uint4 *>(e);
+        ep[0] = make_uint4((uint32_t)h, (uint32_t)(h >> 32), (uint32_t)key_rel, (uint32_t)(key_rel >> 32));
+        ep[1] = make_uint4(len, shard, r0.x, r0.y);          // key_len, shard, rec.rec_off
+        ep[2] = make_uint4(r1.x + file_base, r1.y, r2.x, r2.y);  // rec.file, key_len, value_pos, value_size
+        ep[3] = make_uint4(r3.x, r3.y, r4.x, r4.y);          // rec.crc, ts, flags, crc_calc
     }
 };
+static_assert(offsetof(gck_kd_entry, rec) == 24 && sizeof(gck_rec) == 40, "gck_kd_entry layout");
 
 struct MergedSrc {  // received entries that won the merge
     const gck_kd_entry *E;
@@ -157,11 +163,16 @@ struct MergedSrc {  // received entries that won the merge
     __device__ uint64_t hash(uint64_t i) const { return E[i].hash; }
     __device__ uint32_t klen(uint64_t i) const { return E[i].key_len; }
     __device__ void put(uint64_t i, gck_kd_entry *e, uint64_t key_rel, uint32_t *kdst) const {
-        gck_kd_entry x = E[i];
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(K + koff[i]);
-        for (uint32_t w = 0; 4ull * w < pad8(x.key_len); ++w) kdst[w] = src[w];
-        x.key_off = key_rel;
-        *e = x;
+        const uint4 *sp = reinterpret_cast<const uint4 *>(E + i);
+        const uint4 a = sp[0], b = sp[1], c = sp[2], d = sp[3];
+        const uint2 *src = reinterpret_cast<const uint2 *>(K + koff[i]);
+        uint2 *kd = reinterpret_cast<uint2 *>(kdst);
+        for (uint32_t w = 0; 8ull * w < pad8(b.x); ++w) kd[w] = src[w];  // b.x: key_len
+        uint4 *ep = reinterpret_cast<uint4 *>(e);
+        ep[0] = make_uint4(a.x, a.y, (uint32_t)key_rel, (uint32_t)(key_rel >> 32));
+        ep[1] = b;
+        ep[2] = c;
+        ep[3] = d;
     }
 };
 
