@@ -293,15 +293,19 @@ __global__ __launch_bounds__(256) void k_mg_insert(const gck_kd_entry *__restric
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t h = E[r].hash;
         const uint32_t len = E[r].key_len;
+        // slot = entry index << 1 | 1 for a delete: the max still orders by
+        // index, and k_mg_mark reads the winner's kind from the slot
+        const uint32_t mine = ((uint32_t)r << 1) | ((E[r].rec.flags & GCK_F_TOMBSTONE) ? 1u : 0u);
         for (uint64_t s = h & mask;; s = (s + 1) & mask) {
             uint32_t cur = __hip_atomic_load(table + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (cur == kEmpty) {
-                const uint32_t prev = atomicCAS(table + s, kEmpty, (uint32_t)r);
+                const uint32_t prev = atomicCAS(table + s, kEmpty, mine);
                 if (prev == kEmpty) break;
                 cur = prev;
             }
-            if (E[cur].hash == h && E[cur].key_len == len && blob_same(K, koff[cur], koff[r], len)) {
-                atomicMax(table + s, (uint32_t)r);
+            const uint32_t ci = cur >> 1;
+            if (E[ci].hash == h && E[ci].key_len == len && blob_same(K, koff[ci], koff[r], len)) {
+                atomicMax(table + s, mine);
                 break;
             }
         }
@@ -310,10 +314,10 @@ __global__ __launch_bounds__(256) void k_mg_insert(const gck_kd_entry *__restric
 
 // k_mg_mark: a key's winning entry stays unless it is a delete.
 __global__ __launch_bounds__(256) void k_mg_mark(const uint32_t *__restrict__ table, uint64_t slots,
-                                                 const gck_kd_entry *__restrict__ E, uint32_t *__restrict__ live) {
+                                                 uint32_t *__restrict__ live) {
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t r = table[s];
-        if (r != kEmpty && !(E[r].rec.flags & GCK_F_TOMBSTONE)) live[r] = 1;
+        const uint32_t v = table[s];
+        if (v != kEmpty && !(v & 1u)) live[v >> 1] = 1;
     }
 }
 
@@ -501,7 +505,7 @@ int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_k
     const uint64_t n = pre[nsrc];
     if (ms) *ms = 0;
     if (!n) return GCK_OK;
-    if (n >= kEmpty || !d_entries || !d_keys) return GCK_EINVAL;
+    if (n >= 0x7FFFFFFFull || !d_entries || !d_keys) return GCK_EINVAL;  // (slots: index << 1 | delete)
     uint64_t slots = 1024;
     while (slots < 2 * n) slots <<= 1;
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
@@ -524,7 +528,7 @@ int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_k
     k_mg_koff<<<grid, 256, 0, s>>>(d_entries, n, c->d_msrc.as<uint64_t>(), nsrc, c->d_mkoff.as<uint64_t>());
     k_mg_insert<<<grid, 256, 0, s>>>(d_entries, d_keys, c->d_mkoff.as<uint64_t>(), n, c->d_mtab.as<uint32_t>(),
                                      slots - 1);
-    k_mg_mark<<<grid, 256, 0, s>>>(c->d_mtab.as<uint32_t>(), slots, d_entries, c->d_mlive.as<uint32_t>());
+    k_mg_mark<<<grid, 256, 0, s>>>(c->d_mtab.as<uint32_t>(), slots, c->d_mlive.as<uint32_t>());
     const MergedSrc src{d_entries, d_keys, c->d_mkoff.as<uint64_t>(), c->d_mlive.as<uint32_t>()};
     k_pk_tiles<MergedSrc><<<(uint32_t)nt, kKdTile, 0, s>>>(src, n, 1u, c->d_kpart.as<uint32_t>(),
                                                            c->d_kcrank.as<uint32_t>(), c->d_kbrank.as<uint64_t>(),
