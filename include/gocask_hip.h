@@ -332,7 +332,8 @@ int gck_kd_pack_sizes(gck_ctx *ctx, uint32_t nparts, uint64_t *counts, uint64_t 
 int gck_kd_pack(gck_ctx *ctx, uint32_t shard, uint32_t file_base, gck_kd_entry *d_entries, uint64_t entries_cap,
                 uint8_t *d_keys, uint64_t keys_cap);
 /* Merge the partitions an owner received: DEVICE arrays of nsrc sources in
- * shard order, src_counts[s] entries / src_key_bytes[s] blob bytes each. */
+ * shard order, src_counts[s] entries / src_key_bytes[s] blob bytes each
+ * (fewer than 2^31 - 1 entries in all, else GCK_EINVAL). */
 int gck_kd_merge(gck_ctx *ctx, const gck_kd_entry *d_entries, const uint8_t *d_keys, const uint64_t *src_counts,
                  const uint64_t *src_key_bytes, uint32_t nsrc, uint64_t *n_live, double *ms);
 /* Host copies of the merged entries (key_off into the merged blob) and keys;
