@@ -2245,13 +2245,26 @@ static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, const 
 
 // Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
 // kRounds validate/fixup rounds and a final validation counted at val_cnt[kRounds].
-static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt) {
+// after_spec: launched between the speculation and the walk (the device
+// path's k_run_init: the step's first kernel is then the 0.2 ms speculation,
+// so the GPU is not idle while the host launches the second; 19 us per C3
+// step in the kernel trace of profiles/r5end3 with k_run_init first)
+struct NoLaunch {
+    void operator()() const {}
+};
+template <class AfterSpec = NoLaunch>
+static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt,
+                            AfterSpec after_spec = AfterSpec()) {
     const uint32_t n = c1 - c0, cap = c->opts.chunk_cap;
-    if (!n) return;
+    if (!n) {
+        after_spec();
+        return;
+    }
     k_spec_entry<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_start.as<uint64_t>() + c0,
                                             c->d_ch_end.as<uint64_t>() + c0, c->d_ch_entry.as<uint64_t>() + c0, n,
                                             c->opts.max_key, c->opts.spec_window);
+    after_spec();
     k_walk<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                         c->d_ch_file.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
                                         c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
@@ -2544,8 +2557,11 @@ static int ctx_run_device(Ctx *c) {
     // (without phase timing only the CRC pass is bracketed: an event between
     // two kernels costs ~5-6 us of the run, kernel trace profiles/r5a)
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
-    k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
-    launch_boundary(c, m, 0, nc, cnt + CNT_VAL);
+    // (k_run_init's counters, record base, queue and row 0 are first used
+    // by the walk's validation: it runs after the speculation)
+    launch_boundary(c, m, 0, nc, cnt + CNT_VAL, [&] {
+        k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
+    });
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
     launch_scan(c, m, gb, cap, true, res, grng, rng);
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], m));
