@@ -122,7 +122,7 @@ class GckStats(ctypes.Structure):
         ("files_walked", ctypes.c_uint32),
         ("final_last_offset", ctypes.c_uint32),
         ("n_files", ctypes.c_uint32),
-        ("reserved", ctypes.c_uint32),
+        ("kd_longest_probe", ctypes.c_uint32),
         ("n_runs", ctypes.c_uint64),
         ("ms_crc_rows_sum", ctypes.c_double),
     ]

@@ -685,7 +685,8 @@ class ReplayContext:
                     n_fixups=s.n_fixups, n_overflow=s.n_overflow, ms_total=s.ms_total, ms_phase=phases,
                     device_path=bool(s.device_path), n_reruns=s.n_reruns, status=s.status, err_file=s.err_file,
                     err_off=s.err_off, files_walked=s.files_walked, final_last_offset=s.final_last_offset,
-                    n_files=s.n_files, n_runs=s.n_runs, ms_crc_rows_sum=s.ms_crc_rows_sum)
+                    n_files=s.n_files, n_runs=s.n_runs, ms_crc_rows_sum=s.ms_crc_rows_sum,
+                    kd_longest_probe=s.kd_longest_probe)
 
     def phase_timing(self, on=True):
         """Events between every phase of the next runs (stats()['ms_phase'] per

@@ -49,7 +49,7 @@ enum Phase {
     PH_BOUNDARY = 0,  // k_spec_entry, k_walk, k_validate / k_fixup rounds
     PH_SCAN,          // record slots per chunk, per-file summary
     PH_HOST,          // D2H summary + host bookkeeping (device path: k_account_grp)
-    PH_RECORDS,       // k_row_fill, k_compact, k_row_tail
+    PH_RECORDS,       // k_compact (record table + row index)
     PH_CRC,           // k_crc_rows: the HBM-bound kernel
     PH_FINAL,         // k_finalize: CRC verdict + tuples
     PH_END,           // (event) end of the run
@@ -79,7 +79,8 @@ struct Ctx {
     size_t up_cap = 0;
     gck_opts opts{};
     int n_cu = 256;
-    int fin_blocks_per_cu = 4;  // resident k_finalize workgroups per CU
+    int fin_blocks_per_cu = 4;       // resident k_finalize<false> workgroups per CU
+    int fin_blocks_per_cu_hash = 4;  // the same for k_finalize<true> (hashing: more registers)
 
     // arena: files in walk order, each at a kRow-aligned offset
     DBuf arena;
@@ -140,6 +141,7 @@ struct Ctx {
     uint64_t n_merged = 0, merged_key_bytes = 0;
     bool kd_valid = false;   // d_ktab / d_khash / d_kdout describe the last run
     uint64_t kd_slots = 0;   // table slots (power of two; 0: no records)
+    uint64_t kd_probe_bound = 256;  // lookups probe at most this far (kMaxProbe, or the unbounded build's longest)
     // batched Get / scrub (get.hip): query keys, per-item state, values
     DBuf d_gkeys, d_gkoff, d_gstat, d_gitem, d_gvsize, d_gexp, d_gcrc, d_gvoff, d_gvals, d_gscan;
     // the key blob of gck_replay with GCK_OPT_KEYS: look-back words, offsets, bytes

@@ -19,6 +19,7 @@ namespace gck {
 __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ keys,
                                                     const uint64_t *__restrict__ koff, uint32_t n,
                                                     const unsigned long long *__restrict__ table, uint64_t slots,
+                                                    uint64_t bound,
                                                     const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ rec_off,
                                                     const uint2 *__restrict__ rec_kv,
@@ -41,7 +42,7 @@ __global__ __launch_bounds__(256) void k_get_lookup(const uint8_t *__restrict__ 
             const uint64_t h = key_hash(k, len), mask = slots - 1;
             const unsigned long long want = slot_word0(h, len, 0, false) >> 32;  // tag | length
             uint64_t s = h & mask;
-            for (uint32_t probe = 0; probe < kMaxProbe; ++probe, s = (s + 1) & mask) {  // (kd_insert_rec's bound)
+            for (uint64_t probe = 0; probe < bound; ++probe, s = (s + 1) & mask) {  // (the build's longest probe)
                 const unsigned long long *slot = table + kSlotWords * s;
                 const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(slot);
                 if (a.x == kEmptySlot) break;
@@ -251,6 +252,7 @@ int gck_ctx_get_batch(gck_ctx *ctx, const uint8_t *keys, const uint64_t *key_off
     GCK_HIP(hipMemcpyAsync(c->d_gkoff.p, key_off, (n + 1) * 8ull, hipMemcpyHostToDevice, s));
     k_get_lookup<<<(n + 255) / 256, 256, 0, s>>>(
         c->d_gkeys.as<uint8_t>(), c->d_gkoff.as<uint64_t>(), n, c->d_ktab.as<unsigned long long>(), c->kd_slots,
+        c->kd_probe_bound,
         c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
         c->d_out.as<gck_rec>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_gstat.as<int32_t>(),
         c->d_gitem.as<uint64_t>(), c->d_gvsize.as<uint32_t>(), c->d_gexp.as<uint32_t>());

@@ -94,7 +94,11 @@ __device__ __forceinline__ uint32_t slot_rec(unsigned long long w0) { return (ui
 // M keys of 10.24 M records -> 8 M slots, 256 MiB: it stays in the Infinity
 // Cache, which 16 M slots of 32 B did not).  A key that finds no empty slot
 // within kMaxProbe probes sets the overflow word and the table is built again
-// for every record distinct (kd_table_slots(n)); a lookup stops there too.
+// for every record distinct (kd_table_slots(n), load <= 0.8); that last build
+// probes without a bound (a crafted or unlucky key set whose hashes cluster
+// still gets a keydir, as the reference's Go map would) and records its
+// longest probe past kMaxProbe, which is then the lookups' bound
+// (Ctx::kd_probe_bound).
 constexpr uint32_t kMaxProbe = 256;
 inline uint64_t kd_table_slots(uint64_t keys) {
     uint64_t slots = 1024;
@@ -148,16 +152,18 @@ __device__ __forceinline__ bool slot_key_equal(const uint8_t *__restrict__ arena
 // word 0's tag and length before any key bytes; records of the same key keep
 // the largest index with a 64-bit atomicMax, so the last writer in walk order
 // wins whatever order the lanes run in.  Keys are never removed, so a probe
-// sequence never skips a key's slot.  False: no slot within kMaxProbe probes.
+// sequence never skips a key's slot.  False: no slot within `bound` probes.
+// Probes past kMaxProbe (the unbounded last build) are recorded in *longest.
 // (k_kd_insert, and k_finalize when the run builds the table: gck_ctx_keydir_hash)
 template <class Words>
 __device__ __forceinline__ bool kd_insert_rec(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off,
                                               const uint2 *__restrict__ rec_kv, unsigned long long *__restrict__ table,
                                               uint64_t mask, uint64_t h, uint64_t r, bool tomb, const Words &k,
-                                              uint32_t len) {
+                                              uint32_t len, uint64_t bound = kMaxProbe, uint32_t *longest = nullptr) {
     const unsigned long long mine = slot_word0(h, len, r, tomb);
     uint64_t s = h & mask;
-    for (uint32_t probe = 0; probe < kMaxProbe; ++probe, s = (s + 1) & mask) {
+    for (uint64_t probe = 0; probe < bound; ++probe, s = (s + 1) & mask) {
+        if (probe >= kMaxProbe && longest) atomicMax(longest, (uint32_t)min(probe + 1, (uint64_t)0xFFFFFFFFu));
         unsigned long long *slot = table + kSlotWords * s;
         // plain reads: word 0 only goes EMPTY -> (tag, len, i) -> (tag, len,
         // larger i), the key words EMPTY -> the claimer's key, so a stale word

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
                                                    const uint2 *__restrict__ rec_kv, uint64_t n,
                                                    uint64_t *__restrict__ khash,
                                                    unsigned long long *__restrict__ table, uint64_t mask,
-                                                   int hashed, uint32_t *__restrict__ kstat) {
+                                                   int hashed, uint32_t *__restrict__ kstat, uint64_t bound) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = n - 1 - i;
         const uint2 kv = rec_kv[r];
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void k_kd_insert(const uint8_t *__restrict__ a
         const KeyRegs k(arena, rec_off[r] + 16, len);
         const uint64_t h = hashed ? khash[r] : key_hash(k.m, len);
         if (!hashed) khash[r] = h;
-        if (!kd_insert_rec(arena, rec_off, rec_kv, table, mask, h, r, kv.x == 0, k, len))
+        if (!kd_insert_rec(arena, rec_off, rec_kv, table, mask, h, r, kv.x == 0, k, len, bound, kstat + 2))
             atomicOr(kstat, 1u);
     }
 }
@@ -351,7 +351,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     uint64_t slots = filled ? c->kd_tab_slots : kd_table_slots(kd_keys_expected(c->kd_keys_hint, n));
     const uint64_t nt = (n + kKdTile - 1) / kKdTile;
     int rc;
-    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_live.ensure(n * 4)) || (rc = c->d_kdstat.ensure(8)) ||
+    if ((rc = c->d_khash.ensure(n * 8)) || (rc = c->d_live.ensure(n * 4)) || (rc = c->d_kdstat.ensure(12)) ||
         (rc = c->d_ktile.ensure((nt + 1) * 4)) || (rc = c->d_kdout.ensure(n * sizeof(gck_rec))) ||
         (rc = c->d_kdidx.ensure(n * 4)))
         return rc;
@@ -366,14 +366,15 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
     GCK_HIP(hipEventCreate(&ev.a));
     GCK_HIP(hipEventCreate(&ev.b));
     GCK_HIP(hipEventRecord(ev.a, s));
-    uint32_t live = 0, hst[2] = {0, 0};
+    uint32_t live = 0, hst[3] = {0, 0, 0};
+    constexpr int kLastAttempt = 2;  // sized for every record distinct, probes unbounded
     for (int attempt = 0;; ++attempt) {
         if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords))) return rc;
         if (filled) {
-            GCK_HIP(hipMemsetAsync(kstat + 1, 0, 4, s));  // (word 0: the finalize's overflow)
+            GCK_HIP(hipMemsetAsync(kstat + 1, 0, 8, s));  // (word 0: the finalize's overflow)
         } else {
             GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
-            GCK_HIP(hipMemsetAsync(kstat, 0, 8, s));
+            GCK_HIP(hipMemsetAsync(kstat, 0, 12, s));
         }
         GCK_HIP(hipMemsetAsync(c->d_live.p, 0, n * 4, s));
         const uint32_t grid = (uint32_t)c->n_cu * 8;
@@ -381,7 +382,7 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
             k_kd_insert<<<grid, 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(),
                                              c->d_rec_kv.as<uint2>(), n, c->d_khash.as<uint64_t>(),
                                              c->d_ktab.as<unsigned long long>(), slots - 1, c->kd_hashed ? 1 : 0,
-                                             kstat);
+                                             kstat, attempt == kLastAttempt ? slots : (uint64_t)kMaxProbe);
         c->kd_hashed = true;
         k_kd_mark<<<grid, 256, 0, s>>>(c->d_ktab.as<unsigned long long>(), slots,
                                        (flags & GCK_KD_KEEP_TOMBSTONES) ? 1u : 0u, c->d_live.as<uint32_t>(), kstat);
@@ -392,17 +393,20 @@ int gck_ctx_keydir(gck_ctx *ctx, uint32_t flags, uint64_t *n_live, double *ms) {
                                                       c->d_kdidx.as<uint32_t>());
         GCK_HIP(hipEventRecord(ev.b, s));
         GCK_HIP(hipMemcpyAsync(&live, c->d_ktile.as<uint32_t>() + nt, 4, hipMemcpyDeviceToHost, s));
-        GCK_HIP(hipMemcpyAsync(hst, kstat, 8, hipMemcpyDeviceToHost, s));
+        GCK_HIP(hipMemcpyAsync(hst, kstat, 12, hipMemcpyDeviceToHost, s));
         GCK_HIP(hipStreamSynchronize(s));
         GCK_HIP(hipGetLastError());
         if (!hst[0]) break;
         // a key found no slot within kMaxProbe probes (more keys than the
-        // table was sized for): again, sized for every record distinct
-        if (attempt == 2) return GCK_EDEVICE;
+        // table was sized for, or hashes that cluster): again, sized for every
+        // record distinct, the last time without a probe bound (that build
+        // cannot overflow: its load is <= 0.8)
+        if (attempt == kLastAttempt) return GCK_EDEVICE;
         filled = false;
         const uint64_t all = kd_table_slots(n);
-        slots = slots < all ? all : 2 * slots;
+        slots = attempt + 1 == kLastAttempt ? std::max(all, slots) : (slots < all ? all : 2 * slots);
     }
+    c->kd_probe_bound = std::max<uint64_t>(kMaxProbe, hst[2]);
     float t = 0;
     (void)hipEventElapsedTime(&t, ev.a, ev.b);
     if (ms) *ms = t;

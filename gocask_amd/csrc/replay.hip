@@ -41,6 +41,15 @@ void set_error(const char *what, hipError_t e, const char *file, int line) {
 const char *last_error() { return g_err.c_str(); }
 
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
+// Counter slots (d_counters, u32): 1 fixups, 2 chunks whose stage overflowed
+// (re-walked by k_compact), 3 CRC rejects, 6 record-table capacity overflow,
+// 8.. validation rounds, 12 finalize's workgroup tickets (the device path's
+// publish), 13 the settle rounds' grid barrier, 15 host validation loop.
+enum : int {
+    CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_FINTICKET = 12, CNT_BAR = 13,
+    CNT_HOSTVAL = 15
+};
+constexpr int kRounds = 2;             // device validation/fixup rounds
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
 constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
 constexpr uint32_t kNibBase = 32768;
@@ -386,6 +395,23 @@ __device__ void spec_chunk(const uint8_t *__restrict__ arena, const uint64_t *__
     if (lane == 0) ch_entry[c] = found;
 }
 
+// The device path's per-run zeroing (counters / results, record base and
+// ranges, row_first[0], the CRC block queue), done by k_spec_entry's first
+// wavefront: nothing reads them before the walk, and a separate k_run_init
+// launch cost ~2.5 us plus a dispatch per step.  cnt == nullptr: not asked.
+struct RunInit {
+    uint32_t *cnt;
+    uint64_t *gb;
+    uint32_t *row_first;
+    uint32_t *queue;
+};
+__device__ __forceinline__ void run_init(const RunInit &ri, uint32_t t) {
+    if (t < 32) ri.cnt[t] = 0;
+    if (t < kGbWords) ri.gb[t] = 0;
+    if (t == kQueueCrc) ri.queue[t] = 0;
+    if (t == 0) ri.row_first[0] = 0;
+}
+
 __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
                                                     const uint64_t *__restrict__ fbase,
                                                     const uint64_t *__restrict__ flen,
@@ -393,7 +419,8 @@ __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ 
                                                     const uint64_t *__restrict__ ch_start,
                                                     const uint64_t *__restrict__ ch_end,
                                                     uint64_t *__restrict__ ch_entry, uint32_t n_chunks,
-                                                    uint32_t max_key, uint64_t window) {
+                                                    uint32_t max_key, uint64_t window, RunInit ri) {
+    if (ri.cnt && blockIdx.x == 0 && threadIdx.x < 64) run_init(ri, threadIdx.x);
     const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));  // wave-uniform
     if (c >= n_chunks) return;
     GCK_CLK_BEGIN();
@@ -435,9 +462,10 @@ struct ScratchEmit {
 // that has an entry (its records are that chunk's), else the file end.  A
 // chunk without an entry is covered by the walk of the nearest earlier chunk
 // that has one.  Chunk starts are (index within the file) << chunk_shift.
-__device__ uint64_t walk_bound(const uint64_t *__restrict__ ch_entry, const uint32_t *__restrict__ f_first_chunk,
+// *nxt = that chunk (the file's chunk end fe if none), *nentry = its entry.
+__device__ uint64_t walk_bound(const uint64_t *ch_entry, const uint32_t *__restrict__ f_first_chunk,
                                const uint32_t *__restrict__ f_nchunks, const uint64_t *__restrict__ flen, uint32_t c,
-                               uint32_t f, uint32_t chunk_shift) {
+                               uint32_t f, uint32_t chunk_shift, uint32_t *nxt = nullptr, uint64_t *nentry = nullptr) {
     const uint32_t fc = f_first_chunk[f], fe = fc + f_nchunks[f];
     for (uint32_t d = c + 1; d < fe; d += 4) {
         uint64_t e[4];
@@ -445,8 +473,13 @@ __device__ uint64_t walk_bound(const uint64_t *__restrict__ ch_entry, const uint
         for (int k = 0; k < 4; ++k) e[k] = d + k < fe ? ch_entry[d + k] : kNone;  // 4 loads in flight
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            if (e[k] != kNone) return (uint64_t)(d + k - fc) << chunk_shift;
+            if (e[k] != kNone) {
+                if (nxt) *nxt = d + k;
+                if (nentry) *nentry = e[k];
+                return (uint64_t)(d + k - fc) << chunk_shift;
+            }
     }
+    if (nxt) *nxt = fe;
     return flen[f];
 }
 
@@ -472,7 +505,15 @@ __device__ void walk_into_chunk(const uint8_t *__restrict__ arena, const uint64_
 }
 
 // One lane per chunk of [c_begin, c_end): latency-bound header chain from the
-// speculative entry to the walk bound (walk_bound).
+// speculative entry to the walk bound (walk_bound).  With val (the device
+// path) the walk also does validation round 0 (k_validate's verdicts, counted
+// in *val): a lane with an entry knows the next chunk of its file that has
+// one, c' (walk_bound found it), and its own exit, so it decides c' (bad iff
+// its walk ended at an EOF or exit != entry of c'); the chunks between them
+// have no entry and are covered (the walk went past their ends, or ended at
+// an EOF), so never bad, as a file's first chunk.  Each chunk's flag is
+// written once: by its own lane (no entry, or a file's first chunk) or by
+// the lane of its predecessor with an entry.  One launch fewer per step.
 __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint64_t *__restrict__ fbase,
                                               const uint64_t *__restrict__ flen,
@@ -482,15 +523,42 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
                                               const uint64_t *__restrict__ ch_entry, uint32_t *ch_count,
                                               uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos,
                                               uint64_t *ch_wend, uint64_t *ch_aentry, uint2 *s_kv, uint32_t cap,
-                                              uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end) {
+                                              uint32_t chunk_shift, uint32_t c_begin, uint32_t c_end,
+                                              uint32_t *__restrict__ ch_bad, uint32_t *__restrict__ val) {
     GCK_CLK_BEGIN();
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end) return;
     const uint32_t f = ch_file[c];
     const uint64_t entry = ch_entry[c];
-    const uint64_t ce = entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
-    walk_into_chunk(arena, fbase, flen, c, f, ce, entry, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
-                    ch_wend, ch_aentry);
+    uint32_t nxt = 0;
+    uint64_t nentry = kNone;
+    const uint64_t ce =
+        entry != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift, &nxt, &nentry) : 0;
+    uint32_t count = 0, term = T_NONE;
+    uint64_t exit = kNone, tpos = 0, aentry = 0;
+    if (entry != kNone) {
+        ScratchEmit em{s_kv + stage_slot(c, 0, cap), cap};
+        const uint64_t base = fbase[f];
+        aentry = base + entry;
+        walk_chain(arena, base, flen[f], ce, entry, em, count, exit, term, tpos);
+    }
+    ch_aentry[c] = aentry;
+    ch_count[c] = count;
+    ch_exit[c] = exit;
+    ch_term[c] = term;
+    ch_tpos[c] = tpos;
+    ch_wend[c] = ce;
+    if (val) {
+        const uint32_t fc = f_first_chunk[f], fe = fc + f_nchunks[f];
+        if (entry == kNone || c == fc) ch_bad[c] = 0u;
+        bool bad = false;
+        if (entry != kNone && nxt < fe) {
+            bad = term != T_NONE || exit != nentry;
+            ch_bad[nxt] = bad ? 1u : 0u;
+        }
+        const uint64_t m = __ballot(bad);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(val, (uint32_t)__popcll(m));
+    }
     GCK_CLK_END(3, (c - c_begin) >> 6);
 }
 
@@ -499,7 +567,23 @@ __global__ __launch_bounds__(256) void k_walk(const uint8_t *__restrict__ arena,
 // walk must have ended exactly there (exit == entry, not at an EOF); if c has
 // none, j's walk must have covered c (exit past c's end, or an EOF: then no
 // later record exists).  If every chunk is consistent, every chunk is correct:
-// induction over the chunk order from each file's chunk 0.
+// induction over the chunk order from each file's chunk 0.  (Plain pointers:
+// k_scan_chunks' settle rounds run this after fixups of the same launch.)
+__device__ bool validate_chunk(uint32_t c, const uint32_t *ch_file, const uint64_t *ch_end, const uint64_t *ch_entry,
+                               const uint64_t *ch_exit, const uint32_t *ch_term, const uint32_t *f_first_chunk,
+                               uint32_t *ch_bad) {
+    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
+    bool bad = false;
+    if (c != fc) {
+        uint32_t j = c - 1;
+        while (j > fc && ch_entry[j] == kNone) --j;
+        const bool ended = ch_entry[j] == kNone || ch_term[j] != T_NONE;
+        const uint64_t x = ch_exit[j], e = ch_entry[c];
+        bad = e != kNone ? (ended || x != e) : (!ended && x < ch_end[c]);
+    }
+    ch_bad[c] = bad ? 1u : 0u;
+    return bad;
+}
 __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ ch_file,
                                                   const uint64_t *__restrict__ ch_end,
                                                   const uint64_t *__restrict__ ch_entry,
@@ -514,16 +598,7 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
     if (prev_counter && *prev_counter == 0) return;
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end) return;
-    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
-    bool bad = false;
-    if (c != fc) {
-        uint32_t j = c - 1;
-        while (j > fc && ch_entry[j] == kNone) --j;
-        const bool ended = ch_entry[j] == kNone || ch_term[j] != T_NONE;
-        const uint64_t x = ch_exit[j], e = ch_entry[c];
-        bad = e != kNone ? (ended || x != e) : (!ended && x < ch_end[c]);
-    }
-    ch_bad[c] = bad ? 1u : 0u;
+    const bool bad = validate_chunk(c, ch_file, ch_end, ch_entry, ch_exit, ch_term, f_first_chunk, ch_bad);
     const uint64_t m = __ballot(bad);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, (uint32_t)__popcll(m));
 }
@@ -534,6 +609,26 @@ __global__ __launch_bounds__(256) void k_validate(const uint32_t *__restrict__ c
 // another inconsistent chunk wait for a later round (the next k_validate
 // decides), so no lane reads state another lane is rewriting: the chunks a
 // fixed chunk's walk_bound reads all look back to it and wait.
+__device__ void fixup_chunk(uint32_t c, const uint8_t *__restrict__ arena, const uint64_t *fbase, const uint64_t *flen,
+                            const uint32_t *ch_file, const uint64_t *ch_end, const uint32_t *f_first_chunk,
+                            const uint32_t *f_nchunks, const uint32_t *ch_bad, uint64_t *ch_entry, uint32_t *ch_count,
+                            uint64_t *ch_exit, uint32_t *ch_term, uint64_t *ch_tpos, uint64_t *ch_wend,
+                            uint64_t *ch_aentry, uint2 *s_kv, uint32_t cap, uint32_t chunk_shift, uint32_t *counter) {
+    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
+    uint32_t j = c - 1;
+    while (j > fc && ch_entry[j] == kNone && !ch_bad[j]) --j;
+    if (ch_bad[j] || ch_entry[j] == kNone) return;
+    uint64_t e_new = kNone;
+    if (ch_term[j] == T_NONE) {
+        const uint64_t x = ch_exit[j];
+        if (x < ch_end[c]) e_new = x;
+    }
+    ch_entry[c] = e_new;
+    atomicAdd(counter, 1u);
+    const uint64_t ce = e_new != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
+    walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
+                    ch_wend, ch_aentry);
+}
 __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena,
                                                const uint64_t *__restrict__ fbase,
                                                const uint64_t *__restrict__ flen,
@@ -549,20 +644,8 @@ __global__ __launch_bounds__(256) void k_fixup(const uint8_t *__restrict__ arena
     if (bad_counter && *bad_counter == 0) return;  // nothing to fix (the common case)
     const uint32_t c = c_begin + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= c_end || !ch_bad[c]) return;
-    const uint32_t f = ch_file[c], fc = f_first_chunk[f];
-    uint32_t j = c - 1;
-    while (j > fc && ch_entry[j] == kNone && !ch_bad[j]) --j;
-    if (ch_bad[j] || ch_entry[j] == kNone) return;
-    uint64_t e_new = kNone;
-    if (ch_term[j] == T_NONE) {
-        const uint64_t x = ch_exit[j];
-        if (x < ch_end[c]) e_new = x;
-    }
-    ch_entry[c] = e_new;
-    atomicAdd(counter, 1u);
-    const uint64_t ce = e_new != kNone ? walk_bound(ch_entry, f_first_chunk, f_nchunks, flen, c, f, chunk_shift) : 0;
-    walk_into_chunk(arena, fbase, flen, c, f, ce, e_new, cap, s_kv, ch_count, ch_exit, ch_term, ch_tpos,
-                    ch_wend, ch_aentry);
+    fixup_chunk(c, arena, fbase, flen, ch_file, ch_end, f_first_chunk, f_nchunks, ch_bad, ch_entry, ch_count, ch_exit,
+                ch_term, ch_tpos, ch_wend, ch_aentry, s_kv, cap, chunk_shift, counter);
 }
 
 // Exclusive scan of per-chunk record counts -> rec_base[0..n] (one wavefront
@@ -601,7 +684,8 @@ __device__ __forceinline__ uint64_t lane63(uint64_t v) {
 __device__ void account_run(uint32_t nf, const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
                             const uint32_t *fterm, const uint64_t *ftpos, const uint64_t *ffirst,
                             const uint64_t *fnrec, uint32_t *__restrict__ carry, uint64_t cap,
-                            uint64_t *__restrict__ res, uint64_t *__restrict__ grng, uint64_t *__restrict__ rng) {
+                            uint64_t *__restrict__ res, uint64_t *__restrict__ grng, uint64_t *__restrict__ rng,
+                            bool unsettled) {
     uint32_t last = 0, walked = nf;
     uint64_t n_end = 0;
     for (uint32_t f = 0; f < nf; ++f) {
@@ -623,6 +707,9 @@ __device__ void account_run(uint32_t nf, const uint64_t *__restrict__ flen, cons
     res[5] = n_end;
     grng[0] = 0;
     grng[1] = n_end < cap ? n_end : cap;
+    // chunks left inconsistent by the settle rounds: the run is redone on the
+    // host path; an empty range keeps finalize from reading the table
+    if (unsettled) grng[1] = 0;
     rng[0] = 0;
     rng[1] = grng[1];
 }
@@ -690,20 +777,76 @@ __device__ bool lb_last_done(uint32_t *tickets, uint32_t nb) {
     __threadfence();
     return true;
 }
-__global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__ ch_count, uint64_t *rec_base,
+// The device path's validation/fixup rounds 1..kRounds (round 0 is k_walk's),
+// run at the head of k_scan_chunks when round 0 found an inconsistent chunk:
+// the rounds of k_fixup / k_validate, separated by grid-wide barriers (the
+// launch's workgroups are all resident: one wavefront each, a few dozen).
+// Without an inconsistency (C3: none) this costs one load; the five launches
+// it replaces cost ~25 us per step.  val[r]: round r's inconsistent chunks.
+struct Settle {
+    const uint8_t *arena;
+    const uint64_t *fbase, *flen;
+    const uint32_t *ch_file;
+    const uint64_t *ch_end;
+    uint32_t *ch_bad;
+    uint64_t *ch_exit, *ch_wend, *ch_aentry;
+    uint2 *s_kv;
+    uint32_t cap, chunk_shift;
+    uint32_t *val;      // nullptr: no settle rounds (the host path launches them)
+    uint32_t *fixups;   // CNT_FIXUP
+    uint32_t *bar;      // grid barrier arrivals (zeroed per run)
+};
+// grid barrier: every wavefront of the launch arrives once per phase
+__device__ void grid_sync(uint32_t *bar, uint32_t target) {
+    __threadfence();
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(bar, 1u);
+        while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(2);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __threadfence();
+}
+__device__ void settle_rounds(const Settle &st, uint32_t nc, const uint32_t *f_first_chunk, const uint32_t *f_nchunks,
+                              uint64_t *ch_entry, uint32_t *ch_count, uint32_t *ch_term, uint64_t *ch_tpos) {
+    const uint32_t lane = threadIdx.x & 63, G = gridDim.x, T = G * 64, t = blockIdx.x * 64 + lane;
+    uint32_t phase = 0;
+    for (int r = 0; r < kRounds; ++r) {
+        if (__hip_atomic_load(&st.val[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) break;  // (the same in every wave)
+        for (uint32_t c = t; c < nc; c += T)
+            if (st.ch_bad[c])
+                fixup_chunk(c, st.arena, st.fbase, st.flen, st.ch_file, st.ch_end, f_first_chunk, f_nchunks, st.ch_bad,
+                            ch_entry, ch_count, st.ch_exit, ch_term, ch_tpos, st.ch_wend, st.ch_aentry, st.s_kv, st.cap,
+                            st.chunk_shift, st.fixups);
+        grid_sync(st.bar, ++phase * G);
+        uint32_t nbad = 0;
+        for (uint32_t c = t; c < nc; c += T)
+            nbad += validate_chunk(c, st.ch_file, st.ch_end, ch_entry, st.ch_exit, ch_term, f_first_chunk, st.ch_bad);
+        const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(nbad), 63);
+        if (lane == 0 && sum) atomicAdd(&st.val[r + 1], sum);
+        grid_sync(st.bar, ++phase * G);
+    }
+}
+// workgroups a settling k_scan_chunks launch has at least (one wavefront each)
+constexpr uint32_t kSettleBlocks = 64;
+
+__global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *ch_count, uint64_t *rec_base,
                                                     uint32_t n, uint64_t *lb, uint64_t *base_out, uint64_t cap,
                                                     uint32_t *__restrict__ overflow,
                                                     const uint32_t *__restrict__ f_first_chunk,
                                                     const uint32_t *__restrict__ f_nchunks,
-                                                    const uint64_t *__restrict__ ch_entry,
-                                                    const uint32_t *__restrict__ ch_term,
-                                                    const uint64_t *__restrict__ ch_tpos, uint32_t *f_term,
+                                                    const uint64_t *ch_entry,
+                                                    const uint32_t *ch_term,
+                                                    const uint64_t *ch_tpos, uint32_t *f_term,
                                                     uint64_t *f_tpos, uint64_t *f_first_rec, uint64_t *f_nrec,
                                                     uint32_t nfiles, int acct, const uint64_t *__restrict__ flen,
                                                     const uint32_t *__restrict__ freset, uint32_t *carry,
-                                                    uint64_t *res, uint64_t *grng, uint64_t *rng) {
+                                                    uint64_t *res, uint64_t *grng, uint64_t *rng, uint32_t nb, Settle st) {
     static_assert(kScanBlock == 64 * 64, "a lane owns 64 counts");
-    const uint32_t lane = threadIdx.x, nb = gridDim.x;
+    if (st.val && __hip_atomic_load(&st.val[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+        settle_rounds(st, n, f_first_chunk, f_nchunks, const_cast<uint64_t *>(ch_entry), const_cast<uint32_t *>(ch_count),
+                      const_cast<uint32_t *>(ch_term), const_cast<uint64_t *>(ch_tpos));
+    if (blockIdx.x >= nb) return;  // (settle-only workgroups)
+    const uint32_t lane = threadIdx.x;
     uint32_t *tickets = reinterpret_cast<uint32_t *>(lb + nb);
     const uint32_t b = lb_ticket(tickets);
     const uint32_t i0 = b * kScanBlock + lane * 64;
@@ -783,19 +926,8 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *__restrict__
     __threadfence();
     __builtin_amdgcn_wave_barrier();
     if (acct && lane == 0)
-        account_run(nfiles, flen, freset, f_term, f_tpos, f_first_rec, f_nrec, carry, cap, res, grng, rng);
-}
-
-// Zero the run's counters / results (32 u32: status GCK_OK = 0), the group
-// record bases and ranges, row_first[0] and the groups' CRC block queues: one
-// launch instead of several memsets.
-__global__ void k_run_init(uint32_t *__restrict__ cnt, uint64_t *__restrict__ gb, uint32_t *__restrict__ row_first,
-                           uint32_t *__restrict__ queue) {
-    const uint32_t t = threadIdx.x;
-    if (t < 32) cnt[t] = 0;
-    if (t < kGbWords) gb[t] = 0;
-    if (t == kQueueCrc) queue[t] = 0;
-    if (t == 0) row_first[0] = 0;
+        account_run(nfiles, flen, freset, f_term, f_tpos, f_first_rec, f_nrec, carry, cap, res, grng, rng,
+                    st.val && __hip_atomic_load(&st.val[kRounds], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0);
 }
 
 // Key offsets of a run's records for the key blob gck_replay returns with
@@ -865,36 +997,55 @@ struct DirectEmit {
     uint32_t *rec_file;
     uint32_t *row_first;
     uint64_t rb, n_total, base;
-    uint32_t f;
+    uint32_t f, re;
     __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
         const uint64_t r = rb + i;
         if (r < n_total) {
             rec_off[r] = base + p;
             rec_kv[r] = make_uint2(h.ks, h.vs);
             rec_file[r] = f;
-            set_row_first(row_first, r, base + p, base + p + 16 + (uint64_t)h.ks + h.vs);
         }
+        set_row_first(row_first, r < n_total ? r : re, base + p, base + p + 16 + (uint64_t)h.ks + h.vs);
     }
     __device__ void prime() const {}
 };
 
-// Record table in walk order: a wavefront per kCompactChunks consecutive
-// chunks c0 + c (the chunk arrays are passed offset by c0; the stage is
-// indexed by global chunk) copies their staged (KeySize, ValueSize) pairs and
-// rebuilds the record offsets from each chunk's entry (an arena offset, left
-// by the walk) by a scan of the entry sizes; chunks that overflowed the stage
-// re-walk straight into the table.  Every load a chunk needs -- count, record
-// base, file, entry and the first kPreBatches batches of its stage -- is
-// issued for all of the wavefront's chunks before the first is written: one
-// round trip per wavefront instead of two per chunk (the file's base was a
-// second, dependent one), and a quarter of the wavefronts (the grid ran in
-// eight rounds of resident wavefronts, each paying its round trips).  The
-// stage interleaves slot i of kStageIl consecutive chunks, so a workgroup's
-// stage lines are fetched once per CU.
+// Record table in walk order and the row index row_first, in one launch.
+//
+// Records: a wavefront per kCompactChunks consecutive chunks c0 + c (the
+// chunk arrays are passed offset by c0; the stage is indexed by global chunk)
+// copies their staged (KeySize, ValueSize) pairs and rebuilds the record
+// offsets from each chunk's entry (an arena offset, left by the walk) by a
+// scan of the entry sizes; chunks that overflowed the stage re-walk straight
+// into the table.  Every load a chunk needs -- count, record base, file,
+// entry and the first kPreBatches batches of its stage -- is issued for all of
+// the wavefront's chunks before the first is written: one round trip per
+// wavefront instead of two per chunk (the file's base was a second, dependent
+// one), and a quarter of the wavefronts (the grid ran in eight rounds of
+// resident wavefronts, each paying its round trips).  The stage interleaves
+// slot i of kStageIl consecutive chunks, so a workgroup's stage lines are
+// fetched once per CU.
+//
+// row_first[row] = the first record whose value ends after the row's first
+// byte; every row gets exactly one write: record r sets the rows from its start
+// to its end, [ceil(rs / 4 KiB), ceil(ve / 4 KiB)) -- to r, or to the range end
+// re = rng[1] for a record past the table (r >= n_total); the rows after file
+// f's last record (its length, or where its walk stopped: EOF class or startup
+// error), up to the next file's first row, get min(ffirst[f] + fnrec[f], re)
+// (wavefront w takes files w, w + W, ...); row n_rows (the sentinel) gets re.
+// (Three launches before: k_row_fill set every row to re first, k_row_tail
+// the tails; 12 us and a 33 MB pre-fill per C3 step.)
 #ifndef GCK_COMPACT_CHUNKS
 #define GCK_COMPACT_CHUNKS 1
 #endif
 constexpr uint32_t kCompactChunks = GCK_COMPACT_CHUNKS;
+struct RowTails {
+    const uint32_t *fterm;
+    const uint64_t *ftpos, *ffirst, *fnrec, *rng;
+    uint32_t nfiles;
+    uint64_t n_rows;
+    const uint32_t *unsettled;  // device path: the last settle round's count (nonzero: rows all 0, no table)
+};
 __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ arena,
                                                   const uint64_t *__restrict__ fbase,
                                                   const uint64_t *__restrict__ flen,
@@ -907,109 +1058,98 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   const uint2 *__restrict__ s_kv, uint32_t cap, uint32_t c0,
                                                   uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
                                                   uint2 *rec_kv, uint32_t *rec_file, uint32_t *row_first,
-                                                  uint32_t *counters) {
+                                                  uint32_t *counters, RowTails rt) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t cw = (blockIdx.x * 16 + (threadIdx.x >> 6)) * kCompactChunks;
-    if (cw >= n_chunks) return;
-    GCK_CLK_BEGIN();
-    constexpr uint32_t K = kCompactChunks;
-    uint32_t cnt[K], f[K];
-    uint64_t rb[K], ae[K];
-    uint2 pre[K][kPreBatches];
-#pragma unroll
-    for (uint32_t j = 0; j < K; ++j) {
-        const uint32_t c = min(cw + j, n_chunks - 1);  // (a chunk past the end repeats the last: skipped below)
-        cnt[j] = ch_count[c];
-        rb[j] = rec_base[c];
-        f[j] = ch_file[c];
-        ae[j] = ch_aentry[c];
-#pragma unroll
-        for (uint32_t k = 0; k < kPreBatches; ++k) pre[j][k] = s_kv[stage_slot(c0 + c, 64 * k + lane, cap)];
+    const uint32_t wv = blockIdx.x * 16 + (threadIdx.x >> 6), cw = wv * kCompactChunks;
+    const uint32_t re = (uint32_t)rt.rng[1];
+    if (rt.unsettled && *rt.unsettled) {
+        // chunks left inconsistent (the run is redone on the host path): the
+        // walks may leave rows unset, so every row points at record 0 and
+        // k_crc_rows finds no record end (finalize's range is empty)
+        for (uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= rt.n_rows;
+             row += (uint64_t)gridDim.x * blockDim.x)
+            row_first[row] = 0;
+        return;
     }
+    GCK_CLK_BEGIN();
+    if (cw < n_chunks) {
+        constexpr uint32_t K = kCompactChunks;
+        uint32_t cnt[K], f[K];
+        uint64_t rb[K], ae[K];
+        uint2 pre[K][kPreBatches];
 #pragma unroll
-    for (uint32_t j = 0; j < K; ++j) {
-        const uint32_t c = cw + j;
-        // no entry (count 0), nothing staged, or past the record capacity
-        if (c >= n_chunks || cnt[j] == 0 || rb[j] >= n_total) continue;
-        if (cnt[j] <= cap) {
-            uint64_t run = ae[j];  // arena offset of the next record
-            // batches past the preloaded ones: the next batch's stage entries
-            // are loaded while this batch is written
-            uint2 nxt = make_uint2(0u, 0u);
-            for (uint32_t i0 = 0; i0 < cnt[j]; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                const bool in = i < cnt[j];
-                const uint32_t b = i0 / 64;  // (uniform)
-                uint2 kv = nxt;
+        for (uint32_t j = 0; j < K; ++j) {
+            const uint32_t c = min(cw + j, n_chunks - 1);  // (a chunk past the end repeats the last: skipped below)
+            cnt[j] = ch_count[c];
+            rb[j] = rec_base[c];
+            f[j] = ch_file[c];
+            ae[j] = ch_aentry[c];
 #pragma unroll
-                for (uint32_t k = 0; k < kPreBatches; ++k)
-                    if (b == k) kv = pre[j][k];
-                if (!in) kv = make_uint2(0u, 0u);
-                if (b + 1 >= kPreBatches)
-                    nxt = i + 64 < cnt[j] ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
-                // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
-                // inclusive scan is exact in 24-bit halves (entries < 2^33)
-                const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
-                const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
-                const uint64_t r = rb[j] + i;
-                if (in && r < n_total) {
-                    const uint64_t ve = run + (((uint64_t)hi << 24) + lo);
-                    rec_off[r] = ve - e;
-                    rec_kv[r] = kv;
-                    rec_file[r] = f[j];
-                    set_row_first(row_first, r, ve - e, ve);
+            for (uint32_t k = 0; k < kPreBatches; ++k) pre[j][k] = s_kv[stage_slot(c0 + c, 64 * k + lane, cap)];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < K; ++j) {
+            const uint32_t c = cw + j;
+            // no entry (count 0): nothing staged
+            if (c >= n_chunks || cnt[j] == 0) continue;
+            if (cnt[j] <= cap) {
+                uint64_t run = ae[j];  // arena offset of the next record
+                // batches past the preloaded ones: the next batch's stage entries
+                // are loaded while this batch is written
+                uint2 nxt = make_uint2(0u, 0u);
+                for (uint32_t i0 = 0; i0 < cnt[j]; i0 += 64) {
+                    const uint32_t i = i0 + lane;
+                    const bool in = i < cnt[j];
+                    const uint32_t b = i0 / 64;  // (uniform)
+                    uint2 kv = nxt;
+#pragma unroll
+                    for (uint32_t k = 0; k < kPreBatches; ++k)
+                        if (b == k) kv = pre[j][k];
+                    if (!in) kv = make_uint2(0u, 0u);
+                    if (b + 1 >= kPreBatches)
+                        nxt = i + 64 < cnt[j] ? s_kv[stage_slot(c0 + c, i + 64, cap)] : make_uint2(0u, 0u);
+                    // entry size (a tombstone's: 16 + len(key), as KeySize = 0); the
+                    // inclusive scan is exact in 24-bit halves (entries < 2^33)
+                    const uint64_t e = in ? 16ull + kv.x + kv.y : 0ull;
+                    const uint32_t lo = wave_incl_sum((uint32_t)(e & 0xFFFFFFu)), hi = wave_incl_sum((uint32_t)(e >> 24));
+                    const uint64_t r = rb[j] + i;
+                    if (in) {
+                        const uint64_t ve = run + (((uint64_t)hi << 24) + lo);
+                        if (r < n_total) {
+                            rec_off[r] = ve - e;
+                            rec_kv[r] = kv;
+                            rec_file[r] = f[j];
+                        }
+                        set_row_first(row_first, r < n_total ? r : re, ve - e, ve);
+                    }
+                    run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
+                           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
                 }
-                run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
-                       (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+            } else if (lane == 0) {
+                atomicAdd(&counters[CNT_STAGE], 1u);
+                const uint64_t base = fbase[f[j]];
+                DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb[j], n_total, base, f[j], re};
+                uint32_t count, term;
+                uint64_t exit, tpos;
+                walk_chain(arena, base, flen[f[j]], ch_wend[c], ch_entry[c], em, count, exit, term, tpos);
             }
-        } else if (lane == 0) {
-            atomicAdd(&counters[2], 1u);
-            const uint64_t base = fbase[f[j]];
-            DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb[j], n_total, base, f[j]};
-            uint32_t count, term;
-            uint64_t exit, tpos;
-            walk_chain(arena, base, flen[f[j]], ch_wend[c], ch_entry[c], em, count, exit, term, tpos);
         }
     }
-    GCK_CLK_END(4, cw / K);
+    // the rows after each file's last record, and the sentinel
+    const uint32_t W = gridDim.x * 16;
+    for (uint32_t f = wv; f < rt.nfiles; f += W) {
+        const uint64_t end = fbase[f] + (rt.fterm[f] != T_NONE ? rt.ftpos[f] : flen[f]);
+        const uint64_t r1 = f + 1 < rt.nfiles ? fbase[f + 1] / kRow : rt.n_rows;
+        const uint32_t v = (uint32_t)min(rt.ffirst[f] + rt.fnrec[f], (uint64_t)re);
+        for (uint64_t row = (end + kRow - 1) / kRow + lane; row < r1; row += 64) row_first[row] = v;
+    }
+    if (wv == 0 && lane == 0) row_first[rt.n_rows] = re;
+    GCK_CLK_END(4, cw / kCompactChunks);
 }
 
 __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uint2 *rec_kv, uint64_t r) {
     const uint2 kv = rec_kv[r];
     return rec_off[r] + 16 + (uint64_t)kv.x + kv.y;  // tombstone: KeySize 0, the key is the "value"
-}
-
-// row_first[row] = first record whose value ends after the row's first byte.
-// k_row_fill sets rows [r0, r1] to rng[1] (the record range's end: the value
-// of rows past the last record end); k_compact then sets the rows of every
-// record, k_row_tail the rows after each file's last record, on the same
-// stream.  Grid-stride over the range.
-__global__ void k_row_fill(uint32_t *__restrict__ row_first, uint64_t r0, uint64_t r1,
-                           const uint64_t *__restrict__ rng) {
-    const uint32_t v = (uint32_t)rng[1];
-    for (uint64_t row = r0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= r1;
-         row += (uint64_t)gridDim.x * blockDim.x)
-        row_first[row] = v;
-}
-
-// Rows after file f's last record, up to the next file's first row, get the
-// next record: ffirst[f] + fnrec[f] (the rows of records are set by
-// k_compact).  The last record ends at the file's length, or where its walk
-// stopped (EOF class or startup error, as k_account_grp).  Files whose
-// records all lie past the range rng keep k_row_fill's value.  One workgroup
-// per file of [f0, f0 + gridDim.x); nf = files in the arena.
-__global__ void k_row_tail(const uint64_t *__restrict__ fbase, const uint64_t *__restrict__ flen,
-                           const uint32_t *__restrict__ fterm, const uint64_t *__restrict__ ftpos,
-                           const uint64_t *__restrict__ ffirst, const uint64_t *__restrict__ fnrec, uint32_t f0,
-                           uint32_t nf, uint64_t n_rows, const uint64_t *__restrict__ rng,
-                           uint32_t *__restrict__ row_first) {
-    const uint32_t f = f0 + blockIdx.x;
-    const uint64_t re = rng[1];
-    if (f >= nf || ffirst[f] >= re) return;
-    const uint64_t end = fbase[f] + (fterm[f] != T_NONE ? ftpos[f] : flen[f]);
-    const uint64_t r1 = f + 1 < nf ? fbase[f + 1] / kRow : n_rows;
-    const uint32_t v = (uint32_t)min(ffirst[f] + fnrec[f], re);
-    for (uint64_t row = (end + kRow - 1) / kRow + threadIdx.x; row < r1; row += blockDim.x) row_first[row] = v;
 }
 
 constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
@@ -1604,7 +1744,7 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
                                                   const uint32_t *__restrict__ xb, gck_rec *__restrict__ out,
                                                   uint32_t *counters, uint64_t *__restrict__ khash,
                                                   unsigned long long *__restrict__ ktab, uint64_t kmask,
-                                                  uint32_t *__restrict__ kstat) {
+                                                  uint32_t *__restrict__ kstat, uint32_t *mbox) {
     __shared__ uint32_t Tz[1024];  // Z_4096 as 4 byte tables
     __shared__ uint32_t T[1024];   // slicing-by-4 tables T0..T3
     // gf_mul_lds: one 4 KiB table region per wave, then R (y * x^4 = (y >> 4) ^
@@ -1966,7 +2106,23 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(n_rej), 63);
     if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&blk_rej, wsum);
     __syncthreads();
-    if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[3], blk_rej);
+    if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[CNT_REJECT], blk_rej);
+    // device path: the workgroup that finishes last publishes the run's 32
+    // counters / results into the mapped host mailbox (a k_publish launch
+    // after finalize cost ~4 us and a dispatch per step)
+    if (mbox) {
+        __shared__ uint32_t last;
+        if (threadIdx.x == 0) {
+            __threadfence();
+            last = atomicAdd(&counters[CNT_FINTICKET], 1u) == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (last && threadIdx.x < 32) {
+            __threadfence();
+            const uint32_t v = __hip_atomic_load(&counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(mbox + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ------------------------------------------------------------- host side ---
@@ -2051,9 +2207,11 @@ static int ctx_init(Ctx *c, const gck_opts *o) {
     }
     c->device = d.device;
     c->n_cu = prop.multiProcessorCount;
-    int bpc = 0;
+    int bpc = 0, bph = 0;
     GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, reinterpret_cast<const void *>(k_finalize<false>), kFinThreads, 0));
+    GCK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bph, reinterpret_cast<const void *>(k_finalize<true>), kFinThreads, 0));
     c->fin_blocks_per_cu = bpc > 0 ? bpc : 1;
+    c->fin_blocks_per_cu_hash = bph > 0 ? bph : 1;
     GCK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) GCK_HIP(hipEventCreate(&e));
     if (multmodp(kXinv, kX0 >> 1) != kX0) return GCK_EINVAL;
@@ -2227,11 +2385,6 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
 
 static inline uint32_t nblk(uint64_t n, uint32_t per) { return (uint32_t)((n + per - 1) / per); }
 
-// Counter slots (d_counters, u32): 1 fixups, 2 chunks whose stage overflowed
-// (re-walked by k_compact), 3 CRC rejects, 6 record-table capacity overflow,
-// 8.. validation rounds, 15 host validation loop.
-enum : int { CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_HOSTVAL = 15 };
-constexpr int kRounds = 2;             // device validation/fixup rounds
 
 static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, const uint32_t *bad_cnt = nullptr) {
     k_fixup<<<nblk(c1 - c0, 256), 256, 0, s>>>(
@@ -2243,35 +2396,34 @@ static void launch_fixup(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, const 
         c->d_counters.as<uint32_t>() + CNT_FIXUP, bad_cnt);
 }
 
-// Boundary discovery for chunks [c0, c1): speculative entries, chain walks,
-// kRounds validate/fixup rounds and a final validation counted at val_cnt[kRounds].
-// after_spec: launched between the speculation and the walk (the device
-// path's k_run_init: the step's first kernel is then the 0.2 ms speculation,
-// so the GPU is not idle while the host launches the second; 19 us per C3
-// step in the kernel trace of profiles/r5end3 with k_run_init first)
-struct NoLaunch {
-    void operator()() const {}
-};
-template <class AfterSpec = NoLaunch>
-static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt,
-                            AfterSpec after_spec = AfterSpec()) {
+// Boundary discovery for chunks [c0, c1): speculative entries, chain walks
+// and validation.  Host path (dev == false): kRounds validate/fixup rounds
+// and a final validation, counted at val_cnt[0..kRounds], as launches of
+// their own.  Device path: k_spec_entry also zeroes the run's counters (the
+// k_run_init launch before), k_walk does validation round 0, and the later
+// rounds run at the head of k_scan_chunks only when round 0 found an
+// inconsistent chunk (launch_scan's settle): two launches where there were
+// eight.
+static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint32_t *val_cnt, bool dev) {
     const uint32_t n = c1 - c0, cap = c->opts.chunk_cap;
-    if (!n) {
-        after_spec();
-        return;
-    }
-    k_spec_entry<<<nblk(n, 4), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-                                            c->d_ch_file.as<uint32_t>() + c0, c->d_ch_start.as<uint64_t>() + c0,
-                                            c->d_ch_end.as<uint64_t>() + c0, c->d_ch_entry.as<uint64_t>() + c0, n,
-                                            c->opts.max_key, c->opts.spec_window);
-    after_spec();
+    RunInit ri{nullptr, nullptr, nullptr, nullptr};
+    if (dev)
+        ri = RunInit{c->d_counters.as<uint32_t>(), c->d_gbase.as<uint64_t>(), c->d_row_first.as<uint32_t>(),
+                     c->d_queue.as<uint32_t>()};
+    k_spec_entry<<<std::max<uint32_t>(1, nblk(n, 4)), 256, 0, s>>>(
+        c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>() + c0,
+        c->d_ch_start.as<uint64_t>() + c0, c->d_ch_end.as<uint64_t>() + c0, c->d_ch_entry.as<uint64_t>() + c0, n,
+        c->opts.max_key, c->opts.spec_window, ri);
+    if (!n) return;
     k_walk<<<nblk(n, 256), 256, 0, s>>>(c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
                                         c->d_ch_file.as<uint32_t>(), c->d_ffirst.as<uint32_t>(),
                                         c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
                                         c->d_ch_count.as<uint32_t>(), c->d_ch_exit.as<uint64_t>(),
                                         c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(),
                                         c->d_ch_wend.as<uint64_t>(), c->d_ch_aentry.as<uint64_t>(), c->d_stage.as<uint2>(),
-                                        cap, c->chunk_shift, c0, c1);
+                                        cap, c->chunk_shift, c0, c1, c->d_ch_bad.as<uint32_t>(),
+                                        dev ? val_cnt : nullptr);
+    if (dev) return;
     for (int r = 0; r <= kRounds; ++r) {
         k_validate<<<nblk(n, 256), 256, 0, s>>>(c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(),
                                                 c->d_ch_entry.as<uint64_t>(), c->d_ch_exit.as<uint64_t>(),
@@ -2285,42 +2437,41 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
 
 // Record slots of every chunk, the file summaries and, with acct (the device
 // path), the run's bookkeeping: one launch of k_scan_chunks.  gbase[1] = the
-// record total (clamped to cap); grng / rng as account_run.
+// record total (clamped to cap); grng / rng as account_run.  settle (the
+// device path): the validation/fixup rounds after k_walk's, when it found an
+// inconsistent chunk (val = the run's CNT_VAL counters).
 static void launch_scan(Ctx *c, hipStream_t s, uint64_t *gbase, uint64_t cap, bool acct, uint64_t *res = nullptr,
-                        uint64_t *grng = nullptr, uint64_t *rng = nullptr) {
+                        uint64_t *grng = nullptr, uint64_t *rng = nullptr, bool settle = false) {
     const uint32_t n = c->n_chunks, nb = std::max<uint32_t>(1, nblk(n, kScanBlock));
-    k_scan_chunks<<<nb, 64, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), n,
-                                    c->d_bsum.as<uint64_t>(), gbase + 1, cap, c->d_counters.as<uint32_t>() + CNT_CAP,
-                                    c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
-                                    c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
-                                    c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
-                                    c->nfiles, acct ? 1 : 0, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
-                                    c->d_carry.as<uint32_t>(), res, grng, rng);
+    uint32_t *cnt = c->d_counters.as<uint32_t>();
+    const Settle st{c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
+                    c->d_ch_file.as<uint32_t>(), c->d_ch_end.as<uint64_t>(), c->d_ch_bad.as<uint32_t>(),
+                    c->d_ch_exit.as<uint64_t>(), c->d_ch_wend.as<uint64_t>(), c->d_ch_aentry.as<uint64_t>(),
+                    c->d_stage.as<uint2>(), c->opts.chunk_cap, c->chunk_shift,
+                    settle && n ? cnt + CNT_VAL : nullptr, cnt + CNT_FIXUP, cnt + CNT_BAR};
+    const uint32_t grid = settle ? std::max(nb, kSettleBlocks) : nb;
+    k_scan_chunks<<<grid, 64, 0, s>>>(c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), n,
+                                      c->d_bsum.as<uint64_t>(), gbase + 1, cap, cnt + CNT_CAP,
+                                      c->d_ffirst.as<uint32_t>(), c->d_fnch.as<uint32_t>(), c->d_ch_entry.as<uint64_t>(),
+                                      c->d_ch_term.as<uint32_t>(), c->d_ch_tpos.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
+                                      c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(), c->d_fnrec.as<uint64_t>(),
+                                      c->nfiles, acct ? 1 : 0, c->d_flen.as<uint64_t>(), c->d_freset.as<uint32_t>(),
+                                      c->d_carry.as<uint32_t>(), res, grng, rng, nb, st);
 }
 
-// Record table of chunks [c0, c1) and row index (row_first) of rows [r0, r1]
-// of files [f0, f1); rng = the records' range.
-static void launch_records(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uint64_t r0, uint64_t r1, uint32_t f0,
-                           uint32_t f1, const uint64_t *rng, uint64_t cap) {
-    const uint32_t n = c1 - c0, ccap = c->opts.chunk_cap;
-    const uint32_t grid = (uint32_t)c->n_cu * 4;
-    k_row_fill<<<grid, 256, 0, s>>>(c->d_row_first.as<uint32_t>(), r0, r1, rng);
-    if (n)
-        k_compact<<<nblk(n, 16 * kCompactChunks), 1024, 0, s>>>(
-                                             c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(),
-                                             c->d_ch_file.as<uint32_t>() + c0, c->d_ch_wend.as<uint64_t>() + c0,
-                                             c->d_ch_entry.as<uint64_t>() + c0, c->d_ch_aentry.as<uint64_t>() + c0,
-                                             c->d_ch_count.as<uint32_t>() + c0,
-                                             c->d_rec_base.as<uint64_t>() + c0,
-                                             c->d_stage.as<uint2>(), ccap, c0, n, cap,
-                                             c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
-                                             c->d_rec_file.as<uint32_t>(), c->d_row_first.as<uint32_t>(),
-                                             c->d_counters.as<uint32_t>());
-    if (f1 > f0)
-        k_row_tail<<<f1 - f0, 256, 0, s>>>(c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_fterm.as<uint32_t>(),
-                                           c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
-                                           c->d_fnrec.as<uint64_t>(), f0, c->nfiles, c->n_rows, rng,
-                                           c->d_row_first.as<uint32_t>());
+// Record table and row index (row_first) of the whole arena, one launch;
+// rng = the records' range, cap = the table's records; unsettled (device
+// path): the run's last settle count.
+static void launch_records(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t cap, const uint32_t *unsettled) {
+    const uint32_t n = c->n_chunks, ccap = c->opts.chunk_cap;
+    const RowTails rt{c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
+                      c->d_fnrec.as<uint64_t>(), rng, c->nfiles, c->n_rows, unsettled};
+    k_compact<<<std::max<uint32_t>(1, nblk(n, 16 * kCompactChunks)), 1024, 0, s>>>(
+        c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
+        c->d_ch_wend.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(), c->d_ch_aentry.as<uint64_t>(),
+        c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), c->d_stage.as<uint2>(), ccap, 0u, n, cap,
+        c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), c->d_rec_file.as<uint32_t>(),
+        c->d_row_first.as<uint32_t>(), c->d_counters.as<uint32_t>(), rt);
 }
 
 // CRC partials of rows [r0, r1) (k_crc_rows), block queue slot q.  Record-slot
@@ -2343,9 +2494,13 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     return GCK_OK;
 }
 
-static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs) {
+// mbox (the device path): the last workgroup publishes the run's counters
+// there; *published tells whether a finalize was launched to do it.
+static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t max_recs, uint32_t *mbox = nullptr,
+                           bool *published = nullptr) {
     auto kern = c->hash_keys ? k_finalize<true> : k_finalize<false>;
     c->kd_fin_table = false;
+    if (published) *published = false;
     if (!max_recs) return GCK_OK;
     // the keydir table, filled by this finalize (gck_ctx_keydir then only
     // marks and compacts), sized for the record table's capacity
@@ -2355,16 +2510,17 @@ static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t 
     if (c->kd_fin_table) {
         const uint64_t slots = kd_table_slots(kd_keys_expected(c->kd_keys_hint, max_recs));
         int rc;
-        if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_kdstat.ensure(8))) return rc;
+        if ((rc = c->d_ktab.ensure(slots * 8 * kSlotWords)) || (rc = c->d_kdstat.ensure(12))) return rc;
         GCK_HIP(hipMemsetAsync(c->d_ktab.p, 0xFF, slots * 8 * kSlotWords, s));
-        GCK_HIP(hipMemsetAsync(c->d_kdstat.p, 0, 8, s));
+        GCK_HIP(hipMemsetAsync(c->d_kdstat.p, 0, 12, s));
         c->kd_tab_slots = slots;
         ktab = c->d_ktab.as<unsigned long long>();
         kmask = slots - 1;
     }
     // one wave of workgroups that are all resident at once (a second, partial
     // round of workgroups would double the kernel's latency-bound time)
-    const uint64_t want = nblk(max_recs, kFinThreads), res = (uint64_t)c->n_cu * c->fin_blocks_per_cu;
+    const uint64_t want = nblk(max_recs, kFinThreads),
+                   res = (uint64_t)c->n_cu * (c->hash_keys ? c->fin_blocks_per_cu_hash : c->fin_blocks_per_cu);
     const uint32_t grid = (uint32_t)(want < res ? want : res);
     kern<<<grid, kFinThreads, 0, s>>>(c->arena.as<uint8_t>(), c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(),
                                     c->d_rec_file.as<uint32_t>(), c->d_fbase.as<uint64_t>(), c->d_carry.as<uint32_t>(),
@@ -2374,7 +2530,8 @@ static int launch_finalize(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t 
                                     c->d_xa.as<uint32_t>(), c->d_xb.as<uint32_t>(),
                                     c->d_out.as<gck_rec>(), c->d_counters.as<uint32_t>(),
                                     c->hash_keys ? c->d_khash.as<uint64_t>() : nullptr, ktab, kmask,
-                                    c->d_kdstat.as<uint32_t>());
+                                    c->d_kdstat.as<uint32_t>(), mbox);
+    if (published) *published = mbox != nullptr;
     return GCK_OK;
 }
 
@@ -2450,7 +2607,7 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
     GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
-    launch_boundary(c, s, 0, nc, cnt + CNT_VAL);
+    launch_boundary(c, s, 0, nc, cnt + CNT_VAL, false);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
     const uint64_t big_cap = ~0ull >> 1;
     launch_scan(c, s, gbase, big_cap, false);
@@ -2496,7 +2653,7 @@ static int ctx_run_host(Ctx *c) {
     GCK_HIP(hipMemcpyAsync(gbase, rng_h, 16, hipMemcpyHostToDevice, s));
 
     GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], s));
-    launch_records(c, s, 0, nc, 0, c->n_rows, 0, nf, gbase, n_total);
+    launch_records(c, s, gbase, n_total, nullptr);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], s));
     if (n_total && (rc = launch_crc(c, s, 0, c->n_rows, n_total, kQueueCrc))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], s));
@@ -2524,7 +2681,8 @@ static int ctx_run_host(Ctx *c) {
     return c->status;
 }
 
-// 32 counters / results of a run into the mapped mailbox (Ctx::h_mbox)
+// 32 counters / results of a run into the mapped mailbox (Ctx::h_mbox), when
+// no finalize was launched to publish them
 __global__ void k_publish(const uint32_t *__restrict__ cnt, uint32_t *mbox) {
     __hip_atomic_store(mbox + threadIdx.x, cnt[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2545,7 +2703,7 @@ static int ctx_run_device(Ctx *c) {
     GCK_HIP(hipSetDevice(c->device));
     hipStream_t m = c->stream;
     const uint64_t cap = c->rec_cap;
-    const uint32_t nf = c->nfiles, nc = c->n_chunks;
+    const uint32_t nc = c->n_chunks;
     uint32_t *cnt = c->d_counters.as<uint32_t>();
     uint64_t *gb = c->d_gbase.as<uint64_t>();        // record base gb[0] (0) -> gb[1]
     uint64_t *grng = gb + kGbSlots, *rng = grng + 2;  // the records' range (clamped), the run's range
@@ -2557,22 +2715,22 @@ static int ctx_run_device(Ctx *c) {
     // (without phase timing only the CRC pass is bracketed: an event between
     // two kernels costs ~5-6 us of the run, kernel trace profiles/r5a)
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
-    // (k_run_init's counters, record base, queue and row 0 are first used
-    // by the walk's validation: it runs after the speculation)
-    launch_boundary(c, m, 0, nc, cnt + CNT_VAL, [&] {
-        k_run_init<<<1, 64, 0, m>>>(cnt, gb, c->d_row_first.as<uint32_t>(), c->d_queue.as<uint32_t>());
-    });
+    // six launches: speculation (+ the run's zeroing), walk (+ validation
+    // round 0), scan (+ the later rounds when needed, the bookkeeping),
+    // record table + row index, CRC pass, finalize (+ the mailbox)
+    launch_boundary(c, m, 0, nc, cnt + CNT_VAL, true);
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_SCAN], m));
-    launch_scan(c, m, gb, cap, true, res, grng, rng);
+    launch_scan(c, m, gb, cap, true, res, grng, rng, true);
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_RECORDS], m));
-    launch_records(c, m, 0, nc, 0, c->n_rows, 0, nf, grng, cap);
+    launch_records(c, m, grng, cap, cnt + CNT_VAL + kRounds);
     GCK_HIP(hipEventRecord(c->ev[PH_CRC], m));
     int rc;
     if ((rc = launch_crc(c, m, 0, c->n_rows, cap, kQueueCrc, true))) return rc;
     GCK_HIP(hipEventRecord(c->ev[PH_FINAL], m));
-    if ((rc = launch_finalize(c, m, rng, cap))) return rc;
+    bool published = false;
+    if ((rc = launch_finalize(c, m, rng, cap, c->d_mbox, &published))) return rc;
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_END], m));
-    k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
+    if (!published) k_publish<<<1, 32, 0, m>>>(cnt, c->d_mbox);
     GCK_HIP(hipStreamSynchronize(m));
     GCK_HIP(hipGetLastError());
     uint32_t h[32];
@@ -2756,6 +2914,7 @@ int gck_ctx_stats(gck_ctx *ctx, gck_stats *out) {
     out->files_walked = c->files_walked;
     out->final_last_offset = c->final_last_offset;
     out->n_files = c->nfiles;
+    out->kd_longest_probe = c->kd_probe_bound > kMaxProbe ? (uint32_t)c->kd_probe_bound : 0u;
     out->n_runs = c->n_runs;
     out->ms_crc_rows_sum = c->ms_crc_sum;
     return GCK_OK;

@@ -184,7 +184,7 @@ typedef struct gck_stats {
     uint32_t files_walked;       /* files the reference would have walked         */
     uint32_t final_last_offset;  /* keyDir.lastOffset after replay                */
     uint32_t n_files;            /* files in the arena                            */
-    uint32_t reserved;
+    uint32_t kd_longest_probe;   /* last keydir build: its longest table probe past 256 (0: none) */
     uint64_t n_runs;             /* runs of this context so far                   */
     double ms_crc_rows_sum;      /* k_crc_rows time (HIP events) summed over them */
 } gck_stats;

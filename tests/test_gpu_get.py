@@ -190,3 +190,63 @@ def test_get_batch_value_lengths(g, orc, vlen):
                               max_file_size=max(1 << 16, 48 * (vlen + 28)), n_files=1)
     want, _ = orc.replay(files, [False])
     _run(g, files, [False], np.random.default_rng(vlen), want)
+
+
+def _mix64d(x):
+    """kd_common.h mix64d on a numpy uint64 array (wrapping arithmetic)."""
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _key_hash8(ids):
+    """kd_common.h key_hash of the 8-byte keys struct.pack('<Q', id)."""
+    with np.errstate(over="ignore"):
+        h = np.full(ids.shape, np.uint64(0x9E3779B97F4A7C15) ^ np.uint64(8 << 32), dtype=np.uint64)
+        h = _mix64d(h ^ (ids & np.uint64(0xFFFFFFFF)))
+        h = _mix64d(h ^ (ids >> np.uint64(32))) + np.uint64(1)
+        return _mix64d(h)
+
+
+@pytest.mark.parametrize("hashed", [False, True])
+def test_keydir_clustered_hashes(g, orc, hashed):
+    # 400 keys whose hashes share their low 12 bits: every table the build
+    # sizes (1024..4096 slots) puts them on one home slot, so the bounded
+    # builds (256 probes) overflow and the last build probes without a bound,
+    # as the reference's Go map takes any key set (core/keydir.go:22-34).
+    # The keydir and Get must still be exact, the lookups probing as far as
+    # the build did.
+    import struct
+
+    cand = np.arange(1, 3_000_000, dtype=np.uint64)
+    ids = cand[(_key_hash8(cand) & np.uint64(0xFFF)) == 0][:400]
+    assert len(ids) == 400
+    keys = [struct.pack("<Q", int(i)) for i in ids]
+    rng = np.random.default_rng(7)
+    blob, t = bytearray(), 1700000000
+    for k in keys:  # every key once, then a third of them again (the later record wins)
+        blob += orc.entry(t, k, rng.bytes(int(rng.integers(1, 40))))
+        t += 1
+    for k in keys[::3]:
+        blob += orc.entry(t, k, rng.bytes(int(rng.integers(1, 40))))
+        t += 1
+    for k in keys[1::7]:
+        blob += orc.tombstone(t, k)
+        t += 1
+    files, reset = [np.frombuffer(bytes(blob), dtype=np.uint8)], [False]
+    want, _ = orc.replay(files, reset)
+    kd, deleted = _keydir(files, want)
+    with g.ReplayContext() as ctx:
+        ctx.load(files, reset)
+        if hashed:
+            ctx.keydir_hash(True)
+        ctx.run()
+        live, _ = ctx.keydir()
+        assert ctx.stats()["kd_longest_probe"] > 256
+        q = _queries(kd, deleted, rng)
+        st, vs, cc, vals = ctx.get_batch(q)
+    assert len(live) == len(kd)
+    got = {bytes(files[0][int(r["rec_off"]) + 16:int(r["rec_off"]) + 16 + int(r["key_len"])]): int(r["rec_off"])
+           for r in live}
+    assert got == {k: int(r["rec_off"]) for k, r in kd.items()}
+    _check(files, kd, q, st, vs, cc, vals)

@@ -6,7 +6,8 @@ reps=$1; shift
 for rep in $(seq $reps); do
   for t in "$@"; do
     if [ -d "$t" ]; then dir=$t; lib=; else dir=.; lib=$t; fi
-    ( cd $dir && GCK_LIB_PATH=$lib timeout -k 10 150 python bench.py --no-cpu-baseline --steps 20 --warmup 3 2>/dev/null | python3 -c "
+    diag=; [ -n "$lib" ] && [ -f "${lib/libgocask_hip/libgocask_diag}" ] && diag=${lib/libgocask_hip/libgocask_diag}
+    ( cd $dir && GCK_LIB_PATH=$lib GCK_DIAG_PATH=$diag timeout -k 10 150 python bench.py --no-cpu-baseline --steps 20 --warmup 3 2>/dev/null | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); r=d['roofline']
 print('$t', 'step', d['ms_per_step'], 'crc_rows', round(r['crc_rows_ms'],3), 'stream_ms', round(34359738368/r['stream_read_gbs']/1e6, 3),
       {k: round(v,3) for k,v in d['phase_ms'].items()})" ) || exit 1

@@ -10,5 +10,5 @@ while [ $# -ge 2 ]; do
   sed -i "$expr" $d/$f
   if cmp -s $d/$f gocask_amd/csrc/$f; then echo "sed changed nothing in $f" >&2; exit 1; fi
 done
-make -s -j8 -C $d OUT=../var/libgocask_hip_$name.so BUILD=build ../var/libgocask_hip_$name.so 2>&1 | grep -v warning || true
+make -s -j8 -C $d OUT=../var/libgocask_hip_$name.so DIAG=../var/libgocask_diag_$name.so BUILD=build all 2>&1 | grep -v warning || true
 ls -la gocask_amd/var/libgocask_hip_$name.so
