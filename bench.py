@@ -249,6 +249,32 @@ def keydir_merge(g, ctx, dist, n_files, reps=2):
                      "not part of value")
 
 
+def replay_with_merge(ctx, dist, n_files, steps, my_bytes):
+    """N>1: the path end to end -- every step replays the rank's shard and
+    merges the global keydir over RCCL (shard.merge_keydir), timed together
+    between barriers; the slowest rank's time, all ranks' bytes (the rate of
+    `value` stops before the gather)."""
+    import torch
+
+    from gocask_amd import shard
+
+    base = shard.file_base(dist, n_files, device="cuda")
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.run()
+        shard.merge_keydir(ctx, dist, base)
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed, total = reduce_over_ranks(dist, time.perf_counter() - t0, my_bytes,
+                                       "cpu" if dist.get_backend() == "gloo" else "cuda")
+    return dict(value_with_merge=round(total * steps / elapsed / GiB, 2),
+                ms_per_step_with_merge=round(elapsed / steps * 1e3, 3), steps=steps,
+                note="every step: the replay of each rank's shard, then the keydir merge over RCCL "
+                     "(all-to-all of key-hash partitions, last-shard-wins per owner); max over ranks")
+
+
 def shard_config(cfg_name, rank):
     """A per-rank corpus for the configs that are not sharded (C1-C3, C5 at
     N > 1: rank r replays its own copy of the spec with seed + r)."""
@@ -302,10 +328,21 @@ def relaunch(n, argv):
     return subprocess.run(launcher_cmd(n, argv), env=env).returncode
 
 
+def transport_label(devs):
+    """What the library's keydir exchange crosses for contexts on devs."""
+    if len(devs) == 1:
+        return "RCCL self send/receive (one device: no xGMI link crossed)"
+    if len(set(devs)) < len(devs):
+        return "device copies (loopback)"
+    return "RCCL over xGMI"
+
+
 def lib_multi(args):
     """--lib-multi (see the module docstring): one process, one context per
-    device, the library's own exchange + merge timed.  Prints one JSON line."""
-    import threading
+    device, the library's own exchange + merge timed.  Prints one JSON line.
+    One host thread per device, started once (a pool), so no timed step pays
+    a thread's start-up."""
+    from concurrent.futures import ThreadPoolExecutor
 
     import torch
 
@@ -315,21 +352,11 @@ def lib_multi(args):
     nvis = max(torch.cuda.device_count(), 1)
     devs = [d % nvis for d in range(n)]
     ctxs = [g.ReplayContext(device=dv, chunk_bytes=args.chunk_kib << 10) for dv in devs]
-    infos, errs = [None] * n, []
+    infos = [None] * n
+    pool = ThreadPoolExecutor(max_workers=n)
 
     def each(fn):
-        def wrap(i):
-            try:
-                fn(i)
-            except Exception as e:  # noqa: BLE001  (re-raised below)
-                errs.append(e)
-        th = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        if errs:
-            raise errs[0]
+        list(pool.map(fn, range(n)))  # (re-raises a worker's exception)
 
     def enc(i):
         infos[i] = encode_workload(ctxs[i], "c4", n, i, args.c4_files_per_gpu, args.c4_file_mib << 20)
@@ -350,6 +377,14 @@ def lib_multi(args):
         _, st = g.multi_keydir(ctxs, fetch=False)
         merges.append((time.perf_counter() - t1, st))
     wall, st = merges[-1]
+    # the path end to end: every step replays all shards and gathers the
+    # global keydir (north_star: per-GPU fragments gathered over RCCL)
+    t2 = time.perf_counter()
+    for _ in range(args.steps):
+        each(lambda i: ctxs[i].run())
+        g.multi_keydir(ctxs, fetch=False)
+    elapsed_m = time.perf_counter() - t2
+    pool.shutdown()
     out = {
         "metric": "device-resident data-file GiB/s CRC-verified+header-decoded, 1 GPU (+2/4/8)",
         "value": round(nbytes * args.steps / elapsed / GiB, 2),
@@ -358,10 +393,12 @@ def lib_multi(args):
         "steps": args.steps,
         "mode": "lib-multi: one process, a context per device, replays from one host thread each",
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "value_with_merge": round(nbytes * args.steps / elapsed_m / GiB, 2),
+        "ms_per_step_with_merge": round(elapsed_m / args.steps * 1e3, 3),
         "devices": devs,
         "keydir_merge_lib": dict(ms=round(wall * 1e3, 3), **{k + "_ms": round(v, 3) for k, v in st["ms"].items()},
                                  live_entries=st["n_live"], global_status=st["status"],
-                                 transport="device copies (loopback)" if len(set(devs)) < n else "RCCL over xGMI",
+                                 transport=transport_label(devs),
                                  note="gck_ctx_multi_keydir: per device the keydir with tombstones packed over the "
                                       "owners, partitions exchanged in one RCCL group, per-owner merge (the library's "
                                       "own path behind gck_replay_multi); last of 2 runs; not part of value"),
@@ -391,7 +428,8 @@ def lib_multi_child(args):
     if p.returncode or not lines:
         return dict(error=f"rc {p.returncode}: {p.stderr[-400:]}")
     d = json.loads(lines[-1])
-    return dict(d["keydir_merge_lib"], replay_gibs=d["value"], replay_ms_per_step=d["ms_per_step"])
+    return dict(d["keydir_merge_lib"], replay_gibs=d["value"], replay_ms_per_step=d["ms_per_step"],
+                value_with_merge=d["value_with_merge"], ms_per_step_with_merge=d["ms_per_step_with_merge"])
 
 
 def reduce_over_ranks(dist, elapsed, nbytes, device):
@@ -526,6 +564,7 @@ def main():
         dist1.destroy_process_group()
     elif dist is not None and not args.no_merge:
         merge = keydir_merge(g, ctx, dist, info["n_files"])
+        merge["with_replay"] = replay_with_merge(ctx, dist, info["n_files"], args.steps, my_bytes)
     stream_gbs = blocks_gbs = None
     if rank == 0:
         _, stream_gbs = ctx.stream_read_ceiling(5)
@@ -632,6 +671,9 @@ def main():
                                      "value at (File, ValuePos) re-read and CRC-checked; not part of value")
         if merge is not None:
             out["keydir_merge"] = merge
+            if "with_replay" in merge:
+                # the path end to end (replay + gather), beside `value` (replay only)
+                out["value_with_merge"] = merge["with_replay"]["value_with_merge"]
         if args.host_inclusive:
             out["host_inclusive"] = host_inclusive(g, ctx, info, args.host_inclusive)
         if world == 1 and not args.no_cpu_baseline:

@@ -61,7 +61,7 @@ enum Phase {
 // (clamped to capacity) and the run's range.
 constexpr uint32_t kGbSlots = 2, kGbWords = kGbSlots + 4;
 // d_queue: atomic work queues, zeroed before each use: k_crc_rows' row
-// blocks, k_verify's item groups.
+// blocks, k_verify's item groups, compaction.
 constexpr uint32_t kQueueCrc = 0, kQueueVerify = 1, kQueueCompact = 2, kQueueSlots = 3;
 
 
@@ -108,7 +108,7 @@ struct Ctx {
     DBuf d_rec_off, d_rec_kv, d_rec_file, d_ep, d_out;  // record table: arena offset, (KeySize, ValueSize), file
     // rows
     uint64_t n_rows = 0;
-    DBuf d_row_first, d_rend, d_queue;
+    DBuf d_blk_first, d_rend, d_queue;  // d_blk_first: the first record ending past each 64-row block start
 
     // constant tables
     DBuf d_slice, d_nib, d_xinv, d_xa, d_xb, d_zrow;

@@ -43,10 +43,11 @@ const char *last_error() { return g_err.c_str(); }
 enum : uint32_t { T_NONE = 0, T_SILENT = 1, T_ERR = 2 };
 // Counter slots (d_counters, u32): 1 fixups, 2 chunks whose stage overflowed
 // (re-walked by k_compact), 3 CRC rejects, 6 record-table capacity overflow,
-// 8.. validation rounds, 12 finalize's workgroup tickets (the device path's
-// publish), 13 the settle rounds' grid barrier, 15 host validation loop.
+// 8.. validation rounds, 12-13 finalize's arrivals and rejects (one u64: the
+// device path's publish), 5 the settle rounds' grid barrier, 14 the diag
+// kernels' sink, 15 host validation loop.
 enum : int {
-    CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_CAP = 6, CNT_VAL = 8, CNT_FINTICKET = 12, CNT_BAR = 13,
+    CNT_FIXUP = 1, CNT_STAGE = 2, CNT_REJECT = 3, CNT_BAR = 5, CNT_CAP = 6, CNT_VAL = 8, CNT_FINTICKET = 12,
     CNT_HOSTVAL = 15
 };
 constexpr int kRounds = 2;             // device validation/fixup rounds
@@ -66,7 +67,7 @@ typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
 // d(shader clock) / d(real time) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
 // gck_xp_clock() reads them back.  The product build has no stamp.
 #ifdef GCK_CLOCK_STAMPS
-constexpr uint32_t kClkWaves = 16384;
+constexpr uint32_t kClkWaves = 65536;  // k_spec_entry and k_compact run 65,536 wavefronts on C3
 constexpr int kClkKinds = 6;  // 0 k_crc_rows, 1 k_clk_stream, 2 k_spec_entry, 3 k_walk, 4 k_compact, 5 k_finalize
 __device__ uint64_t g_clk[kClkKinds][4 * kClkWaves];
 __device__ uint32_t g_clk_xcc[kClkKinds][kClkWaves];
@@ -402,14 +403,14 @@ __device__ void spec_chunk(const uint8_t *__restrict__ arena, const uint64_t *__
 struct RunInit {
     uint32_t *cnt;
     uint64_t *gb;
-    uint32_t *row_first;
+    uint32_t *blk_first;
     uint32_t *queue;
 };
 __device__ __forceinline__ void run_init(const RunInit &ri, uint32_t t) {
     if (t < 32) ri.cnt[t] = 0;
     if (t < kGbWords) ri.gb[t] = 0;
     if (t == kQueueCrc) ri.queue[t] = 0;
-    if (t == 0) ri.row_first[0] = 0;
+    if (t == 0) ri.blk_first[0] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_spec_entry(const uint8_t *__restrict__ arena,
@@ -714,6 +715,56 @@ __device__ void account_run(uint32_t nf, const uint64_t *__restrict__ flen, cons
     rng[1] = grng[1];
 }
 
+// account_run for up to 64 files, lane f holding file f's summary (its
+// terminal condition and position, first record, records): the lastOffset
+// carries are an exclusive prefix sum of the files' valid lengths (u32, as
+// the reference's uint32 offsets wrap) restarted after every file that
+// resets, and the first startup error cuts the walk, by wave scans instead of
+// one lane's loop over the files (each iteration's loads waited behind the
+// stores of the one before: ~10 us of the scan kernel's 14 on C3).
+__device__ void account_run_wave(uint32_t nf, uint32_t lane, uint32_t term, uint64_t tpos, uint64_t r0, uint64_t nrec,
+                                 const uint64_t *__restrict__ flen, const uint32_t *__restrict__ freset,
+                                 uint32_t *__restrict__ carry, uint64_t cap, uint64_t *__restrict__ res,
+                                 uint64_t *__restrict__ grng, uint64_t *__restrict__ rng, bool unsettled) {
+    const bool in = lane < nf;
+    const uint32_t valid = in ? (uint32_t)(term != T_NONE ? tpos : flen[lane]) : 0u;
+    const uint32_t rst = in ? freset[lane] : 0u;
+    const uint64_t errs = __ballot(in && term == T_ERR);
+    const uint32_t fe = errs ? (uint32_t)__builtin_ctzll(errs) : nf;  // the walk's last file (or nf)
+    // carry[f] = sum of valid over (the last file g < f that resets, f)
+    const uint32_t pex = wave_incl_sum(valid) - valid;
+    const uint32_t rst_prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rst, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    const uint64_t starts = __ballot(lane == 0 || rst_prev != 0);
+    const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1;
+    const uint32_t g = 63 - (uint32_t)__builtin_clzll(starts & le);
+    const uint32_t cf = pex - (uint32_t)__shfl((int)pex, (int)g);
+    if (in && lane <= fe) carry[lane] = cf;
+    // the file the walk ends with: the error file, else the last
+    const uint32_t fl = fe < nf ? fe : nf - 1;
+    const uint32_t last_cf = (uint32_t)__shfl((int)cf, (int)fl), last_v = (uint32_t)__shfl((int)valid, (int)fl);
+    const uint32_t last_rst = (uint32_t)__shfl((int)rst, (int)fl);
+    const uint64_t n_end = nf ? (uint64_t)__shfl((long long)(r0 + nrec), (int)fl) : 0ull;
+    if (lane == 0) {
+        uint32_t last = 0;
+        if (nf) last = last_cf + last_v;
+        if (fe < nf) {
+            res[0] = GCK_EUNEXPECTED_EOF;  // (res[2], the error's offset: lane fe, below)
+            res[1] = fe;
+        } else if (nf && last_rst) {
+            last = 0;
+        }
+        res[3] = fe < nf ? fe + 1 : nf;
+        res[4] = last;
+        res[5] = n_end;
+        grng[0] = 0;
+        grng[1] = n_end < cap ? n_end : cap;
+        if (unsettled) grng[1] = 0;
+        rng[0] = 0;
+        rng[1] = grng[1];
+    }
+    if (fe < nf && lane == fe) res[2] = tpos;
+}
+
 // Record slots, file summaries and (device path) the run's bookkeeping in one
 // launch (four to five launches before, each ~5 us of dispatch for ~1 us of
 // work).  Block b of the scan is the b-th wavefront to arrive (a ticket), so
@@ -904,13 +955,16 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *ch_count, ui
     }
     // the last wavefront to finish sees every block's bases
     if (!lb_last_done(tickets, nb)) return;
+    uint32_t term = T_NONE;  // lane f's file (the first 64 files)
+    uint64_t tpos = 0, r0 = 0, nrec = 0;
     for (uint32_t f = lane; f < nfiles; f += 64) {
         const uint32_t fc = f_first_chunk[f], nc = f_nchunks[f];
-        const uint64_t r0 = rec_base[fc], r1 = rec_base[fc + nc];
+        r0 = rec_base[fc];
+        nrec = rec_base[fc + nc] - r0;
         f_first_rec[f] = r0;
-        f_nrec[f] = r1 - r0;
-        uint32_t term = T_NONE;
-        uint64_t tpos = 0;
+        f_nrec[f] = nrec;
+        term = T_NONE;
+        tpos = 0;
         // the terminal chunk is the last non-empty chunk of the file
         for (int64_t k = (int64_t)fc + nc - 1; k >= (int64_t)fc; --k) {
             if (ch_entry[k] != kNone) {
@@ -923,11 +977,18 @@ __global__ __launch_bounds__(64) void k_scan_chunks(const uint32_t *ch_count, ui
         f_tpos[f] = tpos;
     }
     for (uint32_t k = lane; k < nb + 1; k += 64) lb[k] = 0;  // lb and both tickets
+    if (!acct) return;
+    const bool unsettled =
+        st.val && __hip_atomic_load(&st.val[kRounds], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (nfiles <= 64) {
+        account_run_wave(nfiles, lane, term, tpos, r0, nrec, flen, freset, carry, cap, res, grng, rng, unsettled);
+        return;
+    }
     __threadfence();
     __builtin_amdgcn_wave_barrier();
-    if (acct && lane == 0)
+    if (lane == 0)
         account_run(nfiles, flen, freset, f_term, f_tpos, f_first_rec, f_nrec, carry, cap, res, grng, rng,
-                    st.val && __hip_atomic_load(&st.val[kRounds], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0);
+                    unsettled);
 }
 
 // Key offsets of a run's records for the key blob gck_replay returns with
@@ -987,15 +1048,20 @@ __global__ void k_gather_keys(const uint8_t *__restrict__ arena, const uint64_t 
 // row_first[row] = the first record whose value ends after the row's first
 // byte.  Record r sets the rows from its start to its end, [ceil(rs / 4 KiB),
 // ceil(ve / 4 KiB)); k_row_tail sets the rows after a file's last record.
-__device__ __forceinline__ void set_row_first(uint32_t *row_first, uint64_t r, uint64_t rs, uint64_t ve) {
-    for (uint64_t row = (rs + kRow - 1) / kRow; row < (ve + kRow - 1) / kRow; ++row) row_first[row] = (uint32_t)r;
+// Record r = [rs, ve) is the first record ending past the start of every row
+// block (kBlkBytes = 64 rows) that starts inside it.
+constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
+constexpr uint64_t kBlkBytes = (uint64_t)kBlockRows * kRow;
+__device__ __forceinline__ void set_blk_first(uint32_t *blk_first, uint64_t r, uint64_t rs, uint64_t ve) {
+    for (uint64_t q = (rs + kBlkBytes - 1) / kBlkBytes; q < (ve + kBlkBytes - 1) / kBlkBytes; ++q)
+        blk_first[q] = (uint32_t)r;
 }
 
 struct DirectEmit {
     uint64_t *rec_off;
     uint2 *rec_kv;
     uint32_t *rec_file;
-    uint32_t *row_first;
+    uint32_t *blk_first;
     uint64_t rb, n_total, base;
     uint32_t f, re;
     __device__ void operator()(uint32_t i, uint64_t p, const Hdr &h) const {
@@ -1005,7 +1071,7 @@ struct DirectEmit {
             rec_kv[r] = make_uint2(h.ks, h.vs);
             rec_file[r] = f;
         }
-        set_row_first(row_first, r < n_total ? r : re, base + p, base + p + 16 + (uint64_t)h.ks + h.vs);
+        set_blk_first(blk_first, r < n_total ? r : re, base + p, base + p + 16 + (uint64_t)h.ks + h.vs);
     }
     __device__ void prime() const {}
 };
@@ -1043,7 +1109,7 @@ struct RowTails {
     const uint32_t *fterm;
     const uint64_t *ftpos, *ffirst, *fnrec, *rng;
     uint32_t nfiles;
-    uint64_t n_rows;
+    uint64_t n_rows, n_blocks;  // n_blocks = ceil(n_rows / 64): blk_first has n_blocks + 1 entries
     const uint32_t *unsettled;  // device path: the last settle round's count (nonzero: rows all 0, no table)
 };
 __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ arena,
@@ -1057,7 +1123,7 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                                                   const uint64_t *__restrict__ rec_base,
                                                   const uint2 *__restrict__ s_kv, uint32_t cap, uint32_t c0,
                                                   uint32_t n_chunks, uint64_t n_total, uint64_t *rec_off,
-                                                  uint2 *rec_kv, uint32_t *rec_file, uint32_t *row_first,
+                                                  uint2 *rec_kv, uint32_t *rec_file, uint32_t *blk_first,
                                                   uint32_t *counters, RowTails rt) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = blockIdx.x * 16 + (threadIdx.x >> 6), cw = wv * kCompactChunks;
@@ -1066,9 +1132,9 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
         // chunks left inconsistent (the run is redone on the host path): the
         // walks may leave rows unset, so every row points at record 0 and
         // k_crc_rows finds no record end (finalize's range is empty)
-        for (uint64_t row = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; row <= rt.n_rows;
-             row += (uint64_t)gridDim.x * blockDim.x)
-            row_first[row] = 0;
+        for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q <= rt.n_blocks;
+             q += (uint64_t)gridDim.x * blockDim.x)
+            blk_first[q] = 0;
         return;
     }
     GCK_CLK_BEGIN();
@@ -1120,7 +1186,7 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
                             rec_kv[r] = kv;
                             rec_file[r] = f[j];
                         }
-                        set_row_first(row_first, r < n_total ? r : re, ve - e, ve);
+                        set_blk_first(blk_first, r < n_total ? r : re, ve - e, ve);
                     }
                     run += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 24) +
                            (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
@@ -1128,22 +1194,24 @@ __global__ __launch_bounds__(1024) void k_compact(const uint8_t *__restrict__ ar
             } else if (lane == 0) {
                 atomicAdd(&counters[CNT_STAGE], 1u);
                 const uint64_t base = fbase[f[j]];
-                DirectEmit em{rec_off, rec_kv, rec_file, row_first, rb[j], n_total, base, f[j], re};
+                DirectEmit em{rec_off, rec_kv, rec_file, blk_first, rb[j], n_total, base, f[j], re};
                 uint32_t count, term;
                 uint64_t exit, tpos;
                 walk_chain(arena, base, flen[f[j]], ch_wend[c], ch_entry[c], em, count, exit, term, tpos);
             }
         }
     }
-    // the rows after each file's last record, and the sentinel
+    // the blocks that start after each file's last record (up to the next
+    // file's first row), and the sentinel
     const uint32_t W = gridDim.x * 16;
     for (uint32_t f = wv; f < rt.nfiles; f += W) {
         const uint64_t end = fbase[f] + (rt.fterm[f] != T_NONE ? rt.ftpos[f] : flen[f]);
-        const uint64_t r1 = f + 1 < rt.nfiles ? fbase[f + 1] / kRow : rt.n_rows;
+        const uint64_t r1 = f + 1 < rt.nfiles ? fbase[f + 1] / kRow : rt.n_rows;  // rows < r1
         const uint32_t v = (uint32_t)min(rt.ffirst[f] + rt.fnrec[f], (uint64_t)re);
-        for (uint64_t row = (end + kRow - 1) / kRow + lane; row < r1; row += 64) row_first[row] = v;
+        for (uint64_t q = (end + kBlkBytes - 1) / kBlkBytes + lane; q < (r1 + kBlockRows - 1) / kBlockRows; q += 64)
+            blk_first[q] = v;
     }
-    if (wv == 0 && lane == 0) row_first[rt.n_rows] = re;
+    if (wv == 0 && lane == 0) blk_first[rt.n_blocks] = re;
     GCK_CLK_END(4, cw / kCompactChunks);
 }
 
@@ -1152,7 +1220,6 @@ __device__ __forceinline__ uint64_t value_end(const uint64_t *rec_off, const uin
     return rec_off[r] + 16 + (uint64_t)kv.x + kv.y;  // tombstone: KeySize 0, the key is the "value"
 }
 
-constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
 constexpr int kArenaAux = 2;     // k_crc_rows' arena loads: non-temporal (buffer aux bit; DESIGN.md §6 load policy)
 #ifndef GCK_CLAIM
 #define GCK_CLAIM 1
@@ -1264,7 +1331,7 @@ __device__ __forceinline__ void fill_crc_lds(uint32_t *lds, const uint32_t *__re
 #endif
 constexpr int kPrefetch = GCK_PREFETCH;  // steps between a row's loads and its processing (2, 3 measured slower)
 __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ arena, uint64_t n_rows,
-                                                   const uint32_t *__restrict__ row_first, uint64_t n_total,
+                                                   const uint32_t *__restrict__ blk_first, uint64_t n_total,
                                                    const uint32_t *__restrict__ g_slice,
                                                    const uint32_t *__restrict__ g_nib, uint2 *__restrict__ out_ep,
                                                    uint32_t *__restrict__ out_rend,
@@ -1339,13 +1406,13 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         return last;
     };
     struct Plan {
-        uint32_t ra;  // row_first of row `lane` of the block
-        uint32_t re;  // row_first of the block's end
+        uint32_t ra;  // the block's first record end (every lane: a vector load, no SMEM in the loop)
+        uint32_t re;  // the next block's
     };
     auto load_plan = [&](uint64_t q, Plan &p) {
         const uint64_t qc = q < n_blocks ? q : n_blocks - 1;
-        p.re = row_first[min(qc * kBlockRows + kBlockRows, n_rows)];
-        p.ra = row_first[min(qc * kBlockRows + lane, n_rows)];
+        p.re = blk_first[qc + 1];
+        p.ra = blk_first[qc];
     };
     // The block's nibbles from its record ends (records [ra0, re) end in its
     // rows, in offset order): a lane per record computes (row, slab, block) of
@@ -1409,7 +1476,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
     };
     // one step: rows row0 .. row0+NR-1 = rows j0 .. j0+NR-1 of the block;
     // nib holds their plan nibbles from bit 0 up
-    auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t ra_reg, const RowBuf (&bs)[NR],
+    auto process = [&](uint64_t row0, uint32_t j0, uint32_t nib, uint32_t &rel, const RowBuf (&bs)[NR],
                        uint32_t &rend_buf) {
         uint32_t w[NR][16];
 #pragma unroll
@@ -1509,7 +1576,6 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             // blocks of this slab holding a record end (the plan is zero past
             // the last row)
             const uint32_t m = (nib >> (4 * i)) & 15u;
-            const uint32_t ra = (uint32_t)__builtin_amdgcn_readlane((int)ra_reg, (int)j);
             // the register at the start of block b (selects, no branches)
             auto cap = [&](uint32_t b) {
                 uint32_t v = b == 3 ? c3[i] : c2[i];
@@ -1518,14 +1584,15 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             };
             if (__ballot(m & (m - 1)) == 0) {
                 // common case: at most one record end per slab, its slot is
-                // ra + (cut lanes before)
+                // the block's ends before this row + (cut lanes before)
                 const uint64_t C = __ballot(m != 0);
                 const uint32_t idx =
                     __builtin_amdgcn_mbcnt_hi((uint32_t)(C >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)C, 0u));
-                store_ep(m ? (ra + idx - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
+                store_ep(m ? (rel + idx) * 8u : kDrop, cap((uint32_t)__builtin_ctz(m | 16u)), pre[i]);
 #ifdef GCK_XP_EBLK
-                { const uint32_t bb = (uint32_t)__builtin_ctz(m | 16u) & 3u; store_blk(m ? (ra + idx - ra0) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
+                { const uint32_t bb = (uint32_t)__builtin_ctz(m | 16u) & 3u; store_blk(m ? (rel + idx) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
 #endif
+                rel += (uint32_t)__builtin_popcountll(C);
             } else {
                 // a slab with 2..4 record ends (records under 64 B): ids by
                 // an exclusive count over the lanes, four stores per lane
@@ -1534,12 +1601,13 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 uint32_t mm = m;
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
-                    store_ep(q < n ? (ra + ex + q - ra0) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
+                    store_ep(q < n ? (rel + ex + q) * 8u : kDrop, cap((uint32_t)__builtin_ctz(mm | 16u)), pre[i]);
 #ifdef GCK_XP_EBLK
-                    { const uint32_t bb = (uint32_t)__builtin_ctz(mm | 16u) & 3u; store_blk(q < n ? (ra + ex + q - ra0) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
+                    { const uint32_t bb = (uint32_t)__builtin_ctz(mm | 16u) & 3u; store_blk(q < n ? (rel + ex + q) * 8u : kDrop, GCK_PICK_BLK(w[i], bb)); }
 #endif
                     mm &= mm - 1;
                 }
+                rel += (uint32_t)__builtin_amdgcn_readlane((int)(ex + n), 63);
             }
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)P[i], 63);  // F(0, row)
             rend_buf = lane == j ? total : rend_buf;
@@ -1581,6 +1649,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         }
         const uint64_t row_b = q * kBlockRows;
         uint32_t rend_buf = 0;
+        uint32_t rel = 0;  // record ends in the block's rows so far (at most one per 16 B block)
         ra0 = (uint32_t)__builtin_amdgcn_readlane((int)pc.ra, 0);  // the block's first record end
         ep_rsrc = make_rsrc(out_ep + ra0, 0x7FFFFFF0);
 #ifdef GCK_XP_EBLK
@@ -1616,7 +1685,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                 // (reusing the current row's registers), so only one row was
                 // in flight while the wave computed
                 __builtin_amdgcn_sched_barrier(0);
-                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), pc.ra, buf[u % NB],
+                process(row_b + (uint64_t)st * NR, (uint32_t)(st * NR), nib >> (4 * NR * u), rel, buf[u % NB],
                         rend_buf);
             }
         }
@@ -1781,12 +1850,14 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     }
     for (uint32_t i = threadIdx.x; i < 512; i += blockDim.x) Gm[kFinWaves * 1024 + i] = mulx(mulx(mulx(mulx(i >> 5))));
     Gm[(threadIdx.x >> 6) * 1024 + (threadIdx.x & 63)] = 0;  // entry 0 of every lane
+    __shared__ uint32_t wg_next;  // the workgroup's next piece slot (its wavefronts claim from it)
+    if (threadIdx.x == 0) wg_next = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
     char *const ldsb = reinterpret_cast<char *>(Gm);  // byte offsets into Gm
     const uint32_t mw = (threadIdx.x >> 6) * 4096 + lane * 4, rxb = kFinWaves * 4096 + (lane & 31) * 4;
     uint4 *const Ost = reinterpret_cast<uint4 *>(ldsb + (threadIdx.x >> 6) * 4096 + 256);
-    const uint64_t rb = rng[0], re = rng[1], G = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t rb = rng[0], re = rng[1];
     uint32_t n_rej = 0;  // verdict rejects of this thread (summed per block at the end)
     // wave-uniform loop: the 64 lanes hold 64 consecutive records.  Loads in
     // three waves per iteration: the record table of this iteration (issued
@@ -2065,20 +2136,36 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     // an iteration's loads (forced vmcnt(0)) and computing it
     uint64_t fin_wait = 0, fin_comp = 0;
 #endif
-    // 64-record pieces, wavefront w taking pieces w, w + W, ...; from the last
-    // piece back when the keys are inserted here (a key's later record then
-    // mostly claims its slot first, as in k_kd_insert)
-    const uint64_t npc = re > rb ? (re - rb + 63) / 64 : 0, W = G / 64;
+    // 64-record pieces.  Workgroup b owns pieces b, b + NB, b + 2 NB, ... (NB
+    // workgroups: every workgroup samples the whole corpus) and its wavefronts
+    // take them one at a time from an LDS counter, each claim issued an
+    // iteration before its piece is loaded.  A wavefront's fixed stride of 39
+    // C3 pieces took 354-443 us (p10-max, profiles/r6c: pieces of long records
+    // cost more); sharing a workgroup's 312 pieces among its 8 wavefronts
+    // evens that out.  (A global queue for the last quarter of the pieces made
+    // the kernel 0.79 ms: 40 K claims on one address serialise, profiles/r6d.)
+    // From the last piece back when the keys are inserted here (a key's later
+    // record then mostly claims its slot first, as in k_kd_insert).
+    const uint64_t npc = re > rb ? (re - rb + 63) / 64 : 0, NB = gridDim.x;
     auto at = [&](uint64_t k) { return rb + 64 * (HASH ? npc - 1 - k : k); };
-    uint64_t pc = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+    auto claim = [&]() {  // lane 0: the wavefront's next slot of its workgroup's pieces
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&wg_next, 1u);
+        return v;
+    };
+    auto piece = [&](uint32_t v) { return blockIdx.x + NB * (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    uint64_t pc = piece(claim());
+    uint32_t vn = claim();  // the piece after pc (read at the end of the first iteration)
     Rec cur, nxt;
     if (pc < npc) load_rec(at(pc), cur);
-    for (; pc < npc; pc += W) {
+    uint64_t pn = piece(vn);
+    while (pc < npc) {
         const uint64_t base = at(pc);
         const Geo g = geo(cur, base);
         Dep dc;
         issue(g, dc);
-        if (pc + W < npc) load_rec(at(pc + W), nxt);
+        if (pn < npc) load_rec(at(pn), nxt);
+        vn = claim();  // the piece after pn, in flight during this compute
 #ifdef GCK_CLOCK_STAMPS
         const uint64_t fa = __builtin_amdgcn_s_memtime();
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2090,6 +2177,8 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
         fin_comp += __builtin_amdgcn_s_memtime() - fb;
 #endif
         cur = nxt;
+        pc = pn;
+        pn = piece(vn);
     }
 #ifdef GCK_CLOCK_STAMPS
     if ((threadIdx.x & 63) == 0 && blockIdx.x * kFinWaves + (threadIdx.x >> 6) < kClkWaves) {
@@ -2106,22 +2195,25 @@ __global__ __launch_bounds__(kFinThreads) __attribute__((amdgpu_waves_per_eu(4))
     const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(n_rej), 63);
     if ((threadIdx.x & 63) == 0 && wsum) atomicAdd(&blk_rej, wsum);
     __syncthreads();
-    if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[CNT_REJECT], blk_rej);
-    // device path: the workgroup that finishes last publishes the run's 32
-    // counters / results into the mapped host mailbox (a k_publish launch
-    // after finalize cost ~4 us and a dispatch per step)
-    if (mbox) {
-        __shared__ uint32_t last;
-        if (threadIdx.x == 0) {
-            __threadfence();
-            last = atomicAdd(&counters[CNT_FINTICKET], 1u) == gridDim.x - 1;
-        }
-        __syncthreads();
-        if (last && threadIdx.x < 32) {
-            __threadfence();
-            const uint32_t v = __hip_atomic_load(&counters[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(mbox + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    if (!mbox) {
+        if (threadIdx.x == 0 && blk_rej) atomicAdd(&counters[CNT_REJECT], blk_rej);
+        return;
+    }
+    // device path: one 64-bit atomic per workgroup carries its rejects (low
+    // 40 bits) and its arrival (bit 40 up); the workgroup that arrives last
+    // knows the total and publishes the run's 32 counters / results into the
+    // mapped host mailbox (the others were written by earlier kernels).  A
+    // k_publish launch after finalize cost ~4 us and a dispatch per step; a
+    // fence per workgroup before a separate ticket cost about as much.
+    __shared__ uint64_t prior;
+    if (threadIdx.x == 0)
+        prior = atomicAdd(reinterpret_cast<unsigned long long *>(counters + CNT_FINTICKET),
+                          (1ull << 40) + blk_rej);
+    __syncthreads();
+    if ((prior >> 40) == gridDim.x - 1 && threadIdx.x < 32) {
+        uint32_t v = counters[threadIdx.x];
+        if (threadIdx.x == CNT_REJECT) v = (uint32_t)((prior & ((1ull << 40) - 1)) + blk_rej);
+        __hip_atomic_store(mbox + threadIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2250,7 +2342,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_ftpos, &c->d_fnrec, &c->d_ffirstrec, &c->d_carry, &c->d_ch_file, &c->d_ch_start,
                    &c->d_ch_end, &c->d_ch_wend, &c->d_ch_aentry, &c->d_ch_entry, &c->d_ch_exit, &c->d_ch_count, &c->d_ch_term, &c->d_ch_tpos, &c->d_ch_bad,
                    &c->d_rec_base, &c->d_bsum, &c->d_stage, &c->d_counters, &c->d_rec_off,
-                   &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_row_first, &c->d_rend,
+                   &c->d_rec_kv, &c->d_rec_file, &c->d_ep, &c->d_out, &c->d_blk_first, &c->d_rend,
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_kdstat, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
@@ -2334,7 +2426,7 @@ int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *res
         (rc = c->d_ch_exit.ensure((nc + 1) * 8)) || (rc = c->d_ch_count.ensure((nc + 1) * 4)) ||
         (rc = c->d_ch_term.ensure((nc + 1) * 4)) || (rc = c->d_ch_tpos.ensure((nc + 1) * 8)) || (rc = c->d_ch_bad.ensure((nc + 1) * 4)) ||
         (rc = c->d_rec_base.ensure((nc + 1) * 8)) || (rc = c->d_bsum.ensure((nc / kScanBlock + 4) * 8)) || (rc = c->d_freset.ensure(nf * 4)) ||
-        (rc = c->d_gbase.ensure(kGbWords * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_row_first.ensure((c->n_rows + 1) * 4)) ||
+        (rc = c->d_gbase.ensure(kGbWords * 8)) || (rc = c->d_stage.ensure((nc + kStageIl) / kStageIl * kStageIl * (cap + 1) * 8)) || (rc = c->d_blk_first.ensure(((c->n_rows + kBlockRows - 1) / kBlockRows + 1) * 4)) ||
         (rc = c->d_rend.ensure((c->n_rows + 64) * 4)) ||
         (rc = c->d_queue.ensure(kQueueSlots * 4)))
         return rc;
@@ -2408,7 +2500,7 @@ static void launch_boundary(Ctx *c, hipStream_t s, uint32_t c0, uint32_t c1, uin
     const uint32_t n = c1 - c0, cap = c->opts.chunk_cap;
     RunInit ri{nullptr, nullptr, nullptr, nullptr};
     if (dev)
-        ri = RunInit{c->d_counters.as<uint32_t>(), c->d_gbase.as<uint64_t>(), c->d_row_first.as<uint32_t>(),
+        ri = RunInit{c->d_counters.as<uint32_t>(), c->d_gbase.as<uint64_t>(), c->d_blk_first.as<uint32_t>(),
                      c->d_queue.as<uint32_t>()};
     k_spec_entry<<<std::max<uint32_t>(1, nblk(n, 4)), 256, 0, s>>>(
         c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>() + c0,
@@ -2465,16 +2557,17 @@ static void launch_scan(Ctx *c, hipStream_t s, uint64_t *gbase, uint64_t cap, bo
 static void launch_records(Ctx *c, hipStream_t s, const uint64_t *rng, uint64_t cap, const uint32_t *unsettled) {
     const uint32_t n = c->n_chunks, ccap = c->opts.chunk_cap;
     const RowTails rt{c->d_fterm.as<uint32_t>(), c->d_ftpos.as<uint64_t>(), c->d_ffirstrec.as<uint64_t>(),
-                      c->d_fnrec.as<uint64_t>(), rng, c->nfiles, c->n_rows, unsettled};
+                      c->d_fnrec.as<uint64_t>(), rng, c->nfiles, c->n_rows,
+                      (c->n_rows + kBlockRows - 1) / kBlockRows, unsettled};
     k_compact<<<std::max<uint32_t>(1, nblk(n, 16 * kCompactChunks)), 1024, 0, s>>>(
         c->arena.as<uint8_t>(), c->d_fbase.as<uint64_t>(), c->d_flen.as<uint64_t>(), c->d_ch_file.as<uint32_t>(),
         c->d_ch_wend.as<uint64_t>(), c->d_ch_entry.as<uint64_t>(), c->d_ch_aentry.as<uint64_t>(),
         c->d_ch_count.as<uint32_t>(), c->d_rec_base.as<uint64_t>(), c->d_stage.as<uint2>(), ccap, 0u, n, cap,
         c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), c->d_rec_file.as<uint32_t>(),
-        c->d_row_first.as<uint32_t>(), c->d_counters.as<uint32_t>(), rt);
+        c->d_blk_first.as<uint32_t>(), c->d_counters.as<uint32_t>(), rt);
 }
 
-// CRC partials of rows [r0, r1) (k_crc_rows), block queue slot q.  Record-slot
+// CRC partials of rows [r0, r1) (k_crc_rows; r0 a multiple of kBlockRows), block queue slot q.  Record-slot
 // scratch: cap .. cap + kEpScratch; rend scratch: rows n_rows ...
 static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t cap, uint32_t q,
                       bool queue_zeroed = false) {
@@ -2484,7 +2577,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
     k_crc_rows<<<grid, 1024, 0, s>>>(
-        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_row_first.as<uint32_t>() + r0, cap,
+        c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_blk_first.as<uint32_t>() + r0 / kBlockRows, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0
 #ifdef GCK_XP_EBLK
@@ -2605,7 +2698,7 @@ static int ctx_run_host(Ctx *c) {
     uint64_t *gbase = c->d_gbase.as<uint64_t>();
     GCK_HIP(hipMemsetAsync(cnt, 0, 64, s));
     GCK_HIP(hipMemsetAsync(gbase, 0, 16, s));
-    GCK_HIP(hipMemsetAsync(c->d_row_first.p, 0, 4, s));
+    GCK_HIP(hipMemsetAsync(c->d_blk_first.p, 0, 4, s));
     GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], s));
     launch_boundary(c, s, 0, nc, cnt + CNT_VAL, false);
     GCK_HIP(hipEventRecord(c->ev[PH_SCAN], s));
@@ -3580,10 +3673,13 @@ extern "C" {
 // k_clk_stream's; out receives 4 u64 per wavefront (clock, real time at the
 // loop start, then at the end), kClkWaves entries; zeroed by reset.
 int gck_xp_clock_reset(void) {
-    static const uint64_t zero[kClkKinds][4 * kClkWaves] = {};
-    GCK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_clk), zero, sizeof zero));
+    void *p = nullptr;
+    GCK_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_clk)));
+    GCK_HIP(hipMemset(p, 0, sizeof(uint64_t) * kClkKinds * 4 * kClkWaves));
     return GCK_OK;
 }
+// wavefronts each kind's stamps hold (the readers size their buffers by it)
+int gck_xp_clock_waves(void) { return (int)kClkWaves; }
 int gck_xp_clock_read(int which, uint64_t *out) {
     if (which < 0 || which >= kClkKinds || !out) return GCK_EINVAL;
     GCK_HIP(hipDeviceSynchronize());

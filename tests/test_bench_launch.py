@@ -92,6 +92,9 @@ def test_bench_gpus2_launches_its_ranks():
     assert "error" not in kl, kl
     assert kl["live_entries"] == km["live_entries"] and kl["global_status"] == 0
     assert kl["transport"].startswith("device copies")
+    # replay + gather timed together: slower than the replay alone, positive
+    assert 0 < d["value_with_merge"] < d["value"]
+    assert 0 < kl["value_with_merge"] < kl["replay_gibs"]
 
 
 @pytest.mark.gpu
@@ -112,4 +115,6 @@ def test_bench_lib_multi(n, self_rccl):
     assert d["n_gpus"] == n and d["value"] > 0
     kl = d["keydir_merge_lib"]
     assert kl["live_entries"] > 0 and kl["global_status"] == 0 and kl["ms"] > 0
-    assert kl["transport"] == ("RCCL over xGMI" if n == 1 else "device copies (loopback)")
+    assert kl["transport"] == ("RCCL self send/receive (one device: no xGMI link crossed)" if n == 1
+                               else "device copies (loopback)")
+    assert 0 < d["value_with_merge"] < d["value"]

@@ -94,8 +94,8 @@ def main():
             ctx.run()
         L.gck_xp_clock_reset()
         ctx.run()
-        buf = np.zeros(4 * 16384, dtype=np.uint64)
-        xb = np.zeros(16384, dtype=np.uint32)
+        buf = np.zeros(4 * L.gck_xp_clock_waves(), dtype=np.uint64)
+        xb = np.zeros(L.gck_xp_clock_waves(), dtype=np.uint32)
         assert L.gck_xp_clock_read(0, buf.ctypes.data) == 0
         assert L.gck_xp_clock_xcc(0, xb.ctypes.data) == 0
         out["crc_rows_stamped"] = stamp_stats(buf.reshape(-1, 4), xb)

@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 
 def stats(L, which, waves_per_wg):
-    buf = np.zeros(4 * 16384, dtype=np.uint64)
+    buf = np.zeros(4 * L.gck_xp_clock_waves(), dtype=np.uint64)
     assert L.gck_xp_clock_read(which, buf.ctypes.data_as(ctypes.c_void_p)) == 0
     s = buf.reshape(-1, 4).astype(np.float64)
     ok = (s[:, 1] > 0) & (s[:, 3] > s[:, 1])

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """In-kernel clocks and wavefront timing of every phase of one replay step
-(the stamps build: GCK_LIB_PATH=gocask_amd/var/libgocask_hip_clk.so).
+(the stamps build: GCK_LIB_PATH=gocask_amd/var/libgocask_hip_clk.so, built by
+make -C gocask_amd/csrc OUT=../var/libgocask_hip_clk.so BUILD=build_clk
+EXTRA=-DGCK_CLOCK_STAMPS ../var/libgocask_hip_clk.so).
 
   python tools/phase_clock.py [--secs 2.0]   -> one JSON line
 
 After >= --secs of back-to-back C3 replays, one more replay with stamps: per
-kernel (k_spec_entry: its first 16,384 chunks; k_walk, k_compact, k_crc_rows,
-k_finalize: every wavefront) the median shader clock, the span from the first
+kernel (every wavefront of k_spec_entry, k_walk, k_compact, k_crc_rows,
+k_finalize, up to 65,536) the median shader clock, the span from the first
 wavefront's start to the last one's end, and the wavefront durations.
 """
 import argparse
@@ -37,7 +39,10 @@ def summary(st):
     return dict(waves=int(len(s)), clock_ghz_median=round(float(np.median(ghz)), 3),
                 span_us=round(float(end.max()), 1), start_us_max=round(float(((s[:, 1] - t0) / 100.0).max()), 1),
                 wave_us_p50=round(float(np.median(dur)), 1), wave_us_p90=round(float(np.percentile(dur, 90)), 1),
-                wave_us_max=round(float(dur.max()), 1), end_us_p50=round(float(np.median(end)), 1),
+                wave_us_max=round(float(dur.max()), 1), wave_us_p10=round(float(np.percentile(dur, 10)), 1),
+                end_us_p50=round(float(np.median(end)), 1),
+                start_us_p50=round(float(np.median((s[:, 1] - t0) / 100.0)), 1),
+                start_us_p90=round(float(np.percentile((s[:, 1] - t0) / 100.0, 90)), 1),
                 t0_realtime=int(t0))
 
 
@@ -66,13 +71,13 @@ def main():
     out = {"config": args.config, "step_ms": round(ctx.stats()["ms_total"], 3)}
     starts = {}
     for k, name in KINDS.items():
-        buf = np.zeros(4 * 16384, dtype=np.uint64)
+        buf = np.zeros(4 * L.gck_xp_clock_waves(), dtype=np.uint64)
         assert L.gck_xp_clock_read(k, buf.ctypes.data) == 0
         out[name] = summary(buf.reshape(-1, 4))
         starts[name] = out[name].pop("t0_realtime", None)
     if hasattr(L, "gck_xp_fin_split"):
         L.gck_xp_fin_split.argtypes = [ctypes.c_void_p]
-        fs = np.zeros(2 * 16384, dtype=np.uint64)
+        fs = np.zeros(2 * L.gck_xp_clock_waves(), dtype=np.uint64)
         assert L.gck_xp_fin_split(fs.ctypes.data) == 0
         fs = fs.reshape(-1, 2).astype(np.float64)
         fs = fs[fs.sum(axis=1) > 0]
