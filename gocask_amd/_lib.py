@@ -281,6 +281,9 @@ def load_diag():
     D.gck_diag_stream_blocks.restype = ctypes.c_int
     D.gck_diag_stream_blocks.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, P(ctypes.c_double),
                                          P(ctypes.c_double)]
+    if hasattr(D, "gck_diag_stream_xp"):  # (diag libraries of older builds, for A/Bs, lack it)
+        D.gck_diag_stream_xp.restype = ctypes.c_int
+        D.gck_diag_stream_xp.argtypes = [vp] + [ctypes.c_int] * 7 + [P(ctypes.c_double), P(ctypes.c_double)]
     D.gck_diag_clock_read.restype = ctypes.c_int
     D.gck_diag_clock_read.argtypes = [vp, vp, ctypes.c_uint32]
     D.gck_diag_chunks.restype = ctypes.c_int

@@ -690,7 +690,10 @@ class ReplayContext:
 
     def phase_timing(self, on=True):
         """Events between every phase of the next runs (stats()['ms_phase'] per
-        phase); off (the default) times only the CRC pass and the whole run."""
+        phase).  Off (the default): a device-path run times only the CRC pass
+        (ms_phase 'crc_rows'; the other phases and 'pipeline' read 0, since an
+        event between two kernels costs ~6 us of the run); a host-path run
+        (a context's first) always times every phase."""
         check(self._L.gck_ctx_phase_timing(self._h, 1 if on else 0))
 
     def stream_read_ceiling(self, iters=10):
@@ -713,10 +716,29 @@ class ReplayContext:
                                                       ctypes.byref(ms), ctypes.byref(gbs)))
         return ms.value, gbs.value
 
+    def stream_xp(self, pf=1, blocks=True, threads=1024, lds_kib=160, wg_per_cu=1, iters=10, stamp=False):
+        """Stream probe (libgocask_diag.so gck_diag_stream_xp): k_crc_rows' row
+        loads with pf rows in flight per wavefront and no compute, 64-row
+        blocks per wavefront (static: block k W + w) or rows strided over the
+        wavefronts; occupancy from the workgroup size, its LDS and workgroups
+        per CU.  (ms per pass, GB/s); stamp: see clock_stamps()."""
+        ms = ctypes.c_double()
+        gbs = ctypes.c_double()
+        check(_lib.load_diag().gck_diag_stream_xp(self._h, pf, int(bool(blocks)), threads, lds_kib, wg_per_cu, iters,
+                                                  int(bool(stamp)), ctypes.byref(ms), ctypes.byref(gbs)))
+        return ms.value, gbs.value
+
+    def stream_rows_ceiling(self, iters=10, stamp=False):
+        """The stream ceiling in k_crc_rows' own geometry: one 1024-thread
+        workgroup per CU holding 160 KiB of LDS, a wavefront per 4 KiB row
+        with the next row in flight, 64-row blocks assigned statically, no
+        compute (the fastest of the round-6 probes, tools/stream_xp.py)."""
+        return self.stream_xp(1, True, 1024, 160, 1, iters, stamp)
+
     @staticmethod
     def clock_stamps():
         """(stamps u64[W, 4] = clock, real time at start; clock, real time at
-        end; xcc u32[W]) of the last stamped stream_blocks_ceiling pass."""
+        end; xcc u32[W]) of the last stamped stream_blocks_ceiling / stream_xp pass."""
         w = 16384
         st = np.zeros(4 * w, dtype=np.uint64)
         xcc = np.zeros(w, dtype=np.uint32)

@@ -193,6 +193,63 @@ __global__ __launch_bounds__(1024) void k_stream_blocks(const uint8_t *__restric
     }
 }
 
+// Stream probes for the bytes-in-flight question (round 6): k_crc_rows' row
+// loads (lane p + 16 b reads the 16 B at 1024 k + 64 p + 16 b, non-temporal
+// buffer loads) with PF rows in flight per wavefront, no compute.  BLOCKS: a
+// wavefront streams whole 64-row blocks (block k W + w, static); otherwise
+// rows are strided over the wavefronts (row k W + w).  Occupancy is set by
+// the workgroup size and the dynamic LDS the launch asks for.
+template <int PF, bool BLOCKS>
+__global__ void k_stream_xp(const uint8_t *__restrict__ arena, uint64_t n_rows, uint32_t *sink, int stamp) {
+    extern __shared__ uint32_t dyn_lds[];
+    const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t lane = threadIdx.x & 63, s_rel = 64 * (lane & 15) + 16 * (lane >> 4);
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)));
+    auto row_of = [&](uint64_t k) -> uint64_t {  // the wavefront's k-th row
+        return BLOCKS ? ((k / 64) * W + w) * 64 + (k % 64) : k * W + w;
+    };
+    auto issue = [&](uint64_t row, v4u (&v)[4]) {
+        const uint32_t r = (uint32_t)min(row, n_rows - 1);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(arena + (uint64_t)r * 4096), 0, 4096, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, s_rel + 1024 * k, 0, 2);
+    };
+    uint32_t acc = 0;
+    if (row_of(0) < n_rows) {
+        v4u B[PF + 1][4];
+#pragma unroll
+        for (int d = 0; d < PF; ++d) issue(row_of(d), B[d]);
+        for (uint64_t k = 0;; k += PF + 1) {
+#pragma unroll
+            for (int u = 0; u <= PF; ++u) {
+                issue(row_of(k + u + PF), B[(u + PF) % (PF + 1)]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc ^= B[u][j].x ^ B[u][j].y ^ B[u][j].z ^ B[u][j].w;
+                if (row_of(k + u + 1) >= n_rows) goto done;
+            }
+        }
+    }
+done:
+    if (acc == 0x9E3779B9u) {
+        dyn_lds[threadIdx.x] = acc;
+        sink[0] = dyn_lds[(threadIdx.x + 1) % blockDim.x];
+    }
+    if (stamp) {  // (as k_stream_blocks<true>: gck_diag_clock_read)
+        const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0 && w < kDclkWaves) {
+            g_dclk[4 * w] = t0;
+            g_dclk[4 * w + 1] = r0;
+            g_dclk[4 * w + 2] = t1;
+            g_dclk[4 * w + 3] = r1;
+            g_dxcc[w] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;  // HW_REG_XCC_ID[3:0]
+        }
+    }
+}
+
 // Random-access probes with k_walk's access shape (a 16 B load per hop):
 // DEP = each lane's next address depends on the bytes it just loaded (a chain
 // walk); otherwise the lane's hops are independent (8 loads in flight).
@@ -406,7 +463,58 @@ extern "C" int gck_diag_stream_blocks(gck_ctx *ctx, int iters, uint32_t static_e
     return GCK_OK;
 }
 
-// The stamps of the last stamped k_stream_blocks launch: 4 u64 per wavefront
+// k_stream_xp<pf, blocks> with workgroups of `threads` (64..1024) and
+// lds_kib of dynamic LDS each, `wg_per_cu` workgroups per CU in the grid.
+extern "C" int gck_diag_stream_xp(gck_ctx *ctx, int pf, int blocks, int threads, int lds_kib, int wg_per_cu,
+                                  int iters, int stamp, double *ms_per_iter, double *gbs) {
+    if (!ctx || iters <= 0 || pf < 1 || pf > 3 || threads < 64 || threads > 1024 || threads % 64 || lds_kib < 0 ||
+        lds_kib > 160 || wg_per_cu < 1)
+        return GCK_EINVAL;
+    Ctx *c = &ctx->c;
+    GCK_HIP(hipSetDevice(c->device));
+    if (!c->n_rows) return GCK_EINVAL;
+    uint32_t *sink = c->d_counters.as<uint32_t>() + 14;
+    const size_t lds = std::max<size_t>((size_t)lds_kib << 10, threads * 4);
+    const uint32_t grid = (uint32_t)(c->n_cu * wg_per_cu);
+    int st = 0;  // the last timed launch stamps its wavefronts
+    auto launch = [&]() {
+#define GCK_XP_L(P, B) k_stream_xp<P, B><<<grid, threads, lds, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink, st)
+        if (blocks) {
+            if (pf == 1) GCK_XP_L(1, true); else if (pf == 2) GCK_XP_L(2, true); else GCK_XP_L(3, true);
+        } else {
+            if (pf == 1) GCK_XP_L(1, false); else if (pf == 2) GCK_XP_L(2, false); else GCK_XP_L(3, false);
+        }
+#undef GCK_XP_L
+    };
+    // (dynamic LDS above 64 KiB needs the attribute)
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<1, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<2, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<3, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<1, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<2, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<3, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+    hipEvent_t a, b;
+    GCK_HIP(hipEventCreate(&a));
+    GCK_HIP(hipEventCreate(&b));
+    launch();  // warm-up
+    GCK_HIP(hipEventRecord(a, c->stream));
+    for (int i = 0; i < iters; ++i) {
+        st = stamp && i == iters - 1;
+        launch();
+    }
+    GCK_HIP(hipEventRecord(b, c->stream));
+    GCK_HIP(hipEventSynchronize(b));
+    float ms = 0;
+    GCK_HIP(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    const double per = ms / iters;
+    if (ms_per_iter) *ms_per_iter = per;
+    if (gbs) *gbs = (double)c->n_rows * 4096 / (per * 1e-3) / 1e9;
+    return GCK_OK;
+}
+
+// The stamps of the last stamped k_stream_blocks / k_stream_xp launch: 4 u64 per wavefront
 // (clock, real time at start; clock, real time at end) and its XCC id.
 extern "C" int gck_diag_clock_read(uint64_t *stamps, uint32_t *xcc, uint32_t cap_waves) {
     if (!stamps || !xcc || cap_waves < kDclkWaves) return GCK_EINVAL;

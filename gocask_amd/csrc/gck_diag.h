@@ -18,6 +18,12 @@ int gck_diag_stream_read(gck_ctx *ctx, int iters, double *ms_per_iter, double *g
  * (64-row blocks, static_eighths / 8 of the full rounds static, the rest from
  * an atomic queue) without its compute.  stamp: the last pass records
  * per-wavefront clock stamps (gck_diag_clock_read). */
+/* Stream probe: k_crc_rows' row loads, pf (1..3) rows in flight per
+ * wavefront, no compute; blocks: 64-row blocks per wavefront (else rows
+ * strided over the wavefronts); workgroups of `threads` with lds_kib of LDS,
+ * wg_per_cu of them per CU in the grid. */
+int gck_diag_stream_xp(gck_ctx *ctx, int pf, int blocks, int threads, int lds_kib, int wg_per_cu, int iters,
+                       int stamp, double *ms_per_iter, double *gbs);
 int gck_diag_stream_blocks(gck_ctx *ctx, int iters, uint32_t static_eighths, int stamp, double *ms_per_iter,
                            double *gbs);
 /* Stamps of the last stamped gck_diag_stream_blocks pass: per wavefront 4 u64

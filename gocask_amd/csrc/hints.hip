@@ -326,8 +326,11 @@ int gck_ctx_replay_hints(gck_ctx *ctx, double *ms) {
         const uint64_t nb = (n + GCK_HINT_BLOCK - 1) / GCK_HINT_BLOCK;
         // the tail must describe this file exactly (sizes checked before any
         // entry is read: every read below stays inside the file)
+        // (a file without entries has no data bytes either: nothing would
+        // check them, yet they would feed the carried lastOffset)
         if ((uint32_t)mv != GCK_HINT_MAGIC || (uint32_t)(mv >> 32) != GCK_HINT_VERSION || n > (1ull << 40) ||
-            eb > c->f_len[f] || eb < (kHintHdrB + 1) * n || c->f_len[f] != eb + 16 * nb + kHintTailB)
+            eb > c->f_len[f] || eb < (kHintHdrB + 1) * n || c->f_len[f] != eb + 16 * nb + kHintTailB ||
+            (n == 0 && db != 0))
             return GCK_EINVAL;
         hf[f] = HintFile{c->f_base[f], eb, db, ents, blks, n, segs, last, 0};
         ents += n;

@@ -1050,7 +1050,12 @@ __global__ void k_gather_keys(const uint8_t *__restrict__ arena, const uint64_t 
 // ceil(ve / 4 KiB)); k_row_tail sets the rows after a file's last record.
 // Record r = [rs, ve) is the first record ending past the start of every row
 // block (kBlkBytes = 64 rows) that starts inside it.
-constexpr int kBlockRows = 64;   // rows per k_crc_rows work item (a "row block")
+#ifndef GCK_BLOCK_ROWS
+#define GCK_BLOCK_ROWS 64
+#endif
+constexpr int kBlockRows = GCK_BLOCK_ROWS;  // rows per k_crc_rows work item (a "row block"): 32 or 64
+static_assert(kBlockRows == 32 || kBlockRows == 64, "k_crc_rows: a lane per row of the block");
+constexpr int kNibDw = kBlockRows / 8;      // nibble dwords per lane (8 rows of 4 blocks each)
 constexpr uint64_t kBlkBytes = (uint64_t)kBlockRows * kRow;
 __device__ __forceinline__ void set_blk_first(uint32_t *blk_first, uint64_t r, uint64_t rs, uint64_t ve) {
     for (uint64_t q = (rs + kBlkBytes - 1) / kBlkBytes; q < (ve + kBlkBytes - 1) / kBlkBytes; ++q)
@@ -1228,11 +1233,14 @@ constexpr uint32_t kClaim = GCK_CLAIM;   // consecutive row blocks per k_crc_row
 #ifndef GCK_LATE_CLAIM
 #define GCK_LATE_CLAIM 13
 #endif
-// the quad of a block at which k_crc_rows claims the block after next (-1: at
-// the block's start).  Claiming one block, late, holds a wave's look-ahead to
-// ~1.2 blocks instead of up to 3 when the queue runs dry: the kernel's tail
-// (wave-end spread) shrinks, -0.04 ms at C3 (profiles/r5f)
+// where in a block k_crc_rows claims the block after next, in 16ths of the
+// block's quads (-1: at the block's start).  Claiming one block, late, holds
+// a wave's look-ahead to ~1.2 blocks instead of up to 3 when the queue runs
+// dry: the kernel's tail (wave-end spread) shrinks, -0.04 ms at C3
+// (profiles/r5f).  (The claim must fall inside the block, whatever its quad
+// count: a block without one re-processed block 0 forever.)
 constexpr int kLateClaim = GCK_LATE_CLAIM;
+static_assert(kLateClaim < 16, "the late claim lies inside the block");
 #ifndef GCK_STATIC_EIGHTHS
 #define GCK_STATIC_EIGHTHS 4
 #endif
@@ -1345,6 +1353,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
                                                    ) {
     constexpr int NR = 1;                     // rows per step (two measured slower: 5.70 vs 5.64 ms)
     constexpr int kSteps = kBlockRows / NR;  // steps per block
+    constexpr int kLateQd = kLateClaim < 0 ? -1 : kLateClaim * (kSteps / 4) / 16;  // the claim's quad
     __shared__ uint32_t lds[40960];  // 128 KiB slicing tables x32 copies + 32 KiB lane-shift tables
     fill_crc_lds(lds, g_slice, g_nib);
     const uint32_t lane = threadIdx.x & 63, l31 = lane & 31;
@@ -1429,9 +1438,9 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         b.off = rec_off[r];
         b.kv = rec_kv[r];
     };
-    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch *first, uint32_t (&nb)[8]) {
+    auto build_nibs = [&](uint64_t row_b, uint32_t ra0_, uint32_t re_, const Batch *first, uint32_t (&nb)[kNibDw]) {
 #pragma unroll
-        for (int d = 0; d < 8; ++d) nb[d] = 0;
+        for (int d = 0; d < kNibDw; ++d) nb[d] = 0;
         const uint64_t base = (row0 + row_b) * kRow;
         for (uint32_t b0 = ra0_; b0 < re_; b0 += 64) {
             const uint32_t r = b0 + lane;
@@ -1449,7 +1458,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             const uint32_t dd = r < re_ ? code >> 11 : 8u;
             const uint32_t tk = (code >> 2) & 63u, tbit = (1u << (code & 3u)) << (4 * ((code >> 8) & 7u));
 #pragma unroll
-            for (int d = 0; d < 8; ++d) {
+            for (int d = 0; d < kNibDw; ++d) {
                 uint64_t act = __ballot(dd == (uint32_t)d);
                 while (act) {
                     const int i = __builtin_ctzll(act);
@@ -1643,7 +1652,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         uint64_t qnn = 0;
         Plan pnn;
         load_batch(pn, bn);
-        if constexpr (kLateClaim < 0) {
+        if constexpr (kLateQd < 0) {
             qnn = grab();
             load_plan(qnn, pnn);
         }
@@ -1655,7 +1664,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
 #ifdef GCK_XP_EBLK
         blk_rsrc = make_rsrc(out_blk + (uint64_t)ra0 * 16, 0x7FFFFFF0);
 #endif
-        uint32_t nibs[8];
+        uint32_t nibs[kNibDw];
         build_nibs(row_b, ra0, pc.re, &bc, nibs);
         // steps in quads: a quad of 4 steps consumes 4 NR plan nibbles per
         // lane; the two row buffers alternate, so each has fixed registers
@@ -1663,11 +1672,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
             // this quad's nibbles (a uniform select: qd is a loop counter)
             uint32_t nib = nibs[0];
 #pragma unroll
-            for (int d = 1; d < 8; ++d)
+            for (int d = 1; d < kNibDw; ++d)
                 if (qd * NR / 2 == d) nib = nibs[d];
             if constexpr (NR == 1) nib >>= 16 * (qd & 1);
-            if constexpr (kLateClaim >= 0) {
-                if (qd == kLateClaim) {  // (uniform)
+            if constexpr (kLateQd >= 0) {
+                if (qd == kLateQd) {  // (uniform)
                     qnn = grab();
                     load_plan(qnn, pnn);
                 }
@@ -1691,7 +1700,7 @@ __global__ __launch_bounds__(1024) void k_crc_rows(const uint8_t *__restrict__ a
         }
         // the block's 64 rrow values, one coalesced store (rows past the end
         // to the scratch slots)
-        *(row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
+        *(lane < kBlockRows && row_b + lane < n_rows ? out_rend + row_b + lane : rend_scratch + lane) = rend_buf;
         if (qn >= n_blocks) {
             GCK_CLK_END(0, w);
             return;
@@ -2382,6 +2391,10 @@ __global__ void k_upload(const uint8_t *__restrict__ src, UpList l) {
 int ctx_layout(Ctx *c, const uint64_t *lens, uint32_t nfiles, const uint8_t *reset_after) {
     GCK_HIP(hipSetDevice(c->device));
     c->nfiles = nfiles;
+    // new files: the last keydir's key count says nothing about them (a
+    // pooled ring context may have held another group or database); the next
+    // table is sized from the run's own record count
+    c->kd_keys_hint = 0;
     c->f_base.assign(nfiles, 0);
     c->f_len.assign(lens, lens + nfiles);
     c->f_reset.assign(reset_after, reset_after + nfiles);
@@ -2801,12 +2814,11 @@ static int ctx_run_device(Ctx *c) {
     uint64_t *gb = c->d_gbase.as<uint64_t>();        // record base gb[0] (0) -> gb[1]
     uint64_t *grng = gb + kGbSlots, *rng = grng + 2;  // the records' range (clamped), the run's range
     uint64_t *res = c->d_counters.as<uint64_t>() + 8;
-    // events: the run's span and the CRC pass always (bench.py's roofline);
-    // between the other phases only with phase timing on (each event between
-    // two kernels costs ~6 us of the run)
+    // events: the CRC pass always (bench.py's roofline); the run's span and
+    // the other phases only with phase timing on (each event between two
+    // kernels costs ~5-6 us of the run, kernel trace profiles/r5a), so without
+    // it ms_phase holds the CRC pass alone (gck_stats.ms_kernel documents it)
     const bool ph = c->phase_timing;
-    // (without phase timing only the CRC pass is bracketed: an event between
-    // two kernels costs ~5-6 us of the run, kernel trace profiles/r5a)
     if (ph) GCK_HIP(hipEventRecord(c->ev[PH_BOUNDARY], m));
     // six launches: speculation (+ the run's zeroing), walk (+ validation
     // round 0), scan (+ the later rounds when needed, the bookkeeping),

@@ -173,8 +173,9 @@ typedef struct gck_stats {
     uint64_t n_overflow;    /* chunks whose records exceeded chunk_cap (re-walked)    */
     double ms_total;        /* last gck_ctx_run wall time (host clock)                */
     double ms_kernel[12];   /* per-phase device time (HIP events), see gck_phase_name; */
-                            /* the device path times boundary..records as one phase  */
-                            /* (under "boundary") unless gck_ctx_phase_timing is on  */
+                            /* a device-path run (no host round trip) times only the */
+                            /* CRC pass unless gck_ctx_phase_timing is on (the other */
+                            /* phases and "pipeline" are 0); a host-path run all     */
     uint32_t device_path;   /* 1: the last run had no host round trip (record table sized by an earlier run) */
     uint32_t n_reruns;      /* device-only runs redone on the host path (capacity / unsettled speculation)  */
     /* the last run's outcome, as gck_result reports it (no records copied):   */

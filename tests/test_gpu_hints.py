@@ -159,8 +159,14 @@ def test_hints_malformed(g, orc):
         "index": h[:len(h) - 32 - 16 * ((n + B - 1) // B) + 16] + (1).to_bytes(8, "little")
                  + h[len(h) - 32 - 16 * ((n + B - 1) // B) + 24:],
     }
+    # a hint file with no entries whose tail claims data-file bytes (they would
+    # only feed the carried lastOffset, checked by nothing)
+    empty_tail = (0).to_bytes(8, "little") * 2 + (100).to_bytes(8, "little") + h[-8:]
+    cases["data bytes without entries"] = empty_tail
     good, _ = g.replay_hints([np.frombuffer(h, np.uint8)], [False])
     assert len(good) == n
+    ok_empty, _ = g.replay_hints([np.frombuffer((0).to_bytes(24, "little") + h[-8:], np.uint8)], [False])
+    assert len(ok_empty) == 0
     for what, b in cases.items():
         with pytest.raises(g._lib.GckError):
             g.replay_hints([np.frombuffer(b, np.uint8)], [False])
