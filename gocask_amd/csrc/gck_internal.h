@@ -135,6 +135,7 @@ struct Ctx {
     // merged headers / keys of the entries this rank owns
     DBuf d_kpart, d_kcrank, d_kbrank, d_kpsum, d_kptot;  // pack: partition, in-tile ranks, tile sums
     DBuf d_mkoff, d_mtab, d_mlive, d_msrc, d_mhdr, d_mkeys;  // merge
+    DBuf d_mout;                                             // its gck_rec array (merged_out)
     uint32_t kd_nparts = 0;                               // of the last gck_kd_pack_sizes
     uint64_t kd_packed = 0;                               // entries it partitioned
     uint64_t kd_tot[128] = {};                            // its per-partition counts, key bytes
@@ -239,6 +240,11 @@ int pool_take(const gck_opts *o, gck_ctx **out);
 void pool_give(const gck_opts *o, gck_ctx *c);
 // the last run's key bytes back to back into a new pinned host buffer (replay.hip)
 int ctx_gather_keys(Ctx *c, void **host, uint64_t *len);
+// the last gck_kd_merge's live entries as a gck_rec array and (keys non-null)
+// their key bytes back to back, shaped on the device: the entry count and key
+// bytes first, then the copies into host memory of those sizes (replay.hip)
+int merged_out_sizes(Ctx *c, bool want_keys, uint64_t *n, uint64_t *key_bytes);
+int merged_out(Ctx *c, gck_rec *h, uint8_t *keys, uint64_t key_bytes);
 // stats every path (GCK_EIO when one fails); the paths must outlive the call
 int open_srcs(const gck_path *files, uint32_t nfiles, std::vector<Src> &out);
 void close_srcs(std::vector<Src> &v);

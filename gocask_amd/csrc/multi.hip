@@ -372,32 +372,30 @@ static int exchange_merge(const std::vector<SrcRef> &srcs, const std::vector<int
     uint64_t tot = 0;
     for (uint64_t v : n_live) tot += v;
     *tot_out = tot;
+    // the output in owner order, each owner's part shaped on its device
+    // (records, unpadded keys) and copied straight into the result arrays
     gck_rec *h = nullptr;
+    std::vector<uint64_t> on(ndev, 0), okb(ndev, 0);
+    uint64_t kb_tot = 0;
+    for (uint32_t p = 0; p < ndev && !rc && h_out; ++p) {
+        rc = merged_out_sizes(&mctx[p]->c, want_keys, &on[p], &okb[p]);
+        kb_tot += okb[p];
+    }
     if (!rc && tot && h_out) {
-        h = static_cast<gck_rec *>(res_alloc(tot * sizeof(gck_rec), false));  // filled by the host below
+        h = static_cast<gck_rec *>(res_alloc(tot * sizeof(gck_rec), false));
         if (!h) rc = GCK_ENOMEM;
     }
-    uint64_t at = 0;
-    std::vector<uint8_t> kblob;  // GCK_OPT_KEYS: the entries' key bytes in output order
-    for (uint32_t p = 0; p < ndev && !rc && h_out; ++p) {
-        uint64_t n = 0, nk = 0;
-        if ((rc = gck_kd_fetch_merged(mctx[p], nullptr, 0, nullptr, 0, &n, &nk))) break;
-        if (!n) continue;
-        std::vector<gck_kd_entry> ents(n);
-        std::vector<uint8_t> keys(nk + 1);
-        if ((rc = gck_kd_fetch_merged(mctx[p], ents.data(), n, keys.data(), nk + 1, &n, &nk))) break;
-        for (uint64_t i = 0; i < n; ++i) {
-            h[at + i] = ents[i].rec;
-            if (want_keys) kblob.insert(kblob.end(), keys.begin() + (ptrdiff_t)ents[i].key_off,
-                                        keys.begin() + (ptrdiff_t)(ents[i].key_off + ents[i].key_len));
-        }
-        at += n;
-    }
     if (!rc && want_keys && h_out) {
-        out->keys = static_cast<uint8_t *>(res_alloc(kblob.size(), false));
+        out->keys = static_cast<uint8_t *>(res_alloc(kb_tot, false));
         if (!out->keys) rc = GCK_ENOMEM;
-        else if (!kblob.empty()) memcpy(out->keys, kblob.data(), kblob.size());
-        out->keys_len = kblob.size();
+        out->keys_len = kb_tot;
+    }
+    uint64_t at = 0, kat = 0;
+    for (uint32_t p = 0; p < ndev && !rc && h_out; ++p) {
+        if (at + on[p] > tot) rc = GCK_EINVAL;  // (the merge's own count: cannot differ)
+        else rc = merged_out(&mctx[p]->c, h + at, want_keys ? out->keys + kat : nullptr, okb[p]);
+        at += on[p];
+        kat += okb[p];
     }
     if (ph_ms) ph_ms[2] = ms_since(t_fe);
     free_recv();

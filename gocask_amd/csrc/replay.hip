@@ -1025,6 +1025,53 @@ __global__ __launch_bounds__(64) void k_scan_keys(const uint2 *__restrict__ rec_
     for (uint32_t k = lane; k < nb + 1; k += 64) lb[k] = 0;  // lb and both tickets
 }
 
+// The same offsets for the entries of a keydir merge (gck_kd_merge's d_mhdr):
+// the key bytes of entries [0, n) back to back, the GCK_OPT_KEYS blob of a
+// live or multi replay (merged_out).
+__global__ __launch_bounds__(64) void k_mo_scan(const gck_kd_entry *__restrict__ E, uint64_t n,
+                                                uint64_t *__restrict__ koff, uint64_t *lb) {
+    const uint32_t lane = threadIdx.x, nb = gridDim.x;
+    uint32_t *tickets = reinterpret_cast<uint32_t *>(lb + nb);
+    const uint32_t b = lb_ticket(tickets);
+    const uint64_t i0 = (uint64_t)b * kScanBlock + lane * 64;
+    uint32_t v[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = i0 + k < n ? E[i0 + k].key_len : 0u;
+    uint64_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) tot += v[k];
+    const uint64_t inc = wave_incl_sum64(tot);
+    const uint64_t btot = lane63(inc);
+    const uint64_t excl = lookback_excl(lb, b, btot);
+    uint64_t run = excl + inc - tot;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+        if (i0 + k < n) koff[i0 + k] = run;
+        run += v[k];
+    }
+    if (b == nb - 1 && lane == 0) koff[n] = excl + btot;
+    if (!lb_last_done(tickets, nb)) return;
+    for (uint32_t k = lane; k < nb + 1; k += 64) lb[k] = 0;  // lb and both tickets
+}
+// recs[i] = entry i's record; with keys, its key bytes (K + key_off, zero
+// padded to 8 B) at keys + koff[i], unpadded
+__global__ void k_mo_out(const gck_kd_entry *__restrict__ E, const uint8_t *__restrict__ K,
+                         const uint64_t *__restrict__ koff, uint64_t n, gck_rec *__restrict__ recs,
+                         uint8_t *__restrict__ keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        recs[i] = E[i].rec;
+        if (!keys) continue;
+        const uint32_t len = E[i].key_len;
+        const uint8_t *src = K + E[i].key_off;
+        uint8_t *dst = keys + koff[i];
+        uint32_t j = 0;
+        if ((reinterpret_cast<uintptr_t>(dst) & 3) == 0)  // (src is 8-byte aligned)
+            for (; j + 4 <= len; j += 4)
+                *reinterpret_cast<uint32_t *>(dst + j) = *reinterpret_cast<const uint32_t *>(src + j);
+        for (; j < len; ++j) dst[j] = src[j];
+    }
+}
+
 // The key bytes of records [0, n) back to back (koff from k_scan_keys): a lane
 // per record, dwords where source and destination allow, else bytes.
 __global__ void k_gather_keys(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ rec_off,
@@ -2355,7 +2402,7 @@ static void ctx_free(Ctx *c) {
                    &c->d_slice, &c->d_nib, &c->d_xinv, &c->d_xa, &c->d_xb, &c->d_zrow,
                    &c->d_freset, &c->d_gbase, &c->d_queue, &c->d_khash, &c->d_ktab, &c->d_kdstat, &c->d_live, &c->d_ktile,
                    &c->d_kdout, &c->d_kdidx, &c->d_kpart, &c->d_kcrank, &c->d_kbrank, &c->d_kpsum, &c->d_kptot,
-                   &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys,
+                   &c->d_mkoff, &c->d_mtab, &c->d_mlive, &c->d_msrc, &c->d_mhdr, &c->d_mkeys, &c->d_mout,
                    &c->d_gkeys, &c->d_gkoff, &c->d_gstat, &c->d_gitem, &c->d_gvsize, &c->d_gexp, &c->d_gcrc,
                    &c->d_gvoff, &c->d_gvals, &c->d_gscan, &c->d_cpos, &c->d_chpos, &c->d_cbsum, &c->d_cfstart, &c->d_cnf,
                    &c->d_cdata, &c->d_chint, &c->d_cfoot, &c->d_cjmp, &c->d_con, &c->d_klb, &c->d_koff, &c->d_keyblob};
@@ -3207,6 +3254,46 @@ static int gather_keys(Ctx *c, void **host, uint64_t *len) {
     return GCK_OK;
 }
 
+// The live entries of the context's last gck_kd_merge shaped on the device as
+// the host wants them (gck_rec array; with want_keys the keys back to back,
+// unpadded) -- mo_sizes first (the key bytes), then mo_out into
+// host memory.  (The host had copied the 64-byte entries and padded keys out
+// and rebuilt both arrays entry by entry: ~0.25 s of a C3 live Open,
+// profiles/r6n.)
+static int mo_sizes(Ctx *c, bool want_keys, uint64_t *n, uint64_t *key_bytes) {
+    *n = c->n_merged;
+    *key_bytes = 0;
+    if (!c->n_merged || !want_keys) return GCK_OK;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const uint64_t m = c->n_merged;
+    const uint32_t nb = std::max<uint32_t>(1, (uint32_t)((m + kScanBlock - 1) / kScanBlock));
+    const size_t had = c->d_klb.cap;
+    int rc;
+    if ((rc = c->d_klb.ensure((nb + 2) * 8ull)) || (rc = c->d_koff.ensure((m + 1) * 8))) return rc;
+    if (c->d_klb.cap != had) GCK_HIP(hipMemsetAsync(c->d_klb.p, 0, c->d_klb.cap, s));  // then self-cleaning
+    k_mo_scan<<<nb, 64, 0, s>>>(c->d_mhdr.as<gck_kd_entry>(), m, c->d_koff.as<uint64_t>(), c->d_klb.as<uint64_t>());
+    GCK_HIP(hipMemcpyAsync(key_bytes, c->d_koff.as<uint64_t>() + m, 8, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    return GCK_OK;
+}
+static int mo_out(Ctx *c, gck_rec *h, uint8_t *keys, uint64_t key_bytes) {
+    const uint64_t m = c->n_merged;
+    if (!m) return GCK_OK;
+    GCK_HIP(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    if ((rc = c->d_mout.ensure(m * sizeof(gck_rec))) || (keys && (rc = c->d_keyblob.ensure(key_bytes ? key_bytes : 1))))
+        return rc;
+    k_mo_out<<<(uint32_t)c->n_cu * 4, 256, 0, s>>>(c->d_mhdr.as<gck_kd_entry>(), c->d_mkeys.as<uint8_t>(),
+                                                   c->d_koff.as<uint64_t>(), m, c->d_mout.as<gck_rec>(),
+                                                   keys ? c->d_keyblob.as<uint8_t>() : nullptr);
+    GCK_HIP(hipMemcpyAsync(h, c->d_mout.p, m * sizeof(gck_rec), hipMemcpyDeviceToHost, s));
+    if (keys && key_bytes) GCK_HIP(hipMemcpyAsync(keys, c->d_keyblob.p, key_bytes, hipMemcpyDeviceToHost, s));
+    GCK_HIP(hipStreamSynchronize(s));
+    return GCK_OK;
+}
+
 // sink: gck_replay_multi's hook (GroupSink, gck_internal.h): each group's
 // context is handed to it after the group has replayed, and no tuples or keys
 // are delivered (out carries the outcome only).
@@ -3248,6 +3335,7 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     // ring size R: every group when the bytes fit the budget
     uint64_t budget = budget_opt;
     if (!budget && (rc0 = auto_budget(opts, &budget))) return rc0;
+    const auto t_budget = std::chrono::steady_clock::now();  // (the process's first Open: HIP's initialisation)
     // a sink (gck_replay_multi, GCK_OPT_LIVE) keeps each group's packed
     // keydir on the device until the exchange: an eighth of the budget is
     // left for those (C3: packs are ~1 % of the data bytes; a database of
@@ -3304,7 +3392,17 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     // contexts are created
     int pre_rc = GCK_OK;
     std::thread pre([&] { pre_rc = stage_prealloc(opts ? opts->device : 0, stage_buffers_wanted()); });
-    for (uint32_t k = 0; k < R && !rc; ++k) rc = pool_take_(opts, &cs[k]);
+    // the contexts on threads of their own: a fresh process's first ones
+    // create the device's hardware queues and load the code objects
+    {
+        std::vector<int> trc(R, GCK_OK);
+        std::vector<std::thread> th;
+        for (uint32_t k = 1; k < R; ++k) th.emplace_back([&, k] { trc[k] = pool_take_(opts, &cs[k]); });
+        trc[0] = pool_take_(opts, &cs[0]);
+        for (auto &t : th) t.join();
+        for (uint32_t k = 0; k < R && !rc; ++k) rc = trc[k];
+    }
+    const auto t_taken = std::chrono::steady_clock::now();
     pre.join();
     if (!rc) rc = pre_rc == GCK_ENOMEM ? GCK_OK : pre_rc;  // (the copier retries the allocation)
     if (rc) {
@@ -3339,7 +3437,11 @@ static int replay_grouped(const Src *files, uint32_t nfiles, const gck_opts *opt
     const bool trace = getenv("GCK_REPLAY_TRACE") != nullptr;
     const auto t_begin = std::chrono::steady_clock::now();
     if (trace)
-        fprintf(stderr, "[gck_replay] %u contexts ready at %.2f ms, copier started at %.2f ms after the call\n", R,
+        fprintf(stderr,
+                "[gck_replay] budget (HIP up) at %.2f ms, %u contexts taken at %.2f ms, staging ready (contexts ready) at "
+                "%.2f ms, copier started at %.2f ms after the call\n",
+                std::chrono::duration<double, std::milli>(t_budget - t_call).count(), R,
+                std::chrono::duration<double, std::milli>(t_taken - t_call).count(),
                 std::chrono::duration<double, std::milli>(t_ctx - t_call).count(),
                 std::chrono::duration<double, std::milli>(t_begin - t_call).count());
     hipEvent_t tev0 = nullptr;
@@ -3676,6 +3778,10 @@ int replay_groups_to(const Src *files, uint32_t nfiles, const gck_opts *opts, Gr
 int pool_take(const gck_opts *o, gck_ctx **out) { return pool_take_(o, out); }
 void pool_give(const gck_opts *o, gck_ctx *c) { pool_give_(o, c); }
 int ctx_gather_keys(Ctx *c, void **host, uint64_t *len) { return gather_keys(c, host, len); }
+int merged_out_sizes(Ctx *c, bool want_keys, uint64_t *n, uint64_t *key_bytes) {
+    return mo_sizes(c, want_keys, n, key_bytes);
+}
+int merged_out(Ctx *c, gck_rec *h, uint8_t *keys, uint64_t key_bytes) { return mo_out(c, h, keys, key_bytes); }
 }  // namespace gck
 
 extern "C" {

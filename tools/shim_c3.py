@@ -39,7 +39,8 @@ try:
     shim = os.path.join(ROOT, "tests", "shim", "build", "shim_test")
     out = []
     modes = [dict(SHIM_PATHS="1"), dict(SHIM_PIN="0"), dict(SHIM_PIN="1"), dict(SHIM_PIN="1", SHIM_MULTI="1"),
-             dict(SHIM_PATHS="1", SHIM_MULTI="1"), dict(SHIM_PATHS="1", SHIM_LIVE="1")]
+             dict(SHIM_PATHS="1", SHIM_MULTI="1"), dict(SHIM_PATHS="1", SHIM_LIVE="1"),
+             dict(SHIM_PATHS="1", SHIM_LIVE="1", GCK_STAGE_HOSTMALLOC="1")]  # (6: staging by hipHostMalloc, an A/B)
     if len(sys.argv) > 2:
         modes = modes[:int(sys.argv[2])]
     if os.environ.get("SHIM_MODES"):  # e.g. "0 4": by path, single and multi
@@ -50,7 +51,7 @@ try:
         modes = [dict(m, GCK_COPY_THREADS=t) for t in threads for m in modes if m.get("SHIM_PIN") != "1"]
     # SHIM_AB_DIRS="dir1 dir2": each mode with the libgocask_hip.so of each directory, interleaved
     libdirs = os.environ.get("SHIM_AB_DIRS", "").split() or [None]
-    runs = [(m, r, ld) for m in modes for r in range(reps) for ld in libdirs]
+    runs = [(m, r, ld) for r in range(reps) for m in modes for ld in libdirs]  # (modes interleaved)
     for mode, r, ld in runs:
         if True:
             env = dict(os.environ, SHIM_TIME="1", **mode)
@@ -62,6 +63,7 @@ try:
             row = json.loads(p.stdout.strip().splitlines()[-1])
             row["rep"] = r
             row["libdir"] = ld
+            row["stage_hostmalloc"] = "GCK_STAGE_HOSTMALLOC" in mode
             row["copy_threads"] = mode.get("GCK_COPY_THREADS", os.environ.get("GCK_COPY_THREADS", "default"))
             tr = [l for l in p.stderr.splitlines() if l.startswith(("gck_replay", "[gck_replay"))]
             if tr:  # GCK_REPLAY_TRACE=1: the library's phase marks
