@@ -568,13 +568,21 @@ def main():
     stream_gbs = rows_gbs = None
     if rank == 0:
         _, stream_gbs = ctx.stream_read_ceiling(5)
-        # the stream ceiling in k_crc_rows' own geometry (a 1024-thread
-        # workgroup per CU with its 160 KiB of LDS, a row in flight per
-        # wavefront, whole 64-row blocks), statically assigned, no compute:
-        # the fastest stream of the round-6 probes (tools/stream_xp.py)
+        # the balanced stream ceiling over k_crc_rows' rows (its loads, whole
+        # 64-row blocks, half static and half from per-XCD queues, no
+        # compute; core.stream_rows_ceiling), with the spread of its
+        # wavefronts' end times from their clock stamps
+        import numpy as np
+        rows_end = None
         try:
-            _, rows_gbs = ctx.stream_rows_ceiling(5)
-        except AttributeError:  # (an older build's diag library, in an A/B: no such probe)
+            _, rows_gbs = ctx.stream_rows_ceiling(5, stamp=True)
+            stamps, _ = ctx.clock_stamps()
+            w = 4 * torch.cuda.get_device_properties(0).multi_processor_count
+            s = stamps[:w].astype(np.float64)
+            ok = (s[:, 1] > 0) & (s[:, 3] > s[:, 1])
+            end = (s[ok, 3] - s[ok, 1].min()) / 100.0  # us (real time at 100 MHz)
+            rows_end = [round(float(np.median(end)), 1), round(float(end.max()), 1)] if ok.any() else None
+        except (AttributeError, RuntimeError):  # (an older build's diag library, in an A/B: no such probe)
             rows_gbs = None
     if rank == 0:
         ms_step = elapsed / args.steps * 1e3
@@ -629,10 +637,12 @@ def main():
                 "frac_of_stream_read": round(achieved / stream_gbs, 4),
                 "rows_ceiling_gbs": round(rows_gbs, 1) if rows_gbs else None,
                 "frac_of_rows_ceiling": round(achieved / rows_gbs, 4) if rows_gbs else None,
+                "rows_ceiling_wave_end_us": rows_end,
                 "ceilings_note": "stream_read: a static grid-stride non-temporal read of the arena; rows: the same "
-                                 "bytes in k_crc_rows' geometry (16 wavefronts per CU, a 4 KiB row in flight each, "
-                                 "64-row blocks) statically assigned, no compute -- the fastest stream measured "
-                                 "(both right after the timed steps, HIP events)",
+                                 "bytes with k_crc_rows' loads in 64-row blocks, half static and the rest from one "
+                                 "queue per XCD, 4 wavefronts per CU with 3 rows in flight, no compute -- the fastest "
+                                 "stream measured whose wavefronts end together (wave_end_us: median and last "
+                                 "wavefront's end from their clock stamps); both right after the timed steps, HIP events",
             },
             "phase_ms": {k: round(v / n_phase, 4) for k, v in phases_sum.items()},
         }

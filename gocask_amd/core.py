@@ -718,22 +718,28 @@ class ReplayContext:
 
     def stream_xp(self, pf=1, blocks=True, threads=1024, lds_kib=160, wg_per_cu=1, iters=10, stamp=False):
         """Stream probe (libgocask_diag.so gck_diag_stream_xp): k_crc_rows' row
-        loads with pf rows in flight per wavefront and no compute, 64-row
-        blocks per wavefront (static: block k W + w) or rows strided over the
-        wavefronts; occupancy from the workgroup size, its LDS and workgroups
-        per CU.  (ms per pass, GB/s); stamp: see clock_stamps()."""
+        loads with pf rows in flight per wavefront and no compute; blocks 0:
+        rows strided over the wavefronts, 1: static 64-row blocks (block
+        k W + w), 2: every block from an atomic queue, 3: k_crc_rows' split
+        (half the full rounds static, the rest queued); occupancy from the
+        workgroup size, its LDS and workgroups per CU.  (ms per pass, GB/s);
+        stamp: see clock_stamps()."""
         ms = ctypes.c_double()
         gbs = ctypes.c_double()
-        check(_lib.load_diag().gck_diag_stream_xp(self._h, pf, int(bool(blocks)), threads, lds_kib, wg_per_cu, iters,
+        check(_lib.load_diag().gck_diag_stream_xp(self._h, pf, int(blocks), threads, lds_kib, wg_per_cu, iters,
                                                   int(bool(stamp)), ctypes.byref(ms), ctypes.byref(gbs)))
         return ms.value, gbs.value
 
     def stream_rows_ceiling(self, iters=10, stamp=False):
-        """The stream ceiling in k_crc_rows' own geometry: one 1024-thread
-        workgroup per CU holding 160 KiB of LDS, a wavefront per 4 KiB row
-        with the next row in flight, 64-row blocks assigned statically, no
-        compute (the fastest of the round-6 probes, tools/stream_xp.py)."""
-        return self.stream_xp(1, True, 1024, 160, 1, iters, stamp)
+        """The balanced stream ceiling over k_crc_rows' rows: its load pattern
+        (a wavefront per 4 KiB row, 16 B per lane, non-temporal) in whole
+        64-row blocks, half of them static and the rest from one queue per
+        XCD, 4 wavefronts per CU with 3 rows in flight each, no compute.  Of
+        the round-6 probes (tools/stream_xp.py, profiles/r6r) the fastest
+        whose wavefronts end together (4.83-4.84 ms for C3, the last wave
+        within 0.03 ms of the median; static blocks stream in 4.78-4.90 ms
+        but their median wave ends 0.2-1.3 ms before the last)."""
+        return self.stream_xp(3, 6, 256, 160, 1, iters, stamp)
 
     @staticmethod
     def clock_stamps():

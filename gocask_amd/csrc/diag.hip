@@ -195,20 +195,65 @@ __global__ __launch_bounds__(1024) void k_stream_blocks(const uint8_t *__restric
 
 // Stream probes for the bytes-in-flight question (round 6): k_crc_rows' row
 // loads (lane p + 16 b reads the 16 B at 1024 k + 64 p + 16 b, non-temporal
-// buffer loads) with PF rows in flight per wavefront, no compute.  BLOCKS: a
-// wavefront streams whole 64-row blocks (block k W + w, static); otherwise
-// rows are strided over the wavefronts (row k W + w).  Occupancy is set by
-// the workgroup size and the dynamic LDS the launch asks for.
-template <int PF, bool BLOCKS>
-__global__ void k_stream_xp(const uint8_t *__restrict__ arena, uint64_t n_rows, uint32_t *sink, int stamp) {
+// buffer loads) with PF rows in flight per wavefront, no compute.  MODE 0:
+// rows strided over the wavefronts (row k W + w); otherwise whole 64-row
+// blocks: 1 static (block k W + w), 2 all from an atomic queue (each claimed
+// as the block before starts), 3 k_crc_rows' split (the first half of the
+// full rounds static, the rest from the queue), 4 static with the
+// wavefronts of a round scattered over its blocks (block k W + (w * odd mod
+// W), W a power of two: a CU's wavefronts no longer read neighbouring
+// blocks), 5 static with a dummy queue claim per block (the atomics of
+// mode 2 without their order); 6 / 7: modes 3 / 2 with one queue per XCD
+// (queue j hands out the queued blocks j, j + 8, ...; a wavefront claims from
+// its XCD's queue and moves to the next queue when that one runs dry), the
+// eight counters 256 B apart.  Occupancy is set by the
+// workgroup size and the dynamic LDS the launch asks for.
+template <int PF, int MODE>
+__global__ void k_stream_xp(const uint8_t *__restrict__ arena, uint64_t n_rows, uint32_t *sink, int stamp,
+                            uint32_t *queue) {
     extern __shared__ uint32_t dyn_lds[];
     const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     const uint32_t lane = threadIdx.x & 63, s_rel = 64 * (lane & 15) + 16 * (lane >> 4);
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x / 64);
     const uint64_t w = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)));
+    const uint64_t n_blocks = (n_rows + 63) / 64;
+    const uint64_t n_static = MODE == 1 || MODE == 4 || MODE == 5 ? ~0ull : MODE == 3 || MODE == 6 ? n_blocks / W / 2 : 0;
+    uint32_t qj = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u, q_tries = 0;  // (HW_REG_XCC_ID)
+    uint64_t st_k = 0;
+    const uint64_t ws = MODE == 4 ? (w * 0x9E3779B1ull) & (W - 1) : w;
+    auto grab = [&]() -> uint64_t {  // the wavefront's next block
+        if (st_k < n_static) {
+            if (MODE == 5) {
+                uint32_t v = 0;
+                if (lane == 0) v = atomicAdd(queue, 1u);
+                if (__builtin_amdgcn_readfirstlane((int)v) == -1) return n_blocks;  // (never: keeps the atomic)
+            }
+            return (st_k++) * W + ws;
+        }
+        if (MODE == 6 || MODE == 7) {
+            for (;;) {
+                uint32_t v = 0;
+                if (lane == 0) v = atomicAdd(queue + 64 * qj, 1u);
+                const uint64_t b = n_static * W + 8ull * (uint32_t)__builtin_amdgcn_readfirstlane((int)v) + qj;
+                if (b < n_blocks || q_tries == 7) return b < n_blocks ? b : n_blocks;
+                ++q_tries;
+                qj = (qj + 1) & 7u;
+            }
+        }
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(queue, 1u);
+        return n_static * W + (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+    };
+    uint64_t bq[2] = {0, 0};  // the blocks of sequence positions 64 j (j even, odd)
+    if (MODE != 0) {
+        bq[0] = grab();
+        bq[1] = grab();
+    }
     auto row_of = [&](uint64_t k) -> uint64_t {  // the wavefront's k-th row
-        return BLOCKS ? ((k / 64) * W + w) * 64 + (k % 64) : k * W + w;
+        if (MODE == 0) return k * W + w;
+        const uint64_t b = bq[(k / 64) & 1];
+        return b < n_blocks ? b * 64 + (k % 64) : n_rows;
     };
     auto issue = [&](uint64_t row, v4u (&v)[4]) {
         const uint32_t r = (uint32_t)min(row, n_rows - 1);
@@ -229,6 +274,9 @@ __global__ void k_stream_xp(const uint8_t *__restrict__ arena, uint64_t n_rows, 
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) acc ^= B[u][j].x ^ B[u][j].y ^ B[u][j].z ^ B[u][j].w;
+                // a block starts: claim the one after it (its rows are issued
+                // PF rows before they are read)
+                if (MODE != 0 && (k + u + 1) % 64 == 0) bq[((k + u + 1) / 64 + 1) & 1] = grab();
                 if (row_of(k + u + 1) >= n_rows) goto done;
             }
         }
@@ -467,7 +515,7 @@ extern "C" int gck_diag_stream_blocks(gck_ctx *ctx, int iters, uint32_t static_e
 // lds_kib of dynamic LDS each, `wg_per_cu` workgroups per CU in the grid.
 extern "C" int gck_diag_stream_xp(gck_ctx *ctx, int pf, int blocks, int threads, int lds_kib, int wg_per_cu,
                                   int iters, int stamp, double *ms_per_iter, double *gbs) {
-    if (!ctx || iters <= 0 || pf < 1 || pf > 3 || threads < 64 || threads > 1024 || threads % 64 || lds_kib < 0 ||
+    if (!ctx || iters <= 0 || pf < 1 || pf > 3 || blocks < 0 || blocks > 7 || threads < 64 || threads > 1024 || threads % 64 || lds_kib < 0 ||
         lds_kib > 160 || wg_per_cu < 1)
         return GCK_EINVAL;
     Ctx *c = &ctx->c;
@@ -477,22 +525,27 @@ extern "C" int gck_diag_stream_xp(gck_ctx *ctx, int pf, int blocks, int threads,
     const size_t lds = std::max<size_t>((size_t)lds_kib << 10, threads * 4);
     const uint32_t grid = (uint32_t)(c->n_cu * wg_per_cu);
     int st = 0;  // the last timed launch stamps its wavefronts
+    static uint32_t *queue = nullptr;  // 8 counters 256 B apart (zeroed before every launch)
+    if (!queue) GCK_HIP(hipMalloc(&queue, 4096));
     auto launch = [&]() {
-#define GCK_XP_L(P, B) k_stream_xp<P, B><<<grid, threads, lds, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink, st)
-        if (blocks) {
-            if (pf == 1) GCK_XP_L(1, true); else if (pf == 2) GCK_XP_L(2, true); else GCK_XP_L(3, true);
-        } else {
-            if (pf == 1) GCK_XP_L(1, false); else if (pf == 2) GCK_XP_L(2, false); else GCK_XP_L(3, false);
-        }
+        (void)hipMemsetAsync(queue, 0, 4096, c->stream);
+#define GCK_XP_L(P, M) k_stream_xp<P, M><<<grid, threads, lds, c->stream>>>(c->arena.as<uint8_t>(), c->n_rows, sink, st, queue)
+#define GCK_XP_M(M) if (pf == 1) GCK_XP_L(1, M); else if (pf == 2) GCK_XP_L(2, M); else GCK_XP_L(3, M)
+        if (blocks == 0) { GCK_XP_M(0); } else if (blocks == 1) { GCK_XP_M(1); } else if (blocks == 2) { GCK_XP_M(2); } else if (blocks == 3) { GCK_XP_M(3); } else if (blocks == 4) { GCK_XP_M(4); } else if (blocks == 5) { GCK_XP_M(5); } else if (blocks == 6) { GCK_XP_M(6); } else { GCK_XP_M(7); }
+#undef GCK_XP_M
 #undef GCK_XP_L
     };
     // (dynamic LDS above 64 KiB needs the attribute)
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<1, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<2, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<3, true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<1, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<2, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
-    GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<3, false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10));
+#define GCK_XP_A(P, M) GCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(k_stream_xp<P, M>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 << 10))
+    GCK_XP_A(1, 0); GCK_XP_A(2, 0); GCK_XP_A(3, 0);
+    GCK_XP_A(1, 1); GCK_XP_A(2, 1); GCK_XP_A(3, 1);
+    GCK_XP_A(1, 2); GCK_XP_A(2, 2); GCK_XP_A(3, 2);
+    GCK_XP_A(1, 3); GCK_XP_A(2, 3); GCK_XP_A(3, 3);
+    GCK_XP_A(1, 4); GCK_XP_A(2, 4); GCK_XP_A(3, 4);
+    GCK_XP_A(1, 5); GCK_XP_A(2, 5); GCK_XP_A(3, 5);
+    GCK_XP_A(1, 6); GCK_XP_A(2, 6); GCK_XP_A(3, 6);
+    GCK_XP_A(1, 7); GCK_XP_A(2, 7); GCK_XP_A(3, 7);
+#undef GCK_XP_A
     hipEvent_t a, b;
     GCK_HIP(hipEventCreate(&a));
     GCK_HIP(hipEventCreate(&b));
