@@ -52,7 +52,10 @@ enum : int {
 };
 constexpr int kRounds = 2;             // device validation/fixup rounds
 constexpr int kHops = 4;          // extra headers a speculative start must chain through
-constexpr int kWaves = 16;        // wavefronts per k_crc_rows workgroup
+#ifndef GCK_CRC_WAVES
+#define GCK_CRC_WAVES 16
+#endif
+constexpr int kWaves = GCK_CRC_WAVES;  // wavefronts per k_crc_rows workgroup (one workgroup per CU: its LDS)
 constexpr uint32_t kNibBase = 32768;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -2636,7 +2639,7 @@ static int launch_crc(Ctx *c, hipStream_t s, uint64_t r0, uint64_t r1, uint64_t 
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nb + kWaves - 1) / kWaves, (uint64_t)c->n_cu);
     uint32_t *queue = c->d_queue.as<uint32_t>() + q;
     if (!queue_zeroed) GCK_HIP(hipMemsetAsync(queue, 0, 4, s));
-    k_crc_rows<<<grid, 1024, 0, s>>>(
+    k_crc_rows<<<grid, kWaves * 64, 0, s>>>(
         c->arena.as<uint8_t>() + r0 * kRow, r1 - r0, c->d_blk_first.as<uint32_t>() + r0 / kBlockRows, cap,
         c->d_slice.as<uint32_t>(), c->d_nib.as<uint32_t>(), c->d_ep.as<uint2>(), c->d_rend.as<uint32_t>() + r0,
         c->d_rend.as<uint32_t>() + c->n_rows, queue, c->d_rec_off.as<uint64_t>(), c->d_rec_kv.as<uint2>(), r0
