@@ -29,7 +29,7 @@ GCK_ENOT_DIR = 9
 F_TOMBSTONE = 1
 F_CRC_OK = 2
 F_HINT = 4  # from a hint file (gck_ctx_replay_hints): value not read
-HINT_BLOCK, HINT_MAGIC, HINT_VERSION = 16, 0x484B4347, 2  # GCK_HINT_*
+HINT_BLOCK, HINT_MAGIC, HINT_VERSION = 16, 0x484B4347, 3  # GCK_HINT_*
 
 REC_DTYPE = np.dtype(
     [

@@ -30,10 +30,10 @@ typedef uint32_t u32x4_a4c __attribute__((ext_vector_type(4), aligned(4)));
 
 constexpr uint32_t kCmpBlock = 1024;  // records per first-level scan block
 constexpr uint64_t kHintHdr = 20;      // hint entry header bytes (GCK_HINT_*)
-constexpr uint64_t kHintTail = 32;
+constexpr uint64_t kHintTail = 32, kHintIdx = 24;  // tail, index entry bytes
 // index + tail bytes of a hint file of n entries
 __host__ __device__ __forceinline__ uint64_t hint_footer(uint64_t n) {
-    return 16 * ((n + GCK_HINT_BLOCK - 1) / GCK_HINT_BLOCK) + kHintTail;
+    return kHintIdx * ((n + GCK_HINT_BLOCK - 1) / GCK_HINT_BLOCK) + kHintTail;
 }
 
 __device__ __forceinline__ uint64_t wave_incl_sum64(uint64_t v) {
@@ -390,39 +390,84 @@ __global__ __launch_bounds__(256) void k_cmp_copy(const uint8_t *__restrict__ ar
 // Hint entries: a lane per record (20 + KeySize bytes each), at hpos[i] plus
 // the index and tail bytes of the files before its own (foot[f]); the lane of
 // every GCK_HINT_BLOCK-th record of a file writes its index entry.
-__global__ void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
+// The integrity word of hint entry t (record kd[t], at data offset qo in its
+// merged file): hint_entry_check over its header words and key.
+__device__ __forceinline__ unsigned long long cmp_entry_check(const uint8_t *__restrict__ arena,
+                                                              const uint64_t *__restrict__ fbase, const gck_rec &q,
+                                                              uint64_t qo) {
+    const uint8_t *kp = arena + fbase[q.file] + q.rec_off + 16;
+    const uint32_t ql = q.key_len;
+    auto kw = [&](uint32_t w) {  // key word w, zero past the key (the arena is padded)
+        const uint8_t *p = kp + 4 * w;
+        const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(p) & 3);
+        const uint32_t *a = reinterpret_cast<const uint32_t *>(p - sh);
+        const uint32_t v = __builtin_amdgcn_alignbyte(a[1], a[0], sh), left = ql - 4 * w;
+        return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
+    };
+    return hint_entry_check(q.ts, ql, q.value_size, (uint32_t)(qo + 16 + ql), q.crc, kw);
+}
+
+__global__ __launch_bounds__(256) void k_cmp_hints(const uint8_t *__restrict__ arena, const uint64_t *__restrict__ fbase,
                             const gck_rec *__restrict__ kd, const uint64_t *__restrict__ pos,
                             const uint64_t *__restrict__ hpos, const uint32_t *__restrict__ fstart,
                             const uint64_t *__restrict__ foot, uint32_t nf, uint64_t n, uint8_t *__restrict__ hints) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const gck_rec r = kd[i];
-    // the merged file of record i: the last k with fstart[k] <= i
-    uint32_t lo = 0, hi = nf - 1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) / 2;
-        if (fstart[mid] <= i) lo = mid; else hi = mid - 1;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = i - lane;  // the wavefront's first record
+    // (every lane stays to the wave-wide prefix below; lanes past n carry 0)
+    unsigned long long c = 0;
+    gck_rec r{};
+    uint32_t lo = 0;
+    uint64_t i0 = 0, fo = 0;
+    if (i < n) {
+        r = kd[i];
+        // the merged file of record i: the last k with fstart[k] <= i
+        uint32_t hi = nf - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (fstart[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        i0 = fstart[lo];
+        fo = pos[i] - pos[i0];  // the record's offset in its merged file
+        uint8_t *d = hints + hpos[i] + foot[lo];
+        const uint8_t *key = arena + fbase[r.file] + r.rec_off + 16;
+        // 16 B pieces at any alignment: the key's last 16 bytes first (a key
+        // under 16 B reaches back into the entry's header, from the record's
+        // header in the arena: written over below), then its whole pieces, then
+        // the header -- one thread's stores land in program order.  (Byte stores:
+        // 370 us for C3's 138 MB of hints, pieces 215 us, profiles/r4zzf.)
+        const uint32_t kl = r.key_len;
+        if (kl & 15) st16u(d + kHintHdr + kl - 16, ld16u(key + kl - 16));
+        for (uint32_t k = 0; k + 16 <= kl; k += 16) st16u(d + kHintHdr + k, ld16u(key + k));
+        st16u(d, make_uint4(r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)));
+        st4u(d + 16, r.crc);
+        c = cmp_entry_check(arena, fbase, r, fo);
     }
-    const uint64_t i0 = fstart[lo], fo = pos[i] - pos[i0];  // the record's offset in its merged file
-    const uint64_t h0 = hpos[i0] + foot[lo];                // the hint file's first byte
-    uint8_t *d = hints + hpos[i] + foot[lo];
-    const uint8_t *key = arena + fbase[r.file] + r.rec_off + 16;
-    // 16 B pieces at any alignment: the key's last 16 bytes first (a key
-    // under 16 B reaches back into the entry's header, from the record's
-    // header in the arena: written over below), then its whole pieces, then
-    // the header -- one thread's stores land in program order.  (Byte stores:
-    // 370 us for C3's 138 MB of hints, pieces 215 us, profiles/r4zzf.)
-    const uint32_t kl = r.key_len;
-    if (kl & 15) st16u(d + kHintHdr + kl - 16, ld16u(key + kl - 16));
-    for (uint32_t k = 0; k + 16 <= kl; k += 16) st16u(d + kHintHdr + k, ld16u(key + k));
-    st16u(d, make_uint4(r.ts, r.key_len, r.value_size, (uint32_t)(fo + 16 + r.key_len)));
-    st4u(d + 16, r.crc);
+    // inclusive prefix XOR of the entries' words over the wavefront: a block
+    // [i, i1) inside the wave is P[i1 - 1] ^ P[i - 1] (files in between cancel)
+    unsigned long long P = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(P, d);
+        if (lane >= (uint32_t)d) P ^= y;
+    }
     const uint64_t j = i - i0;
-    if (j % GCK_HINT_BLOCK == 0) {  // the block's index entry, after the file's entries
+    const bool idx = i < n && j % GCK_HINT_BLOCK == 0;
+    const uint64_t i1 = idx ? min<uint64_t>(i + GCK_HINT_BLOCK, (uint64_t)fstart[lo + 1]) : i + 1;
+    const uint32_t last = (uint32_t)(min<uint64_t>(i1, w0 + 64) - 1 - w0);  // the block's last lane in this wave
+    const unsigned long long P_last = __shfl(P, (int)last), P_before = __shfl(P, (int)(lane ? lane - 1 : 0));
+    if (idx) {
+        // the block's index entry, after the file's entries: its first entry's
+        // hint and data offsets, and the XOR of its entries' integrity words
+        unsigned long long chk = P_last ^ (lane ? P_before : 0ull);
+        for (uint64_t t = w0 + 64; t < i1; ++t) chk ^= cmp_entry_check(arena, fbase, kd[t], pos[t] - pos[i0]);  // (past the wave)
+        const uint64_t h0 = hpos[i0] + foot[lo];  // the hint file's first byte
         const uint64_t ebytes = hpos[fstart[lo + 1]] - hpos[i0];
-        uint8_t *x = hints + h0 + ebytes + 16 * (j / GCK_HINT_BLOCK);
+        uint8_t *x = hints + h0 + ebytes + kHintIdx * (j / GCK_HINT_BLOCK);
         st16u(x, make_uint4((uint32_t)(hpos[i] - hpos[i0]), (uint32_t)((hpos[i] - hpos[i0]) >> 32), (uint32_t)fo,
                             (uint32_t)(fo >> 32)));
+        st4u(x + 16, (uint32_t)chk);
+        st4u(x + 20, (uint32_t)(chk >> 32));
     }
 }
 

@@ -65,6 +65,31 @@ constexpr uint32_t kGbSlots = 2, kGbWords = kGbSlots + 4;
 constexpr uint32_t kQueueCrc = 0, kQueueVerify = 1, kQueueCompact = 2, kQueueSlots = 3;
 
 
+// 64-bit finaliser (splitmix64): the keydir's key hash (kd_common.h) and the
+// hint entries' integrity word
+__device__ __forceinline__ uint64_t mix64d(uint64_t x) {
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+// The integrity word of one hint entry (GCK_HINT_VERSION 3): a mix of its
+// five header words and its key's 4-byte little-endian words k(i) (the last
+// one zero past the key).  Each index entry of a hint file holds the XOR of
+// its block's words; the writer (compact.hip) and the reader (hints.hip)
+// compute it the same way, and oracle.hint_entry_check restates it.
+template <class Words>
+__device__ __forceinline__ uint64_t hint_entry_check(uint32_t ts, uint32_t ks, uint32_t vs, uint32_t vpos,
+                                                     uint32_t crc, const Words &k) {
+    uint64_t h = 0x2545F4914F6CDD1Dull ^ ((uint64_t)ks << 32);
+    h = mix64d(h ^ ts) + 1;
+    h = mix64d(h ^ vs) + 2;
+    h = mix64d(h ^ vpos) + 3;
+    h = mix64d(h ^ crc) + 4;
+    for (uint32_t i = 0; 4 * i < ks; ++i) h = mix64d(h ^ k(i)) + 5 + i;
+    return mix64d(h);
+}
+
 struct Ctx {
     int device = 0;
     hipStream_t stream = nullptr;

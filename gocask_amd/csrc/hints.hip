@@ -34,7 +34,7 @@
 
 namespace gck {
 
-constexpr uint64_t kHintHdrB = 20, kHintTailB = 32;
+constexpr uint64_t kHintHdrB = 20, kHintTailB = 32, kHintIdxB = 24;  // entry header, tail, index entry
 
 typedef uint32_t u32x4h __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -99,9 +99,13 @@ __device__ __forceinline__ void put_entry(const HintFile &F, uint32_t lo, uint64
     rec_file[e] = lo;
 }
 
+// want: the block's integrity word from its index entry, the XOR of its
+// entries' hint_entry_check (a changed key, timestamp, size or CRC byte in a
+// well-formed entry fails it)
 template <class Rd, class Emit>
 __device__ __forceinline__ bool parse_block(const HintFile &F, uint64_t lb, uint64_t hoff, uint64_t doff,
-                                            uint64_t end_h, uint64_t end_d, Rd rd, Emit emit) {
+                                            uint64_t end_h, uint64_t end_d, Rd rd, Emit emit, uint64_t want) {
+    uint64_t chk = 0;
     const uint32_t cnt = (uint32_t)min<uint64_t>(GCK_HINT_BLOCK, F.n - GCK_HINT_BLOCK * lb);
     for (uint32_t j = 0; j < cnt; ++j) {
         if (hoff + kHintHdrB > F.ebytes) return false;  // (a read past the entries is never issued)
@@ -109,11 +113,15 @@ __device__ __forceinline__ bool parse_block(const HintFile &F, uint64_t lb, uint
         // a merged file holds Puts only (KeySize >= 1); ValuePos is the value's
         // offset in the data file mod 2^32 -- the data offset the entries add up to
         if (ks == 0 || hoff + kHintHdrB + ks > F.ebytes || vpos != (uint32_t)(doff + 16 + ks)) return false;
+        chk ^= hint_entry_check(rd(hoff, 0), ks, vs, vpos, rd(hoff, 16), [&](uint32_t q) {
+            const uint32_t v = rd(hoff, (uint32_t)kHintHdrB + 4 * q), left = ks - 4 * q;
+            return left >= 4 ? v : v & ((1u << (8 * left)) - 1u);
+        });
         emit(j, hoff, doff, ks, vs, vpos);
         hoff += kHintHdrB + ks;
         doff += 16ull + ks + vs;
     }
-    return hoff == end_h && doff == end_d;
+    return hoff == end_h && doff == end_d && chk == want;
 }
 
 // k_hint_parse: a wavefront per segment of kHintSeg blocks of one file.  The
@@ -152,12 +160,12 @@ __global__ __launch_bounds__(64) void k_hint_parse(const uint8_t *__restrict__ a
     const bool act = lane < nbs;
     // this block's index entry and where it must end: the next block's entry
     // (the lane above), or past the segment the next segment's first / the tail
-    const uint8_t *ix = h + F.ebytes + 16 * (act ? lb : lb0);
-    const uint64_t hoff = ld8u(ix), doff = ld8u(ix + 8);
+    const uint8_t *ix = h + F.ebytes + kHintIdxB * (act ? lb : lb0);
+    const uint64_t hoff = ld8u(ix), doff = ld8u(ix + 8), want = ld8u(ix + 16);
     uint64_t end_h = __shfl_down(hoff, 1), end_d = __shfl_down(doff, 1);
     if (lane == nbs - 1) {
-        end_h = lb + 1 < nb ? ld8u(ix + 16) : F.ebytes;
-        end_d = lb + 1 < nb ? ld8u(ix + 24) : F.dbytes;
+        end_h = lb + 1 < nb ? ld8u(ix + kHintIdxB) : F.ebytes;
+        end_d = lb + 1 < nb ? ld8u(ix + kHintIdxB + 8) : F.dbytes;
     }
     // the segment's entry bytes [h0, h1) (index values checked before use)
     const uint64_t h0 = __shfl(hoff, 0), h1 = __shfl(end_h, (int)(nbs - 1));
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(64) void k_hint_parse(const uint8_t *__restrict__ a
                              [&](uint32_t j, uint64_t ho, uint64_t dof, uint32_t, uint32_t, uint32_t) {
                                  Eq[eb + j] = (uint32_t)(ho - a0);
                                  Ed[eb + j] = dof;
-                             });
+                             }, want);
         if (__ballot(act && !ok)) {
             if (lane == 0) atomicOr(err, 1u);
             return;
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(64) void k_hint_parse(const uint8_t *__restrict__ a
                              [&](uint32_t j, uint64_t ho, uint64_t dof, uint32_t ks, uint32_t vs, uint32_t vpos) {
                                  put_entry(F, lo, e0 + j, ho, dof, rd(ho, 0), ks, vs, vpos, rd(ho, 16), out, rec_off,
                                            rec_kv, rec_file);
-                             });
+                             }, want);
     }
     if (act && !ok) atomicOr(err, 1u);
 }
@@ -329,7 +337,7 @@ int gck_ctx_replay_hints(gck_ctx *ctx, double *ms) {
         // (a file without entries has no data bytes either: nothing would
         // check them, yet they would feed the carried lastOffset)
         if ((uint32_t)mv != GCK_HINT_MAGIC || (uint32_t)(mv >> 32) != GCK_HINT_VERSION || n > (1ull << 40) ||
-            eb > c->f_len[f] || eb < (kHintHdrB + 1) * n || c->f_len[f] != eb + 16 * nb + kHintTailB ||
+            eb > c->f_len[f] || eb < (kHintHdrB + 1) * n || c->f_len[f] != eb + kHintIdxB * nb + kHintTailB ||
             (n == 0 && db != 0))
             return GCK_EINVAL;
         hf[f] = HintFile{c->f_base[f], eb, db, ents, blks, n, segs, last, 0};

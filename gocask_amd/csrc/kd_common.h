@@ -12,12 +12,6 @@ constexpr int kKdTile = 1024;  // records per compaction tile (one workgroup)
 // tombstone (KeySize 0; core/db.go:151-155).
 __device__ __forceinline__ uint32_t key_len(const uint2 &kv) { return kv.x ? kv.x : kv.y; }  // (KeySize, ValueSize)
 
-__device__ __forceinline__ uint64_t mix64d(uint64_t x) {
-    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-    return x ^ (x >> 31);
-}
-
 // Word i (4 key bytes, little-endian) of a key at arena offset o, read as
 // aligned dwords and funnel-shifted; bytes past the key are masked to zero
 // (the arena is padded, so the word after the key is always readable).

@@ -239,8 +239,11 @@ int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * (format invented here, parity unpinned: the reference has no hint files),
  * little-endian:
  *   entries [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][CRC u32][key bytes]
- *   index   [hint-file offset u64][data-file offset u64] of entries 0, B, 2B, ...
- *           (B = GCK_HINT_BLOCK)
+ *   index   [hint-file offset u64][data-file offset u64][check u64] of entries
+ *           0, B, 2B, ... (B = GCK_HINT_BLOCK); check = the XOR over the
+ *           block's entries of a 64-bit mix of each entry's header words and
+ *           key (gck_internal.h hint_entry_check): a reader refuses a block
+ *           whose entries do not give it
  *   tail    [entries u64][entry bytes u64][data-file bytes u64][GCK_HINT_MAGIC u32]
  *           [GCK_HINT_VERSION u32]
  * (ValuePos = the value's offset in its merged file mod 2^32, as
@@ -252,7 +255,7 @@ int gck_ctx_fetch_keydir(gck_ctx *ctx, gck_rec *dst, uint64_t cap, uint64_t *n);
  * may be NULL).  *ms (optional) = device time. */
 #define GCK_HINT_BLOCK 16u
 #define GCK_HINT_MAGIC 0x484B4347u /* "GCKH" */
-#define GCK_HINT_VERSION 2u
+#define GCK_HINT_VERSION 3u
 int gck_ctx_compact(gck_ctx *ctx, uint64_t max_file_size, uint32_t *n_files, uint64_t *data_bytes,
                     uint64_t *hint_bytes, double *ms);
 int gck_ctx_fetch_compact(gck_ctx *ctx, uint8_t *data, uint64_t *file_sizes, uint8_t *hints, uint64_t *hint_sizes);

@@ -284,7 +284,30 @@ def tombstone(now: int, key: bytes) -> bytes:
     return struct.pack("<IIII", zlib.crc32(key), now & 0xFFFFFFFF, 0, len(key)) + key
 
 
-HINT_MAGIC, HINT_VERSION, HINT_BLOCK = 0x484B4347, 2, 16
+HINT_MAGIC, HINT_VERSION, HINT_BLOCK = 0x484B4347, 3, 16
+_M64 = (1 << 64) - 1
+
+
+def _mix64(x):
+    """splitmix64's finaliser on Python ints (gocask_amd/csrc/gck_internal.h mix64d)."""
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def hint_entry_check(ts, key, value_size, value_pos, crc):
+    """The integrity word of one hint entry (gck_internal.h hint_entry_check,
+    restated): a mix of its header words and its key's 4-byte little-endian
+    words, the last one zero past the key.  Each index entry holds the XOR of
+    its block's words."""
+    ks = len(key)
+    h = 0x2545F4914F6CDD1D ^ (ks << 32)
+    for i, w in enumerate((ts, value_size, value_pos, crc)):
+        h = (_mix64(h ^ w) + i + 1) & _M64
+    padded = key + bytes(-ks % 4)
+    for i in range(0, ks, 4):
+        h = (_mix64(h ^ int.from_bytes(padded[i:i + 4], "little")) + 5 + i // 4) & _M64
+    return _mix64(h)
 
 
 def hint_file(entries, data_bytes):
@@ -293,15 +316,20 @@ def hint_file(entries, data_bytes):
     of one merged data file in record order; little-endian
       entries [Timestamp u32][KeySize u32][ValueSize u32][ValuePos u32][CRC u32] + key
       index   per block of HINT_BLOCK entries: [hint offset u64][data-file offset u64]
-              of the block's first entry
+              of the block's first entry, [check u64] = the XOR of
+              hint_entry_check over the block's entries
       tail    [entries u64][entry bytes u64][data-file bytes u64][magic u32][version u32]
     so a reader finds every block of entries without walking the file, and a
     record's offset in its data file (rec_off) past 4 GiB, where ValuePos wraps."""
     body, index = bytearray(), bytearray()
-    for j, (ts, key, vs, vpos, crc, rec_off) in enumerate(entries):
-        if j % HINT_BLOCK == 0:
-            index += struct.pack("<QQ", len(body), rec_off)
-        body += struct.pack("<IIIII", ts, len(key), vs, vpos, crc) + key
+    for j0 in range(0, len(entries), HINT_BLOCK):
+        blk = entries[j0:j0 + HINT_BLOCK]
+        check = 0
+        for ts, key, vs, vpos, crc, _ in blk:
+            check ^= hint_entry_check(ts, key, vs, vpos, crc)
+        index += struct.pack("<QQQ", len(body), blk[0][5], check)
+        for ts, key, vs, vpos, crc, _ in blk:
+            body += struct.pack("<IIIII", ts, len(key), vs, vpos, crc) + key
     tail = struct.pack("<QQQII", len(entries), len(body), data_bytes, HINT_MAGIC, HINT_VERSION)
     return bytes(body + index + tail)
 
@@ -341,14 +369,19 @@ def parse_hints(h):
     value_size, value_pos, crc, rec_off)]."""
     n, nbytes, dbytes, magic, ver = struct.unpack_from("<QQQII", h, len(h) - 32)
     nb = (n + HINT_BLOCK - 1) // HINT_BLOCK
-    assert magic == HINT_MAGIC and ver == HINT_VERSION and len(h) == nbytes + 16 * nb + 32
+    assert magic == HINT_MAGIC and ver == HINT_VERSION and len(h) == nbytes + 24 * nb + 32
     out, p, d = [], 0, 0
     for j in range(n):
         if j % HINT_BLOCK == 0:
-            assert struct.unpack_from("<QQ", h, nbytes + 16 * (j // HINT_BLOCK)) == (p, d)
+            assert struct.unpack_from("<QQ", h, nbytes + 24 * (j // HINT_BLOCK)) == (p, d)
         ts, kl, vs, vpos, crc = struct.unpack_from("<IIIII", h, p)
         out.append((ts, bytes(h[p + 20:p + 20 + kl]), vs, vpos, crc, d))
         p += 20 + kl
         d += 16 + kl + vs
     assert p == nbytes and d == dbytes
+    for b in range(nb):
+        x = 0
+        for ts, key, vs, vpos, crc, _ in out[b * HINT_BLOCK:(b + 1) * HINT_BLOCK]:
+            x ^= hint_entry_check(ts, key, vs, vpos, crc)
+        assert struct.unpack_from("<Q", h, nbytes + 24 * b + 16)[0] == x
     return out

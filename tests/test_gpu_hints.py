@@ -149,15 +149,22 @@ def test_hints_malformed(g, orc):
     n = int.from_bytes(h[-32:-24], "little")
     B = g._lib.HINT_BLOCK
     assert n > 2 * B + 3  # several blocks, a partial last one
+    T, X = 32, 24  # tail, index entry bytes
+    ix = len(h) - T - X * ((n + B - 1) // B)  # the index
+    first_key = 20  # the first entry's key (after its five header words)
     cases = {
         "truncated": h[:-1],
         "magic": h[:-8] + b"XXXX" + h[-4:],
-        "version": h[:-4] + (3).to_bytes(4, "little"),
-        "entry count": h[:-32] + (n + 1).to_bytes(8, "little") + h[-24:],
+        "version": h[:-4] + (2).to_bytes(4, "little"),
+        "entry count": h[:-T] + (n + 1).to_bytes(8, "little") + h[-T + 8:],
         "key size": h[:4] + (0xFFFF).to_bytes(4, "little") + h[8:],
         "value pos": h[:12] + (int.from_bytes(h[12:16], "little") + 1).to_bytes(4, "little") + h[16:],
-        "index": h[:len(h) - 32 - 16 * ((n + B - 1) // B) + 16] + (1).to_bytes(8, "little")
-                 + h[len(h) - 32 - 16 * ((n + B - 1) // B) + 24:],
+        "index": h[:ix + X] + (1).to_bytes(8, "little") + h[ix + X + 8:],
+        # well-formed entries whose bytes changed: only the tail's check sees them
+        "key byte": h[:first_key] + bytes([h[first_key] ^ 1]) + h[first_key + 1:],
+        "timestamp": bytes([h[0] ^ 0x80]) + h[1:],
+        "crc": h[:16] + bytes([h[16] ^ 1]) + h[17:],
+        "check": h[:ix + X + 16] + bytes([h[ix + X + 16] ^ 1]) + h[ix + X + 17:],
     }
     # a hint file with no entries whose tail claims data-file bytes (they would
     # only feed the carried lastOffset, checked by nothing)

@@ -43,7 +43,7 @@ def test_oracle_compact_roundtrip(orc, name, max_size):
 def test_oracle_hint_format(orc):
     """hint_file's layout (the format gck_replay_hints reads; invented here,
     parity unpinned): entries [Timestamp][KeySize][ValueSize][ValuePos][CRC] +
-    key, an index entry (hint offset, data offset) per HINT_BLOCK entries, a
+    key, an index entry (hint offset, data offset, check) per HINT_BLOCK entries, a
     32-byte tail; parse_hints walks it and checks index and tail; the CRC
     field is the record header's (kdEntry.CRC, core/keydir.go:3-9)."""
     import struct
@@ -59,7 +59,7 @@ def test_oracle_hint_format(orc):
         ents = orc.parse_hints(h)
         n, eb, db, magic, ver = struct.unpack_from("<QQQII", h, len(h) - 32)
         assert (n, db, magic, ver) == (len(ents), len(d), orc.HINT_MAGIC, orc.HINT_VERSION)
-        assert len(h) == eb + 16 * ((n + B - 1) // B) + 32
+        assert len(h) == eb + 24 * ((n + B - 1) // B) + 32
         for ts, key, vs, vpos, crc, rec_off in ents:  # each entry describes its record in the data file
             hcrc, hts, ks, hvs = struct.unpack_from("<IIII", d, rec_off)
             assert (hcrc, hts, ks, hvs) == (crc, ts, len(key), vs)
