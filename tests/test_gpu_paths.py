@@ -92,6 +92,33 @@ def test_paths_files_larger_than_a_staging_chunk(g, orc, tmp_path, monkeypatch):
     _same(got, gst, want, wst)
 
 
+def test_paths_staging_by_hostmalloc(g, orc, tmp_path):
+    # The staging buffers are registered huge-page memory by default and
+    # hipHostMalloc memory when registration fails; GCK_STAGE_HOSTMALLOC (read
+    # once per process) forces the second kind, so a child process replays
+    # with it and the parent compares with the oracle.
+    import subprocess
+    import sys
+
+    wf, reset = _corpus(orc, seed=95, n_files=5, fsize=3 << 20, active=2)
+    want, wst = orc.replay(wf, reset)
+    paths = _write(tmp_path, wf)
+    out = tmp_path / "got.npy"
+    code = ("import sys, json, numpy as np; sys.path.insert(0, sys.argv[1]); import gocask_amd as g; "
+            "got, st = g.replay_paths(json.loads(sys.argv[2]), json.loads(sys.argv[3])); "
+            "np.save(sys.argv[4], got); print(json.dumps({k: int(v) for k, v in st.items() "
+            "if isinstance(v, (int, np.integer))}))")
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GCK_STAGE_HOSTMALLOC="1")
+    p = subprocess.run([sys.executable, "-c", code, root, json.dumps(paths), json.dumps(reset), str(out)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    gst = json.loads(p.stdout.strip().splitlines()[-1])
+    _same(np.load(out), gst, want, wst)
+
+
 def test_paths_startup_error_and_empty_files(g, orc, tmp_path):
     wf, reset = _corpus(orc, seed=95, n_files=6)
     bad = np.frombuffer(orc_mod.entry(1, b"user", b"x" * 10) + orc_mod.entry(2, b"key", b"yy")[:-4], np.uint8)
