@@ -177,3 +177,30 @@ def test_hints_malformed(g, orc):
     for what, b in cases.items():
         with pytest.raises(g._lib.GckError):
             g.replay_hints([np.frombuffer(b, np.uint8)], [False])
+
+
+def test_hints_every_single_byte_flip_refused(g, orc):
+    # Every byte of a version-3 hint file is covered: entry bytes by their
+    # block's integrity word, index entries by the walk (offsets) and the word,
+    # the tail by the size checks.  So one flipped bit anywhere must make
+    # gck_replay_hints refuse the file -- never return different tuples.
+    files = _demo(orc)
+    _, hints = _merge(g, files, [True, False], 1 << 30)
+    h = bytes(hints[0])
+    good, _ = g.replay_hints([np.frombuffer(h, np.uint8)], [False])
+    rng = np.random.default_rng(123)
+    n_idx = (int.from_bytes(h[-32:-24], "little") + 15) // 16
+    ebytes = int.from_bytes(h[-24:-16], "little")
+    # positions: every region (entries, index, tail) plus random ones
+    pos = [0, 4, 8, 12, 16, 20, ebytes - 1, ebytes, ebytes + 8, ebytes + 16, ebytes + 24 * n_idx - 1,
+           len(h) - 32, len(h) - 24, len(h) - 16, len(h) - 8, len(h) - 4, len(h) - 1]
+    pos += [int(x) for x in rng.integers(0, len(h), 60)]
+    for p in pos:
+        bit = 1 << int(rng.integers(0, 8))
+        b = bytearray(h)
+        b[p] ^= bit
+        try:
+            got, _ = g.replay_hints([np.frombuffer(bytes(b), np.uint8)], [False])
+        except g._lib.GckError:
+            continue
+        raise AssertionError(f"flip at {p} (bit {bit}) accepted: {len(got)} vs {len(good)} tuples")
