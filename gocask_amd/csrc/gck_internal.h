@@ -73,20 +73,23 @@ __device__ __forceinline__ uint64_t mix64d(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-// The integrity word of one hint entry (GCK_HINT_VERSION 3): a mix of its
-// five header words and its key's 4-byte little-endian words k(i) (the last
-// one zero past the key).  Each index entry of a hint file holds the XOR of
-// its block's words; the writer (compact.hip) and the reader (hints.hip)
-// compute it the same way, and oracle.hint_entry_check restates it.
+// The integrity word of one hint entry (GCK_HINT_VERSION 3): its five header
+// words and its key's 4-byte little-endian words k(i) (the last one zero past
+// the key) folded by h = (h ^ w) * K + i, then one finaliser.  Every step is
+// a bijection of h, so a change in any one word always changes the word.
+// Each index entry of a hint file holds the XOR of its block's words; the
+// writer (compact.hip) and the reader (hints.hip) compute it the same way, and
+// oracle.hint_entry_check restates it.
 template <class Words>
 __device__ __forceinline__ uint64_t hint_entry_check(uint32_t ts, uint32_t ks, uint32_t vs, uint32_t vpos,
                                                      uint32_t crc, const Words &k) {
+    constexpr uint64_t K = 0x9E3779B97F4A7C15ull;  // odd
     uint64_t h = 0x2545F4914F6CDD1Dull ^ ((uint64_t)ks << 32);
-    h = mix64d(h ^ ts) + 1;
-    h = mix64d(h ^ vs) + 2;
-    h = mix64d(h ^ vpos) + 3;
-    h = mix64d(h ^ crc) + 4;
-    for (uint32_t i = 0; 4 * i < ks; ++i) h = mix64d(h ^ k(i)) + 5 + i;
+    h = (h ^ ts) * K + 1;
+    h = (h ^ vs) * K + 2;
+    h = (h ^ vpos) * K + 3;
+    h = (h ^ crc) * K + 4;
+    for (uint32_t i = 0; 4 * i < ks; ++i) h = (h ^ k(i)) * K + 5 + i;
     return mix64d(h);
 }
 

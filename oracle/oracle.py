@@ -297,16 +297,18 @@ def _mix64(x):
 
 def hint_entry_check(ts, key, value_size, value_pos, crc):
     """The integrity word of one hint entry (gck_internal.h hint_entry_check,
-    restated): a mix of its header words and its key's 4-byte little-endian
-    words, the last one zero past the key.  Each index entry holds the XOR of
-    its block's words."""
+    restated): its header words and its key's 4-byte little-endian words (the
+    last one zero past the key) folded by h = (h ^ w) * K + i mod 2^64, then
+    splitmix64's finaliser.  Each index entry holds the XOR of its block's
+    words."""
+    K = 0x9E3779B97F4A7C15
     ks = len(key)
     h = 0x2545F4914F6CDD1D ^ (ks << 32)
     for i, w in enumerate((ts, value_size, value_pos, crc)):
-        h = (_mix64(h ^ w) + i + 1) & _M64
+        h = ((h ^ w) * K + i + 1) & _M64
     padded = key + bytes(-ks % 4)
     for i in range(0, ks, 4):
-        h = (_mix64(h ^ int.from_bytes(padded[i:i + 4], "little")) + 5 + i // 4) & _M64
+        h = ((h ^ int.from_bytes(padded[i:i + 4], "little")) * K + 5 + i // 4) & _M64
     return _mix64(h)
 
 
